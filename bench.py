@@ -1,0 +1,135 @@
+#!/usr/bin/env python
+"""Headline benchmark: training tokens/s of a PyTorchJob-style Llama-3-8B DDP job.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 it is
+launched by torchrun (one rank per GPU, RCCL over xGMI).  W untimed warmup steps, then
+exactly K timed steps bracketed by barrier + device synchronize on both sides; the MAX
+elapsed time over ranks is used; rank 0 prints ONE JSON line.
+
+Workload: full Llama-3-8B architecture (32 layers, hidden 4096, GQA 32/8, FFN 14336,
+vocab 128256), random init, synthetic tokens, bf16 compute with fp32 master weights and
+AdamW (grad clipping on), seq_len 8192, per-GPU micro-batch ``--micro-batch`` sequences
+x ``--grad-accum`` accumulation steps.  Weak scaling: per-GPU work is fixed as N grows.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from service_account_auth_improvements_amd.ops import set_attention_backend  # noqa: E402
+from service_account_auth_improvements_amd.parallel.state import init_distributed  # noqa: E402
+from service_account_auth_improvements_amd.runtime.trainer import (SyntheticData, TrainConfig,  # noqa: E402
+                                                                   Trainer)
+
+BASELINE_METRIC = "tokens/sec PyTorchJob Llama-3-8B DDP at 1/2/4/8 MI355X; CRD-to-first-step p50"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--seq-len", type=int, default=8192)
+    ap.add_argument("--micro-batch", type=int, default=1)
+    ap.add_argument("--grad-accum", type=int, default=1)
+    ap.add_argument("--zero1", action="store_true", help="ZeRO-1 (reduce-scatter + sharded AdamW)")
+    ap.add_argument("--bucket-mb", type=int, default=256)
+    ap.add_argument("--attn", default="hip", choices=["hip", "sdpa"])
+    ap.add_argument("--layers", type=int, default=None, help="DEBUG ONLY: invalid for reporting")
+    ap.add_argument("--json-out", default=None)
+    a = ap.parse_args()
+
+    set_attention_backend(a.attn)
+    st = init_distributed(tp=1, pp=1)
+    world = st.world_size
+    if world != a.gpus and st.rank == 0:
+        print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    tcfg = TrainConfig(model=a.model, seq_len=a.seq_len, micro_batch=a.micro_batch,
+                       grad_accum=a.grad_accum, zero1=a.zero1, bucket_mb=a.bucket_mb,
+                       n_layers=a.layers)
+    t0 = time.time()
+    tr = Trainer(tcfg, st)
+    data = SyntheticData(tr.mcfg.vocab_size, a.micro_batch, a.seq_len, st.device, seed=1,
+                         rank=st.rank)
+    batches = [[data.next() for _ in range(a.grad_accum)] for _ in range(2)]
+    if st.device.type == "cuda":
+        torch.cuda.synchronize()
+    init_s = time.time() - t0
+
+    losses = []
+    for i in range(a.warmup):
+        losses.append(tr.train_step(batches[i % 2]))
+    if dist.is_initialized():
+        dist.barrier()
+    if st.device.type == "cuda":
+        torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for i in range(a.steps):
+        losses.append(tr.train_step(batches[i % 2]))
+    if st.device.type == "cuda":
+        torch.cuda.synchronize()
+    if dist.is_initialized():
+        dist.barrier()
+    el = time.perf_counter() - t1
+    el_t = torch.tensor([el], dtype=torch.float64, device=st.device)
+    if dist.is_initialized():
+        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
+    el = float(el_t)
+    tok_rank = tr.tokens_per_step
+    value = world * tok_rank * a.steps / el
+    peak_mem = torch.cuda.max_memory_allocated() / 2**30 if st.device.type == "cuda" else 0.0
+    flops_tok = tr.mcfg.flops_per_token(a.seq_len)
+    if st.rank == 0:
+        out = {
+            "metric": BASELINE_METRIC,
+            "value": round(value, 1),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(el / a.steps * 1e3, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (random token ids, random-init weights)",
+            "config": {
+                "model": "Llama-3-8B" if a.model == "llama3-8b" else a.model,
+                "global_batch": world * a.micro_batch * a.grad_accum,
+                "seq_len": a.seq_len,
+                "parallelism": f"dp{world}" + ("-zero1" if a.zero1 else ""),
+                "micro_batch": a.micro_batch,
+                "grad_accum": a.grad_accum,
+                "n_layers": tr.mcfg.n_layers,
+                "attention": a.attn,
+            },
+            "tokens_per_s_per_gpu": round(value / world, 1),
+            "model_tflops_per_gpu": round(value / world * flops_tok / 1e12, 1),
+            "peak_mem_gib": round(peak_mem, 1),
+            "init_s": round(init_s, 1),
+            "loss_first": round(float(losses[0]), 4),
+            "loss_last": round(float(losses[-1]), 4),
+        }
+        if a.layers is not None:
+            out["INVALID"] = "reduced layer count (debug run)"
+        line = json.dumps(out)
+        print(line, flush=True)
+        if a.json_out:
+            with open(a.json_out, "w") as f:
+                f.write(line + "\n")
+    if dist.is_initialized():
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,358 @@
+"""Llama-3 decoder (8B / 70B shapes) with an explicit, autograd-free training step.
+
+Design (MI355X-first):
+
+* Activations are 2-D ``[T, hidden]`` bf16 (T = micro_batch * seq).  Per layer there are
+  exactly four GEMMs (hipBLASLt): fused QKV, O, fused gate/up, down -- and the rest is
+  hand-written gfx950 kernels: fused residual-add+RMSNorm (K1), in-place RoPE on the fused
+  QKV buffer (K2), flash attention reading q/k/v straight out of that buffer (K3), SwiGLU
+  (K4), fused CE with in-place gradient (K5); AdamW (K6) runs over the flat buffers.
+* The residual add is deferred into the next RMSNorm: a layer maps (r, d) -> (h2, d_mlp)
+  with h1 = r + d computed inside the norm kernel, so no stand-alone add kernel exists.
+* Forward and backward are explicit (no autograd graph): ``layer_fwd`` returns a context
+  of saved tensors, ``layer_bwd`` consumes it.  Weight gradients are written by the
+  backward GEMMs straight into their slice of the flat gradient buffer (``out=`` for the
+  first micro-batch, ``addmm_`` with beta=1 afterwards) and the DP engine is told the
+  moment each layer's slice is final, so its bucket all-reduce overlaps the remaining
+  backward.
+* Tensor parallelism (Megatron column/row split, vocab-parallel embedding / LM head / CE)
+  is built in: local head counts and FFN width are the global ones divided by ``tp``; the
+  two per-layer reductions go through RCCL over xGMI.
+* 288 GB of HBM per GPU means no activation recomputation is needed for 8B at 8k tokens
+  per micro-batch (~1.1 GB of saved activations per layer): everything is kept resident.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, replace
+from typing import Callable, List, Optional
+
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+
+from .. import ops
+from ..ops.attention import attention_bwd, attention_fwd
+from ..parallel.state import ParallelState, get_state, tp_all_reduce
+from ..runtime.flat import FlatGroup
+
+
+@dataclass
+class LlamaConfig:
+    name: str = "llama3-8b"
+    vocab_size: int = 128256
+    hidden: int = 4096
+    n_layers: int = 32
+    n_heads: int = 32
+    n_kv_heads: int = 8
+    head_dim: int = 128
+    ffn: int = 14336
+    rope_theta: float = 500000.0
+    norm_eps: float = 1e-5
+    max_seq: int = 8192
+    init_std: float = 0.02
+
+    @staticmethod
+    def preset(name: str) -> "LlamaConfig":
+        name = name.lower()
+        if name in ("llama3-8b", "llama-3-8b", "8b"):
+            return LlamaConfig()
+        if name in ("llama3-70b", "llama-3-70b", "70b"):
+            return LlamaConfig(name="llama3-70b", hidden=8192, n_layers=80, n_heads=64,
+                               n_kv_heads=8, ffn=28672)
+        if name in ("tiny", "llama3-tiny"):
+            return LlamaConfig(name="llama3-tiny", vocab_size=512, hidden=256, n_layers=2,
+                               n_heads=4, n_kv_heads=2, head_dim=64, ffn=512, max_seq=256)
+        if name in ("small", "llama3-small"):
+            return LlamaConfig(name="llama3-small", vocab_size=32000, hidden=1024, n_layers=4,
+                               n_heads=8, n_kv_heads=2, head_dim=128, ffn=3584, max_seq=2048)
+        raise ValueError(f"unknown preset {name}")
+
+    def with_(self, **kw) -> "LlamaConfig":
+        return replace(self, **kw)
+
+    def num_params(self) -> int:
+        H, F_, V, L = self.hidden, self.ffn, self.vocab_size, self.n_layers
+        qkv = H * (self.n_heads + 2 * self.n_kv_heads) * self.head_dim
+        o = self.n_heads * self.head_dim * H
+        per_layer = qkv + o + 3 * H * F_ + 2 * H
+        return L * per_layer + 2 * V * H + H
+
+    def flops_per_token(self, seq: int) -> float:
+        """Training FLOPs/token: 6*N_matmul + causal attention (fwd+bwd = 3x fwd)."""
+        H, L = self.hidden, self.n_layers
+        n_mm = self.num_params() - self.vocab_size * H - (2 * L + 1) * H  # no embed gather, no norms
+        attn = 3 * 2 * 2 * self.n_heads * self.head_dim * seq / 2 * L   # causal: half of S^2
+        return 6 * n_mm + attn
+
+
+class _LayerCtx:
+    __slots__ = ("h1", "rstd1", "a", "qkv", "o", "lse", "h2", "rstd2", "m", "gu", "s")
+
+
+class Llama:
+    """One pipeline stage (all layers when pp == 1) of a Llama-3 model shard."""
+
+    def __init__(self, cfg: LlamaConfig, st: Optional[ParallelState] = None, device=None,
+                 layer_range: Optional[range] = None, seed: int = 1234, full_init: bool = False):
+        self.cfg = cfg
+        self.st = st or get_state()
+        tp = self.st.tp
+        assert cfg.n_heads % tp == 0 and cfg.n_kv_heads % tp == 0 and cfg.ffn % tp == 0
+        assert cfg.vocab_size % tp == 0
+        self.tp = tp
+        self.hq = cfg.n_heads // tp
+        self.hkv = cfg.n_kv_heads // tp
+        self.ff = cfg.ffn // tp
+        self.vl = cfg.vocab_size // tp
+        self.vstart = self.st.tp_rank * self.vl
+        self.device = torch.device(device) if device is not None else self.st.device
+        self.layers = list(layer_range if layer_range is not None else range(cfg.n_layers))
+        self.first = self.layers[0] == 0 if self.layers else self.st.is_first_stage
+        self.last = (self.layers[-1] == cfg.n_layers - 1) if self.layers else self.st.is_last_stage
+        H, D = cfg.hidden, cfg.head_dim
+        self.qkv_w = (self.hq + 2 * self.hkv) * D
+        # ---- parameter registration in reverse execution order (see runtime/flat.py)
+        mats, norms = FlatGroup("matrices"), FlatGroup("norms")
+        if self.last:
+            mats.add("lm_head", (self.vl, H), std=cfg.init_std)
+            norms.add("final_norm", (H,), init="ones", decay=False)
+        out_std = cfg.init_std / math.sqrt(2 * cfg.n_layers)
+        for i in reversed(self.layers):
+            mats.add(f"l{i}.wd", (H, self.ff), std=out_std)
+            mats.add(f"l{i}.wgu", (2 * self.ff, H), std=cfg.init_std)
+            mats.add(f"l{i}.wo", (H, self.hq * D), std=out_std)
+            mats.add(f"l{i}.wqkv", (self.qkv_w, H), std=cfg.init_std)
+            norms.add(f"l{i}.norm2", (H,), init="ones", decay=False)
+            norms.add(f"l{i}.norm1", (H,), init="ones", decay=False)
+        if self.first:
+            mats.add("embed", (self.vl, H), std=cfg.init_std)
+        self.mats, self.norms = mats, norms
+        self.groups = [mats, norms]
+        self._full_init = full_init
+        self._seed = seed
+        self.on_grad_ready: Optional[Callable[[FlatGroup, int], None]] = None
+        cos, sin = ops.rope_tables(cfg.max_seq, D, cfg.rope_theta)
+        self.cos = cos.to(self.device)
+        self.sin = sin.to(self.device)
+
+    # ------------------------------------------------------------------ storage
+    def allocate(self, pad_to: int = 1):
+        for g in self.groups:
+            g.allocate(self.device, pad_to=pad_to)
+        self._init()
+        return self
+
+    def _tp_slicers(self):
+        """Map each TP-sharded tensor to (full_shape, slicer) so every TP degree draws the
+        same full matrix (exact TP==1 equivalence in tests)."""
+        cfg, r, tp = self.cfg, self.st.tp_rank, self.tp
+        H, D, F_, V = cfg.hidden, cfg.head_dim, cfg.ffn, cfg.vocab_size
+        Hq, Hkv = cfg.n_heads, cfg.n_kv_heads
+        out = {}
+
+        def rows(lo, hi):
+            return lambda t: t[lo:hi]
+
+        for i in self.layers:
+            def qkv_slice(t, r=r):
+                q = t[:Hq * D].view(Hq, D, H)[r * self.hq:(r + 1) * self.hq].reshape(-1, H)
+                k = t[Hq * D:(Hq + Hkv) * D].view(Hkv, D, H)[r * self.hkv:(r + 1) * self.hkv].reshape(-1, H)
+                v = t[(Hq + Hkv) * D:].view(Hkv, D, H)[r * self.hkv:(r + 1) * self.hkv].reshape(-1, H)
+                return torch.cat([q, k, v], 0)
+
+            def gu_slice(t, r=r):
+                return torch.cat([t[r * self.ff:(r + 1) * self.ff], t[F_ + r * self.ff:F_ + (r + 1) * self.ff]], 0)
+
+            out[f"l{i}.wqkv"] = ((( Hq + 2 * Hkv) * D, H), qkv_slice)
+            out[f"l{i}.wo"] = ((H, Hq * D), lambda t, r=r: t[:, r * self.hq * D:(r + 1) * self.hq * D])
+            out[f"l{i}.wgu"] = ((2 * F_, H), gu_slice)
+            out[f"l{i}.wd"] = ((H, F_), lambda t, r=r: t[:, r * self.ff:(r + 1) * self.ff])
+        if self.first:
+            out["embed"] = ((V, H), rows(r * self.vl, (r + 1) * self.vl))
+        if self.last:
+            out["lm_head"] = ((V, H), rows(r * self.vl, (r + 1) * self.vl))
+        return out
+
+    def _init(self):
+        full = self._tp_slicers() if self._full_init else None
+        for g in self.groups:
+            g.init_(self._seed, full)
+
+    def P(self, name):
+        g = self.mats if name in self.mats._index else self.norms
+        return g.param(name)
+
+    def G(self, name):
+        g = self.mats if name in self.mats._index else self.norms
+        return g.grad(name)
+
+    def _ready(self, group: FlatGroup, name: str):
+        if self.on_grad_ready is not None:
+            self.on_grad_ready(group, group.end_offset(name))
+
+    @staticmethod
+    def _mm_into(out, a, b, accumulate):
+        if accumulate:
+            out.addmm_(a, b)
+        else:
+            torch.mm(a, b, out=out)
+
+    # ------------------------------------------------------------------ embedding
+    def embed_fwd(self, tokens: torch.Tensor) -> torch.Tensor:
+        E = self.P("embed")
+        if self.tp == 1:
+            return F.embedding(tokens, E)
+        loc = tokens - self.vstart
+        mask = (loc >= 0) & (loc < self.vl)
+        x = F.embedding(loc.clamp(0, self.vl - 1), E) * mask.unsqueeze(-1).to(E.dtype)
+        return tp_all_reduce(x, self.st)
+
+    def embed_bwd(self, tokens: torch.Tensor, g: torch.Tensor, accumulate: bool):
+        idx = tokens
+        if self.tp > 1:
+            loc = tokens - self.vstart
+            mask = (loc >= 0) & (loc < self.vl)
+            idx = loc.clamp(0, self.vl - 1)
+            g = g * mask.unsqueeze(-1).to(g.dtype)
+        gE = torch.ops.aten.embedding_dense_backward(g, idx, self.vl, -1, False)
+        dst = self.G("embed")
+        if accumulate:
+            dst.add_(gE)
+        else:
+            dst.copy_(gE)
+        self._ready(self.mats, "embed")
+
+    # ------------------------------------------------------------------ decoder layer
+    def layer_fwd(self, i: int, r: torch.Tensor, d: Optional[torch.Tensor], B: int, S: int):
+        cfg = self.cfg
+        c = _LayerCtx()
+        a, h1, rstd1 = ops.rmsnorm_fwd(r, self.P(f"l{i}.norm1"), cfg.norm_eps, residual=d)
+        qkv = torch.mm(a, self.P(f"l{i}.wqkv").t())
+        ops.rope_(qkv, self.hq + self.hkv, cfg.head_dim, self.cos, self.sin, seq_len=S)
+        o, lse = attention_fwd(qkv, B, S, self.hq, self.hkv, cfg.head_dim)
+        da = tp_all_reduce(torch.mm(o, self.P(f"l{i}.wo").t()), self.st)
+        m, h2, rstd2 = ops.rmsnorm_fwd(h1, self.P(f"l{i}.norm2"), cfg.norm_eps, residual=da)
+        del da
+        gu = torch.mm(m, self.P(f"l{i}.wgu").t())
+        s = ops.swiglu_fwd(gu)
+        dm = tp_all_reduce(torch.mm(s, self.P(f"l{i}.wd").t()), self.st)
+        c.h1, c.rstd1, c.a, c.qkv, c.o, c.lse = h1, rstd1, a, qkv, o, lse
+        c.h2, c.rstd2, c.m, c.gu, c.s = h2, rstd2, m, gu, s
+        return h2, dm, c
+
+    def layer_bwd(self, i: int, c: _LayerCtx, g: torch.Tensor, B: int, S: int, accumulate: bool):
+        cfg = self.cfg
+        Wd, Wgu, Wo, Wqkv = (self.P(f"l{i}.{n}") for n in ("wd", "wgu", "wo", "wqkv"))
+        # MLP
+        gs = torch.mm(g, Wd)
+        self._mm_into(self.G(f"l{i}.wd"), g.t(), c.s, accumulate)
+        c.s = None
+        dgu = ops.swiglu_bwd(c.gu, gs)
+        del gs
+        c.gu = None
+        dmm = tp_all_reduce(torch.mm(dgu, Wgu), self.st)
+        self._mm_into(self.G(f"l{i}.wgu"), dgu.t(), c.m, accumulate)
+        del dgu
+        dh2 = ops.rmsnorm_bwd(dmm, c.h2, c.rstd2, self.P(f"l{i}.norm2"), self.G(f"l{i}.norm2"),
+                              accumulate, dres=g)
+        del dmm
+        # attention
+        do = torch.mm(dh2, Wo)
+        self._mm_into(self.G(f"l{i}.wo"), dh2.t(), c.o, accumulate)
+        dqkv = attention_bwd(c.qkv, c.o, c.lse, do, B, S, self.hq, self.hkv, cfg.head_dim)
+        del do
+        ops.rope_(dqkv, self.hq + self.hkv, cfg.head_dim, self.cos, self.sin, seq_len=S, inverse=True)
+        da = tp_all_reduce(torch.mm(dqkv, Wqkv), self.st)
+        self._mm_into(self.G(f"l{i}.wqkv"), dqkv.t(), c.a, accumulate)
+        del dqkv
+        dh1 = ops.rmsnorm_bwd(da, c.h1, c.rstd1, self.P(f"l{i}.norm1"), self.G(f"l{i}.norm1"),
+                              accumulate, dres=dh2)
+        self._ready(self.mats, f"l{i}.wqkv")
+        return dh1
+
+    # ------------------------------------------------------------------ LM head + CE
+    def head_fwd(self, r, d, labels: torch.Tensor, scale: float):
+        """Returns (loss_sum fp32 0-d tensor already multiplied by scale, ctx)."""
+        cfg = self.cfg
+        y, h, rstd = ops.rmsnorm_fwd(r, self.P("final_norm"), cfg.norm_eps, residual=d)
+        logits = torch.mm(y, self.P("lm_head").t())
+        if self.tp == 1:
+            loss_rows, _ = ops.cross_entropy_fused_(logits, labels, scale)
+        else:
+            m, s, xy = ops.cross_entropy_stats(logits, labels, self.vstart)
+            M = m.clone()
+            dist.all_reduce(M, op=dist.ReduceOp.MAX, group=self.st.tp_group)
+            s = s * torch.exp(m - M)
+            sx = torch.stack([s, xy])
+            dist.all_reduce(sx, group=self.st.tp_group)
+            lse = M + torch.log(sx[0])
+            loss_rows = torch.where(labels != -100, lse - sx[1], torch.zeros_like(lse))
+            ops.cross_entropy_grad_(logits, labels, lse, scale, self.vstart)
+        loss = loss_rows.sum() * scale
+        return loss, (h, rstd, y, logits)
+
+    def head_bwd(self, ctx, accumulate: bool):
+        h, rstd, y, dlogits = ctx
+        dy = tp_all_reduce(torch.mm(dlogits, self.P("lm_head")), self.st)
+        self._mm_into(self.G("lm_head"), dlogits.t(), y, accumulate)
+        self._ready(self.mats, "lm_head")
+        dh = ops.rmsnorm_bwd(dy, h, rstd, self.P("final_norm"), self.G("final_norm"), accumulate)
+        return dh
+
+    # ------------------------------------------------------------------ stage-level API
+    def stage_forward(self, inp, B: int, S: int, labels=None, scale: float = 1.0):
+        """inp: tokens [B*S] (first stage) or activation [B*S, H].  Returns (out, ctx) where
+        out is the loss (last stage) or the activation handed to the next stage."""
+        ctx = {"layers": []}
+        if self.first:
+            ctx["tokens"] = inp
+            r, d = self.embed_fwd(inp), None
+        else:
+            r, d = inp, None
+        for i in self.layers:
+            r, d, c = self.layer_fwd(i, r, d, B, S)
+            ctx["layers"].append(c)
+        if self.last:
+            loss, hctx = self.head_fwd(r, d, labels, scale)
+            ctx["head"] = hctx
+            return loss, ctx
+        out = r + d if d is not None else r
+        return out, ctx
+
+    def stage_backward(self, ctx, grad_out: Optional[torch.Tensor], B: int, S: int,
+                       accumulate: bool):
+        """grad_out: None on the last stage (loss), else d(out).  Returns d(inp) or None."""
+        if self.last:
+            g = self.head_bwd(ctx.pop("head"), accumulate)
+        else:
+            g = grad_out
+        layers = ctx["layers"]
+        for i in reversed(self.layers):
+            c = layers.pop()
+            g = self.layer_bwd(i, c, g, B, S, accumulate)
+            del c
+        if self.first:
+            self.embed_bwd(ctx["tokens"], g, accumulate)
+            return None
+        return g
+
+    def forward_backward(self, tokens: torch.Tensor, labels: torch.Tensor, accumulate: bool = False,
+                         scale: Optional[float] = None):
+        """Single-stage fused step: tokens/labels [B, S] -> loss (device scalar); grads
+        written into the flat gradient buffers."""
+        B, S = tokens.shape
+        scale = scale if scale is not None else 1.0 / (B * S)
+        loss, ctx = self.stage_forward(tokens.reshape(-1), B, S, labels.reshape(-1), scale)
+        self.stage_backward(ctx, None, B, S, accumulate)
+        return loss
+
+    @torch.no_grad()
+    def forward_logits(self, tokens: torch.Tensor) -> torch.Tensor:
+        """Plain forward to logits [B, S, V_local] (evaluation / tests)."""
+        B, S = tokens.shape
+        r, d = self.embed_fwd(tokens.reshape(-1)), None
+        for i in self.layers:
+            r, d, _ = self.layer_fwd(i, r, d, B, S)
+        y, _, _ = ops.rmsnorm_fwd(r, self.P("final_norm"), self.cfg.norm_eps, residual=d)
+        return torch.mm(y, self.P("lm_head").t()).view(B, S, -1)

@@ -1,0 +1,191 @@
+"""Hot-path kernels of the worker runtime.
+
+Raw (non-autograd) entry points take and return plain tensors; GPU tensors run the
+hand-written gfx950 HIP kernels (``torch.ops.kfamd``), CPU tensors run the fp32
+references in :mod:`.reference`.  There is no GPU-side fallback: if the HIP library
+cannot be loaded on a GPU box these functions raise.
+
+Autograd wrappers (``rmsnorm``, ``swiglu``, ``attention``, ...) are provided for users
+composing their own models; the Llama runtime uses the raw entry points inside its
+fused per-layer autograd functions.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _ext, reference
+from .attention import (attention, attention_bwd, attention_fwd, decode_attention,  # noqa: F401
+                        set_attention_backend, get_attention_backend)
+
+
+def _k():
+    return _ext.ops()
+
+
+# ---------------------------------------------------------------- RMSNorm (K1)
+def rmsnorm_fwd(a, w, eps, residual=None):
+    """y = rmsnorm(a [+ residual]) * w. Returns (y, h, rstd); h is the summed residual
+    stream (== a when residual is None)."""
+    if a.is_cuda:
+        y, h, rstd = _k().rmsnorm_fwd(a, residual, w, eps)
+    else:
+        y, h, rstd = reference.rmsnorm_fwd(a, residual, w, eps)
+    if residual is None:
+        h = a
+    return y, h, rstd
+
+
+def rmsnorm_bwd(dy, h, rstd, w, dw_out, accumulate=False, dres=None):
+    """Returns dh (+ dres); writes (or accumulates) dw into ``dw_out``."""
+    if dy.is_cuda:
+        return _k().rmsnorm_bwd(dy.contiguous(), h, rstd, w, dres, dw_out, accumulate)
+    dh, dw = reference.rmsnorm_bwd(dy, h, rstd, w, dres)
+    if accumulate:
+        dw_out.add_(dw.to(dw_out.dtype))
+    else:
+        dw_out.copy_(dw)
+    return dh
+
+
+# ---------------------------------------------------------------- RoPE (K2)
+def rope_(x, nheads, head_dim, cos_t, sin_t, seq_len=None, pos=None, inverse=False):
+    if x.is_cuda:
+        _k().rope_(x, nheads, head_dim, cos_t, sin_t, pos, int(seq_len or 0), inverse)
+        return x
+    return reference.rope_(x, nheads, head_dim, cos_t, sin_t, pos, seq_len, inverse)
+
+
+rope_tables = reference.rope_tables
+
+
+# ---------------------------------------------------------------- SwiGLU (K4)
+def swiglu_fwd(gu):
+    return _k().swiglu_fwd(gu) if gu.is_cuda else reference.swiglu_fwd(gu)
+
+
+def swiglu_bwd(gu, dout):
+    return _k().swiglu_bwd(gu, dout.contiguous()) if gu.is_cuda else reference.swiglu_bwd(gu, dout)
+
+
+# ---------------------------------------------------------------- Cross entropy (K5)
+CE_FUSED, CE_STATS, CE_GRAD = 0, 1, 2
+
+
+def cross_entropy_fused_(logits, labels, scale, ignore_index=-100, vocab_start=0):
+    """Loss rows + in-place gradient. ``scale`` may be a float or a 1-element fp32 device
+    tensor (e.g. 1/num_valid computed on device, avoiding a host sync).
+    Returns (loss_rows fp32 [T], lse fp32 [T]); logits now hold dlogits."""
+    T = logits.shape[0]
+    if logits.is_cuda:
+        loss = torch.empty(T, device=logits.device, dtype=torch.float32)
+        lse = torch.empty_like(loss)
+        st = scale if torch.is_tensor(scale) else None
+        sh = 0.0 if torch.is_tensor(scale) else float(scale)
+        _k().cross_entropy_(logits, labels, vocab_start, ignore_index, st, sh, CE_FUSED, loss, lse,
+                            None, None, None)
+        return loss, lse
+    sc = float(scale) if not torch.is_tensor(scale) else float(scale.reshape(-1)[0])
+    loss, lse, g = reference.cross_entropy(logits, labels - vocab_start if vocab_start else labels,
+                                           ignore_index, sc)
+    logits.copy_(g.to(logits.dtype))
+    return loss, lse
+
+
+def cross_entropy_stats(logits, labels, vocab_start, ignore_index=-100):
+    """Per-row (max, sumexp, target-logit-or-0) of one vocab shard (TP)."""
+    T, V = logits.shape
+    if logits.is_cuda:
+        f = dict(device=logits.device, dtype=torch.float32)
+        m, s, xy = torch.empty(T, **f), torch.empty(T, **f), torch.empty(T, **f)
+        dummy = torch.empty(T, **f)
+        _k().cross_entropy_(logits, labels, vocab_start, ignore_index, None, 0.0, CE_STATS, dummy,
+                            dummy, m, s, xy)
+        return m, s, xy
+    lf = logits.float()
+    m = lf.max(-1).values
+    s = (lf - m.unsqueeze(1)).exp().sum(-1)
+    loc = labels - vocab_start
+    inr = (loc >= 0) & (loc < V)
+    xy = torch.where(inr, lf.gather(1, loc.clamp(0, V - 1).unsqueeze(1)).squeeze(1),
+                     torch.zeros_like(m))
+    return m, s, xy
+
+
+def cross_entropy_grad_(logits, labels, lse, scale, vocab_start, ignore_index=-100):
+    """Write the shard's dlogits in place given the GLOBAL log-sum-exp."""
+    T, V = logits.shape
+    if logits.is_cuda:
+        st = scale if torch.is_tensor(scale) else None
+        sh = 0.0 if torch.is_tensor(scale) else float(scale)
+        dummy = torch.empty(T, device=logits.device, dtype=torch.float32)
+        _k().cross_entropy_(logits, labels, vocab_start, ignore_index, st, sh, CE_GRAD, dummy,
+                            lse.contiguous(), None, None, None)
+        return logits
+    sc = float(scale) if not torch.is_tensor(scale) else float(scale.reshape(-1)[0])
+    p = (logits.float() - lse.unsqueeze(1)).exp()
+    loc = labels - vocab_start
+    inr = (loc >= 0) & (loc < V) & (labels != ignore_index)
+    rows = torch.arange(T, device=logits.device)[inr]
+    p[rows, loc[inr]] -= 1.0
+    p = p * sc
+    p[labels == ignore_index] = 0
+    logits.copy_(p.to(logits.dtype))
+    return logits
+
+
+# ---------------------------------------------------------------- AdamW (K6)
+def adamw_(p, w, m, v, g, n_decay, lr, b1, b2, eps, wd, step, gscale=1.0, sumsq=None,
+           max_norm=0.0):
+    if p.is_cuda:
+        _k().adamw_(p, w, m, v, g, int(n_decay), lr, b1, b2, eps, wd, int(step), gscale, sumsq,
+                    max_norm)
+    else:
+        reference.adamw_(p, w, m, v, g, n_decay, lr, b1, b2, eps, wd, step, gscale,
+                         None if sumsq is None else float(sumsq.reshape(-1)[0]), max_norm)
+
+
+def sumsq_(g, out, accumulate=False):
+    """out[0] (+)= sum(g^2) (fp32, deterministic)."""
+    if g.is_cuda:
+        _k().sumsq(g, out, accumulate)
+    else:
+        s = g.float().pow(2).sum()
+        out.copy_(out + s if accumulate else s.reshape(out.shape))
+    return out
+
+
+# ---------------------------------------------------------------- autograd wrappers
+class _RMSNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, eps):
+        y, h, rstd = rmsnorm_fwd(x.contiguous(), w, eps)
+        ctx.save_for_backward(h, rstd, w)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        h, rstd, w = ctx.saved_tensors
+        dw = torch.empty_like(w)
+        dh = rmsnorm_bwd(dy.contiguous(), h, rstd, w, dw)
+        return dh, dw, None
+
+
+def rmsnorm(x, w, eps=1e-5):
+    return _RMSNormFn.apply(x, w, eps)
+
+
+class _SwiGLUFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, gu):
+        gu = gu.contiguous()
+        ctx.save_for_backward(gu)
+        return swiglu_fwd(gu)
+
+    @staticmethod
+    def backward(ctx, d):
+        (gu,) = ctx.saved_tensors
+        return swiglu_bwd(gu, d)
+
+
+def swiglu(gu):
+    return _SwiGLUFn.apply(gu)

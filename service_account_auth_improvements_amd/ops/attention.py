@@ -1,0 +1,114 @@
+"""K3/K8: causal GQA attention on the fused QKV activation.
+
+The Llama block keeps q, k and v inside one [T, (Hq + 2*Hkv) * D] bf16 buffer (one QKV
+GEMM, RoPE in place).  The gfx950 flash kernels read q/k/v straight out of that buffer
+with its row stride, so no transpose/copy to [B, H, S, D] is ever made, and write the
+output as [T, Hq*D] -- exactly the operand the O-projection GEMM wants.
+
+Backends:
+  * ``hip``  -- hand-written MFMA flash attention (ops/csrc/flash_attn.hip); the default.
+  * ``sdpa`` -- torch SDPA (AOTriton on ROCm); kept only as a measured baseline to beat.
+  * CPU tensors always use the fp32 reference.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from . import _ext, reference
+
+_BACKEND = "sdpa"  # flipped to "hip" once flash_attn.hip lands
+
+
+def set_attention_backend(name: str) -> None:
+    global _BACKEND
+    assert name in ("hip", "sdpa"), name
+    _BACKEND = name
+
+
+def get_attention_backend() -> str:
+    return _BACKEND
+
+
+def _split(qkv, B, S, Hq, Hkv, D):
+    q = qkv[:, : Hq * D].reshape(B, S, Hq, D).transpose(1, 2)
+    k = qkv[:, Hq * D:(Hq + Hkv) * D].reshape(B, S, Hkv, D).transpose(1, 2)
+    v = qkv[:, (Hq + Hkv) * D:(Hq + 2 * Hkv) * D].reshape(B, S, Hkv, D).transpose(1, 2)
+    return q, k, v
+
+
+def attention_fwd(qkv, B, S, Hq, Hkv, D, causal=True):
+    """Returns (o [T, Hq*D] bf16, lse [B, Hq, S] fp32)."""
+    scale = 1.0 / math.sqrt(D)
+    if qkv.is_cuda and _BACKEND == "hip":
+        return _ext.ops().flash_fwd(qkv, B, S, Hq, Hkv, D, scale, causal)
+    q, k, v = _split(qkv, B, S, Hq, Hkv, D)
+    if qkv.is_cuda:  # sdpa baseline
+        o = F.scaled_dot_product_attention(q, k, v, is_causal=causal, enable_gqa=True)
+        lse = torch.empty(B, Hq, S, device=qkv.device, dtype=torch.float32)
+    else:
+        o, lse = reference.attention(q, k, v, causal, scale)
+        o = o.to(qkv.dtype)
+    return o.transpose(1, 2).reshape(B * S, Hq * D), lse
+
+
+def attention_bwd(qkv, o, lse, do, B, S, Hq, Hkv, D, causal=True):
+    """Returns dqkv [T, (Hq + 2*Hkv)*D] in the fused layout."""
+    scale = 1.0 / math.sqrt(D)
+    if qkv.is_cuda and _BACKEND == "hip":
+        return _ext.ops().flash_bwd(qkv, o, lse, do.contiguous(), B, S, Hq, Hkv, D, scale, causal)
+    # baseline / CPU: recompute through autograd
+    with torch.enable_grad():
+        x = qkv.detach().requires_grad_(True)
+        q, k, v = _split(x, B, S, Hq, Hkv, D)
+        if qkv.is_cuda:
+            oo = F.scaled_dot_product_attention(q, k, v, is_causal=causal, enable_gqa=True)
+        else:
+            oo = reference.attention(q, k, v, causal, scale)[0].to(qkv.dtype)
+        oo = oo.transpose(1, 2).reshape(B * S, Hq * D)
+        (dqkv,) = torch.autograd.grad(oo, x, do)
+    return dqkv
+
+
+class _AttnFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, B, S, Hq, Hkv, D, causal):
+        qkv = qkv.contiguous()
+        o, lse = attention_fwd(qkv, B, S, Hq, Hkv, D, causal)
+        ctx.save_for_backward(qkv, o, lse)
+        ctx.cfg = (B, S, Hq, Hkv, D, causal)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, o, lse = ctx.saved_tensors
+        return (attention_bwd(qkv, o, lse, do, *ctx.cfg),) + (None,) * 6
+
+
+def attention(qkv, B, S, Hq, Hkv, D, causal=True):
+    """Autograd-aware attention over a fused [B*S, (Hq+2Hkv)*D] qkv tensor."""
+    return _AttnFn.apply(qkv, B, S, Hq, Hkv, D, causal)
+
+
+def decode_attention(q, k_cache, v_cache, lengths, scale=None):
+    """Single-query GQA attention over a KV cache (K8, InferenceService decode).
+
+    q [B, Hq, D]; k_cache/v_cache [B, Lmax, Hkv, D]; lengths int32 [B] (valid keys per
+    sequence, including the current token). Returns o [B, Hq, D]."""
+    B, Hq, D = q.shape
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    if q.is_cuda:
+        return _ext.ops().decode_attn(q.contiguous(), k_cache, v_cache, lengths, scale)
+    Hkv = k_cache.shape[2]
+    rep = Hq // Hkv
+    out = torch.empty_like(q)
+    for b in range(B):
+        L = int(lengths[b])
+        k = k_cache[b, :L].float().permute(1, 0, 2).repeat_interleave(rep, 0)  # [Hq, L, D]
+        v = v_cache[b, :L].float().permute(1, 0, 2).repeat_interleave(rep, 0)
+        s = torch.einsum("hd,hld->hl", q[b].float(), k) * scale
+        p = torch.softmax(s, -1)
+        out[b] = torch.einsum("hl,hld->hd", p, v).to(q.dtype)
+    return out

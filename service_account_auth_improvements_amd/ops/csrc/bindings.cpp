@@ -1,0 +1,223 @@
+// Torch operator registrations for the gfx950 kernels (namespace torch.ops.kfamd).
+//
+// The .hip translation units expose plain `extern "C"` launchers taking raw pointers and
+// a hipStream_t; only this file sees libtorch.  Every op launches on the caller's current
+// HIP stream, allocates scratch through the caching allocator (capturable in hipGraphs)
+// and validates shapes/dtypes on the host BEFORE any kernel is launched: a kernel is
+// never started on operands whose shape it does not support.
+#include <torch/library.h>
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPGuard.h>
+#include <hip/hip_runtime.h>
+
+#include <tuple>
+
+extern "C" {
+int kf_rmsnorm_fwd(const void*, const void*, void*, void*, float*, const void*, int, int, float,
+                   hipStream_t);
+int kf_rmsnorm_bwd(const void*, const void*, const float*, const void*, const void*, void*, float*,
+                   int, void*, int, int, int, hipStream_t);
+int kf_rope(void*, long, int, int, int, const float*, const float*, const int*, int, int,
+            hipStream_t);
+int kf_swiglu_fwd(const void*, void*, int, int, hipStream_t);
+int kf_swiglu_bwd(const void*, const void*, void*, int, int, hipStream_t);
+int kf_adamw(void*, float*, float*, float*, const void*, size_t, size_t, float, float, float, float,
+             float, int, float, const float*, float, hipStream_t);
+int kf_sumsq(const void*, size_t, float*, float*, int, hipStream_t);
+int kf_cross_entropy(void*, long, int, int, const long*, long, long, float*, float*, float*, float*,
+                     float*, const float*, float, int, hipStream_t);
+int kf_flash_fwd(const void*, const void*, const void*, void*, float*, int, int, int, int, int, int,
+                 long, long, long, long, float, int, hipStream_t);
+int kf_flash_bwd(const void*, const void*, const void*, const void*, const void*, const float*,
+                 void*, void*, void*, float*, float*, int, int, int, int, int, int, long, long,
+                 long, long, long, long, float, int, hipStream_t);
+int kf_decode_attn(const void*, const void*, const void*, const int*, void*, float*, int, int, int,
+                   int, int, long, long, long, long, float, int, hipStream_t);
+}
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check_bf16_cuda(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bfloat16");
+}
+void check_rc(int rc, const char* op) { TORCH_CHECK(rc == 0, op, ": unsupported shape (rc=", rc, ")"); }
+
+// ---------------- RMSNorm ----------------
+std::tuple<at::Tensor, at::Tensor, at::Tensor> rmsnorm_fwd(const at::Tensor& a,
+                                                           const std::optional<at::Tensor>& b,
+                                                           const at::Tensor& w, double eps) {
+  check_bf16_cuda(a, "a");
+  check_bf16_cuda(w, "w");
+  TORCH_CHECK(a.is_contiguous() && w.is_contiguous(), "rmsnorm: contiguous inputs required");
+  const int64_t H = a.size(-1);
+  TORCH_CHECK(w.numel() == H, "rmsnorm: weight size mismatch");
+  const int64_t rows = a.numel() / H;
+  c10::hip::HIPGuard g(a.device());
+  auto y = at::empty_like(a);
+  auto rstd = at::empty({rows}, a.options().dtype(at::kFloat));
+  at::Tensor h;
+  const void* bp = nullptr;
+  void* hp = nullptr;
+  if (b.has_value()) {
+    check_bf16_cuda(*b, "b");
+    TORCH_CHECK(b->is_contiguous() && b->sizes() == a.sizes(), "rmsnorm: residual shape mismatch");
+    h = at::empty_like(a);
+    bp = b->data_ptr();
+    hp = h.data_ptr();
+  } else {
+    h = at::empty({0}, a.options());
+  }
+  check_rc(kf_rmsnorm_fwd(a.data_ptr(), bp, hp, y.data_ptr(), rstd.data_ptr<float>(), w.data_ptr(),
+                          (int)rows, (int)H, (float)eps, cur_stream()),
+           "rmsnorm_fwd");
+  return {y, h, rstd};
+}
+
+at::Tensor rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& h, const at::Tensor& rstd,
+                       const at::Tensor& w, const std::optional<at::Tensor>& dres, at::Tensor dw,
+                       bool accumulate) {
+  check_bf16_cuda(dy, "dy");
+  check_bf16_cuda(h, "h");
+  check_bf16_cuda(dw, "dw");
+  TORCH_CHECK(dy.is_contiguous() && h.is_contiguous() && dy.sizes() == h.sizes(), "rmsnorm_bwd: shapes");
+  TORCH_CHECK(dw.is_contiguous() && dw.numel() == h.size(-1), "rmsnorm_bwd: dw shape");
+  const int64_t H = h.size(-1), rows = h.numel() / H;
+  TORCH_CHECK(rstd.numel() == rows, "rmsnorm_bwd: rstd shape");
+  c10::hip::HIPGuard g(h.device());
+  auto dh = at::empty_like(h);
+  const void* dr = nullptr;
+  if (dres.has_value()) {
+    TORCH_CHECK(dres->sizes() == h.sizes() && dres->is_contiguous(), "rmsnorm_bwd: dres shape");
+    dr = dres->data_ptr();
+  }
+  int nblocks = (int)std::min<int64_t>(256, (rows + 3) / 4);
+  if (nblocks < 1) nblocks = 1;
+  auto part = at::empty({(int64_t)nblocks * 4, H}, h.options().dtype(at::kFloat));
+  check_rc(kf_rmsnorm_bwd(dy.data_ptr(), h.data_ptr(), rstd.data_ptr<float>(), w.data_ptr(), dr,
+                          dh.data_ptr(), part.data_ptr<float>(), nblocks, dw.data_ptr(),
+                          accumulate ? 1 : 0, (int)rows, (int)H, cur_stream()),
+           "rmsnorm_bwd");
+  return dh;
+}
+
+// ---------------- RoPE (in place) ----------------
+void rope_(at::Tensor x, int64_t nheads, int64_t head_dim, const at::Tensor& cos_t,
+           const at::Tensor& sin_t, const std::optional<at::Tensor>& pos, int64_t seq_len,
+           bool inverse) {
+  check_bf16_cuda(x, "x");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "rope: x must be [T, C] with unit inner stride");
+  TORCH_CHECK(nheads * head_dim <= x.size(1), "rope: heads exceed row");
+  TORCH_CHECK(cos_t.scalar_type() == at::kFloat && sin_t.scalar_type() == at::kFloat &&
+                  cos_t.is_contiguous() && sin_t.is_contiguous() && cos_t.size(-1) == head_dim / 2,
+              "rope: cos/sin must be contiguous fp32 [P, D/2]");
+  const int* pp = nullptr;
+  if (pos.has_value()) {
+    TORCH_CHECK(pos->scalar_type() == at::kInt && pos->numel() == x.size(0), "rope: pos int32 [T]");
+    pp = pos->data_ptr<int>();
+  } else {
+    TORCH_CHECK(seq_len > 0 && seq_len <= cos_t.size(0), "rope: seq_len exceeds table");
+  }
+  c10::hip::HIPGuard g(x.device());
+  check_rc(kf_rope(x.data_ptr(), x.stride(0), (int)x.size(0), (int)nheads, (int)head_dim,
+                   cos_t.data_ptr<float>(), sin_t.data_ptr<float>(), pp, (int)seq_len,
+                   inverse ? 1 : 0, cur_stream()),
+           "rope");
+}
+
+// ---------------- SwiGLU ----------------
+at::Tensor swiglu_fwd(const at::Tensor& gu) {
+  check_bf16_cuda(gu, "gu");
+  TORCH_CHECK(gu.is_contiguous() && gu.size(-1) % 2 == 0, "swiglu: [.., 2F] contiguous");
+  const int64_t F = gu.size(-1) / 2, rows = gu.numel() / gu.size(-1);
+  auto sizes = gu.sizes().vec();
+  sizes.back() = F;
+  c10::hip::HIPGuard g(gu.device());
+  auto out = at::empty(sizes, gu.options());
+  check_rc(kf_swiglu_fwd(gu.data_ptr(), out.data_ptr(), (int)rows, (int)F, cur_stream()), "swiglu_fwd");
+  return out;
+}
+
+at::Tensor swiglu_bwd(const at::Tensor& gu, const at::Tensor& dout) {
+  check_bf16_cuda(gu, "gu");
+  check_bf16_cuda(dout, "dout");
+  const int64_t F = gu.size(-1) / 2, rows = gu.numel() / gu.size(-1);
+  TORCH_CHECK(gu.is_contiguous() && dout.is_contiguous() && dout.numel() == rows * F, "swiglu_bwd: shapes");
+  c10::hip::HIPGuard g(gu.device());
+  auto dgu = at::empty_like(gu);
+  check_rc(kf_swiglu_bwd(gu.data_ptr(), dout.data_ptr(), dgu.data_ptr(), (int)rows, (int)F, cur_stream()),
+           "swiglu_bwd");
+  return dgu;
+}
+
+// ---------------- AdamW (flat) ----------------
+void adamw_(at::Tensor p, at::Tensor w, at::Tensor m, at::Tensor v, const at::Tensor& g,
+            int64_t n_decay, double lr, double b1, double b2, double eps, double wd, int64_t step,
+            double gscale, const std::optional<at::Tensor>& sumsq, double max_norm) {
+  check_bf16_cuda(p, "p");
+  check_bf16_cuda(g, "g");
+  const int64_t n = p.numel();
+  TORCH_CHECK(w.numel() == n && m.numel() == n && v.numel() == n && g.numel() == n, "adamw: sizes");
+  TORCH_CHECK(w.scalar_type() == at::kFloat && m.scalar_type() == at::kFloat && v.scalar_type() == at::kFloat,
+              "adamw: master/m/v must be fp32");
+  TORCH_CHECK(p.is_contiguous() && w.is_contiguous() && m.is_contiguous() && v.is_contiguous() &&
+                  g.is_contiguous(), "adamw: contiguous flat buffers required");
+  const float* sp = nullptr;
+  if (sumsq.has_value()) sp = sumsq->data_ptr<float>();
+  c10::hip::HIPGuard gd(p.device());
+  check_rc(kf_adamw(p.data_ptr(), w.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
+                    g.data_ptr(), (size_t)n, (size_t)n_decay, (float)lr, (float)b1, (float)b2,
+                    (float)eps, (float)wd, (int)step, (float)gscale, sp, (float)max_norm, cur_stream()),
+           "adamw");
+}
+
+void sumsq(const at::Tensor& g, at::Tensor out, bool accumulate) {
+  check_bf16_cuda(g, "g");
+  TORCH_CHECK(g.is_contiguous() && out.scalar_type() == at::kFloat, "sumsq: args");
+  c10::hip::HIPGuard gd(g.device());
+  auto part = at::empty({2048}, g.options().dtype(at::kFloat));
+  check_rc(kf_sumsq(g.data_ptr(), (size_t)g.numel(), part.data_ptr<float>(), out.data_ptr<float>(),
+                    accumulate ? 1 : 0, cur_stream()),
+           "sumsq");
+}
+
+// ---------------- Cross entropy (grad in place) ----------------
+void cross_entropy_(at::Tensor logits, const at::Tensor& labels, int64_t vocab_start,
+                    int64_t ignore_index, const std::optional<at::Tensor>& scale, double scale_h,
+                    int64_t mode, at::Tensor loss, at::Tensor lse, const std::optional<at::Tensor>& sm,
+                    const std::optional<at::Tensor>& ss, const std::optional<at::Tensor>& sxy) {
+  check_bf16_cuda(logits, "logits");
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "ce: logits [T, V]");
+  TORCH_CHECK(labels.scalar_type() == at::kLong && labels.numel() == logits.size(0) && labels.is_contiguous(),
+              "ce: labels int64 [T]");
+  const int64_t rows = logits.size(0);
+  TORCH_CHECK(loss.numel() == rows && lse.numel() == rows && loss.scalar_type() == at::kFloat &&
+                  lse.scalar_type() == at::kFloat, "ce: loss/lse fp32 [T]");
+  float *pm = nullptr, *ps = nullptr, *pxy = nullptr;
+  if (mode == 1) {
+    TORCH_CHECK(sm.has_value() && ss.has_value() && sxy.has_value(), "ce: stats outputs required");
+    pm = sm->data_ptr<float>(); ps = ss->data_ptr<float>(); pxy = sxy->data_ptr<float>();
+  }
+  const float* scp = scale.has_value() ? scale->data_ptr<float>() : nullptr;
+  c10::hip::HIPGuard g(logits.device());
+  check_rc(kf_cross_entropy(logits.data_ptr(), logits.stride(0), (int)rows, (int)logits.size(1),
+                            labels.data_ptr<int64_t>(), vocab_start, ignore_index, loss.data_ptr<float>(),
+                            lse.data_ptr<float>(), pm, ps, pxy, scp, (float)scale_h, (int)mode, cur_stream()),
+           "cross_entropy");
+}
+
+}  // namespace
+
+TORCH_LIBRARY(kfamd, m) {
+  m.def("rmsnorm_fwd", &rmsnorm_fwd);
+  m.def("rmsnorm_bwd", &rmsnorm_bwd);
+  m.def("rope_", &rope_);
+  m.def("swiglu_fwd", &swiglu_fwd);
+  m.def("swiglu_bwd", &swiglu_bwd);
+  m.def("adamw_", &adamw_);
+  m.def("sumsq", &sumsq);
+  m.def("cross_entropy_", &cross_entropy_);
+}

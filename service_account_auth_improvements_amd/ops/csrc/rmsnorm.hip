@@ -1,0 +1,200 @@
+// K1: fused residual-add + RMSNorm forward / backward for gfx950.
+//
+// Layout: rows of H bf16 values (the [T, hidden] activation of a Llama block).
+// One wave64 owns one row: lane l holds 16-byte vectors l, l+64, ... of the row in
+// registers, so the row is read from HBM exactly once in the forward (sum of
+// squares + normalise from registers) and once in the backward.
+//
+//   fwd:  h = a (+ b);  r = rsqrt(mean(h^2) + eps);  y = h * r * w
+//   bwd:  g = dy * w;   dh = r*g - h * r^3 * mean(g*h)  (+ dres);  dw = sum_rows dy*h*r
+//
+// dw is reduced in two steps (per-wave partial rows, then a column reduce kernel)
+// so no float atomics are needed and the result is bitwise reproducible.
+#include "common.h"
+
+using namespace kf;
+
+template <int VPT>
+__global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(
+    const bf16_t* __restrict__ a, const bf16_t* __restrict__ b, bf16_t* __restrict__ h_out,
+    bf16_t* __restrict__ y, float* __restrict__ rstd, const bf16_t* __restrict__ w,
+    int rows, int H, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int nv = H >> 3;
+  const size_t base = (size_t)row * H;
+  float x[VPT][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int v = i * 64 + lane;
+    if (v < nv) {
+      unpack8(ld16(a + base + v * 8), x[i]);
+      if (b) {
+        float t[8];
+        unpack8(ld16(b + base + v * 8), t);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[i][j] += t[j];
+        // round the residual sum to bf16 exactly as it is stored, so fwd/bwd agree
+        u32x4 hv = pack8(x[i]);
+        st16(h_out + base + v * 8, hv);
+        unpack8(hv, x[i]);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += x[i][j] * x[i][j];
+    }
+  }
+  ss = wave_sum(ss);
+  const float r = rsqrtf(ss / (float)H + eps);
+  if (lane == 0) rstd[row] = r;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int v = i * 64 + lane;
+    if (v < nv) {
+      float wf[8], o[8];
+      unpack8(ld16(w + v * 8), wf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = x[i][j] * r * wf[j];
+      st16(y + base + v * 8, pack8(o));
+    }
+  }
+}
+
+template <int VPT>
+__global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ h, const float* __restrict__ rstd,
+    const bf16_t* __restrict__ w, const bf16_t* __restrict__ dres, bf16_t* __restrict__ dh,
+    float* __restrict__ dw_part, int rows, int H) {
+  const int lane = threadIdx.x & 63;
+  const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int nwaves = gridDim.x * 4;
+  const int nv = H >> 3;
+  float wf[VPT][8], dwacc[VPT][8];
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int v = i * 64 + lane;
+    if (v < nv) unpack8(ld16(w + v * 8), wf[i]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dwacc[i][j] = 0.f;
+  }
+  for (int row = wid; row < rows; row += nwaves) {
+    const size_t base = (size_t)row * H;
+    const float r = rstd[row];
+    float g[VPT][8], hx[VPT][8];
+    float dot = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      const int v = i * 64 + lane;
+      if (v < nv) {
+        float d[8];
+        unpack8(ld16(dy + base + v * 8), d);
+        unpack8(ld16(h + base + v * 8), hx[i]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          g[i][j] = d[j] * wf[i][j];
+          dot += g[i][j] * hx[i][j];
+          dwacc[i][j] += d[j] * hx[i][j] * r;
+        }
+      }
+    }
+    dot = wave_sum(dot);
+    const float c = r * r * r * dot / (float)H;
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      const int v = i * 64 + lane;
+      if (v < nv) {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = r * g[i][j] - hx[i][j] * c;
+        if (dres) {
+          float t[8];
+          unpack8(ld16(dres + base + v * 8), t);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] += t[j];
+        }
+        st16(dh + base + v * 8, pack8(o));
+      }
+    }
+  }
+  float* out = dw_part + (size_t)wid * H;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int v = i * 64 + lane;
+    if (v < nv) {
+      stf4(out + v * 8, f32x4{dwacc[i][0], dwacc[i][1], dwacc[i][2], dwacc[i][3]});
+      stf4(out + v * 8 + 4, f32x4{dwacc[i][4], dwacc[i][5], dwacc[i][6], dwacc[i][7]});
+    }
+  }
+}
+
+// Column-sum P partial rows of length H (fp32) into a bf16 vector, optionally
+// accumulating into the existing value (gradient accumulation into the flat grad buffer).
+// Block = 16 waves x 64 columns; wave k sums rows k, k+16, ... (256-B coalesced row
+// segments, 8 loads in flight per lane), then the 16 wave sums meet in LDS.
+__global__ __launch_bounds__(1024) void colsum_to_bf16_kernel(const float* __restrict__ part, int P,
+                                                              int H, bf16_t* __restrict__ out,
+                                                              int accumulate) {
+  __shared__ float red[16][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  float s = 0.f;
+  if (c < H) {
+    int p = wv;
+    for (; p + 16 * 7 < P; p += 16 * 8) {
+      float t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t[u] = part[(size_t)(p + 16 * u) * H + c];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += t[u];
+    }
+    for (; p < P; p += 16) s += part[(size_t)p * H + c];
+  }
+  red[wv][lane] = s;
+  __syncthreads();
+  if (wv == 0 && c < H) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t += red[k][lane];
+    if (accumulate) t += bf2f(out[c]);
+    out[c] = f2bf(t);
+  }
+}
+
+#define DISPATCH_VPT(nv, ...)                 \
+  do {                                        \
+    int _v = ((nv) + 63) / 64;                \
+    if (_v <= 1) { constexpr int VPT = 1; __VA_ARGS__; }        \
+    else if (_v <= 2) { constexpr int VPT = 2; __VA_ARGS__; }   \
+    else if (_v <= 4) { constexpr int VPT = 4; __VA_ARGS__; }   \
+    else if (_v <= 8) { constexpr int VPT = 8; __VA_ARGS__; }   \
+    else if (_v <= 12) { constexpr int VPT = 12; __VA_ARGS__; } \
+    else { constexpr int VPT = 16; __VA_ARGS__; }               \
+  } while (0)
+
+extern "C" {
+
+int kf_rmsnorm_fwd(const void* a, const void* b, void* h_out, void* y, float* rstd, const void* w,
+                   int rows, int H, float eps, hipStream_t s) {
+  if (H % 8 != 0 || H > 8192) return 1;
+  dim3 grid(cdiv(rows, 4));
+  DISPATCH_VPT(H / 8, rmsnorm_fwd_kernel<VPT><<<grid, 256, 0, s>>>(
+                          (const bf16_t*)a, (const bf16_t*)b, (bf16_t*)h_out, (bf16_t*)y, rstd,
+                          (const bf16_t*)w, rows, H, eps));
+  return 0;
+}
+
+// dw_part must hold (nblocks*4) * H floats; returns nblocks used via *nparts.
+int kf_rmsnorm_bwd(const void* dy, const void* h, const float* rstd, const void* w,
+                   const void* dres, void* dh, float* dw_part, int nblocks, void* dw_out,
+                   int accumulate, int rows, int H, hipStream_t s) {
+  if (H % 8 != 0 || H > 8192) return 1;
+  DISPATCH_VPT(H / 8, rmsnorm_bwd_kernel<VPT><<<nblocks, 256, 0, s>>>(
+                          (const bf16_t*)dy, (const bf16_t*)h, rstd, (const bf16_t*)w,
+                          (const bf16_t*)dres, (bf16_t*)dh, dw_part, rows, H));
+  colsum_to_bf16_kernel<<<cdiv(H, 64), 1024, 0, s>>>(dw_part, nblocks * 4, H, (bf16_t*)dw_out,
+                                                      accumulate);
+  return 0;
+}
+
+}  // extern "C"

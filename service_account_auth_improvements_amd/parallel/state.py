@@ -1,0 +1,136 @@
+"""Process-group state for one-process-per-GPU training over RCCL (xGMI).
+
+Rank layout inside one node (8 x MI355X) is [pp][dp][tp] with TP innermost, so a TP
+group is the set of GPUs with the most point-to-point traffic per layer; on an 8-GPU
+xGMI mesh every pair of GPUs has its own link, so any contiguous block works and TP=8
+spans the whole node.
+
+``torch.distributed``'s ``nccl`` backend IS RCCL on ROCm.  CPU runs (tests) use gloo.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class ParallelState:
+    world_size: int = 1
+    rank: int = 0
+    local_rank: int = 0
+    tp: int = 1
+    pp: int = 1
+    dp: int = 1
+    tp_rank: int = 0
+    pp_rank: int = 0
+    dp_rank: int = 0
+    tp_group: Optional[object] = None
+    dp_group: Optional[object] = None
+    pp_group: Optional[object] = None
+    pp_prev: Optional[int] = None   # global rank of previous stage
+    pp_next: Optional[int] = None
+    device: torch.device = torch.device("cpu")
+    backend: str = "none"
+
+    @property
+    def is_first_stage(self):
+        return self.pp_rank == 0
+
+    @property
+    def is_last_stage(self):
+        return self.pp_rank == self.pp - 1
+
+
+_STATE: Optional[ParallelState] = None
+
+
+def init_distributed(tp: int = 1, pp: int = 1, backend: Optional[str] = None,
+                     device: Optional[str] = None, timeout_s: int = 1800) -> ParallelState:
+    """Initialise the default process group from torchrun env vars (RANK, WORLD_SIZE,
+    LOCAL_RANK, MASTER_ADDR/PORT) and build TP/DP/PP groups.  Works with world_size 1
+    without any env."""
+    global _STATE
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    use_gpu = torch.cuda.is_available() if device is None else device.startswith("cuda")
+    if backend is None:
+        backend = "nccl" if use_gpu else "gloo"
+    if use_gpu:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+    else:
+        dev = torch.device("cpu")
+    assert world % (tp * pp) == 0, f"world {world} not divisible by tp*pp={tp * pp}"
+    dp = world // (tp * pp)
+    st = ParallelState(world_size=world, rank=rank, local_rank=local, tp=tp, pp=pp, dp=dp,
+                       device=dev, backend=backend)
+    if world > 1:
+        if not dist.is_initialized():
+            kw = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
+            if backend == "nccl":
+                kw["device_id"] = dev
+            dist.init_process_group(**kw)
+        # rank = ((pp_rank * dp) + dp_rank) * tp + tp_rank
+        st.tp_rank = rank % tp
+        st.dp_rank = (rank // tp) % dp
+        st.pp_rank = rank // (tp * dp)
+        for p in range(pp):
+            for d in range(dp):
+                ranks = [(p * dp + d) * tp + t for t in range(tp)]
+                g = dist.new_group(ranks) if tp > 1 else None
+                if rank in ranks:
+                    st.tp_group = g
+        for p in range(pp):
+            for t in range(tp):
+                ranks = [(p * dp + d) * tp + t for d in range(dp)]
+                g = dist.new_group(ranks) if dp > 1 else None
+                if rank in ranks:
+                    st.dp_group = g
+        for d in range(dp):
+            for t in range(tp):
+                ranks = [(p * dp + d) * tp + t for p in range(pp)]
+                g = dist.new_group(ranks) if pp > 1 else None
+                if rank in ranks:
+                    st.pp_group = g
+                    i = ranks.index(rank)
+                    st.pp_prev = ranks[i - 1] if i > 0 else None
+                    st.pp_next = ranks[i + 1] if i < pp - 1 else None
+    _STATE = st
+    return st
+
+
+def get_state() -> ParallelState:
+    global _STATE
+    if _STATE is None:
+        _STATE = ParallelState()
+    return _STATE
+
+
+def set_state(st: ParallelState):
+    global _STATE
+    _STATE = st
+
+
+def tp_all_reduce(x: torch.Tensor, st: Optional[ParallelState] = None) -> torch.Tensor:
+    st = st or get_state()
+    if st.tp > 1:
+        dist.all_reduce(x, group=st.tp_group)
+    return x
+
+
+def barrier():
+    if dist.is_initialized():
+        dist.barrier()
+
+
+def destroy():
+    global _STATE
+    if dist.is_initialized():
+        dist.destroy_process_group()
+    _STATE = None

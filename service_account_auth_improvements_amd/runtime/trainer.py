@@ -1,0 +1,103 @@
+"""Training step driver for the Llama worker runtime.
+
+One process per GPU.  A step = micro-batches of explicit forward+backward (no autograd),
+weight gradients written into flat buffers, DP gradient buckets reduced over RCCL while
+backward is still running, then one fused AdamW kernel per flat group.  Pipeline
+parallel training uses :mod:`..parallel.pipeline` on top of the same pieces.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+from typing import Iterable, List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+from ..models.llama import Llama, LlamaConfig
+from ..parallel.ddp import GradReducer
+from ..parallel.state import ParallelState, get_state
+from .optim import AdamWConfig, FlatAdamW
+
+
+@dataclass
+class TrainConfig:
+    model: str = "llama3-8b"
+    seq_len: int = 8192
+    micro_batch: int = 1
+    grad_accum: int = 1
+    zero1: bool = False
+    bucket_mb: int = 256
+    lr: float = 3e-4
+    weight_decay: float = 0.1
+    max_grad_norm: float = 1.0
+    seed: int = 1234
+    n_layers: Optional[int] = None   # override (tests only; benches must use the full model)
+
+
+class Trainer:
+    def __init__(self, tcfg: TrainConfig, st: Optional[ParallelState] = None,
+                 mcfg: Optional[LlamaConfig] = None, full_init: bool = False):
+        self.tcfg = tcfg
+        self.st = st or get_state()
+        mcfg = mcfg or LlamaConfig.preset(tcfg.model)
+        if tcfg.n_layers is not None:
+            mcfg = mcfg.with_(n_layers=tcfg.n_layers)
+        if tcfg.seq_len > mcfg.max_seq:
+            mcfg = mcfg.with_(max_seq=tcfg.seq_len)
+        self.mcfg = mcfg
+        assert self.st.pp == 1, "use parallel.pipeline.PipelineTrainer for pp > 1"
+        self.model = Llama(mcfg, self.st, seed=tcfg.seed, full_init=full_init)
+        self.model.allocate(pad_to=self.st.dp * 64 if tcfg.zero1 else 1)
+        mode = "reduce_scatter" if (tcfg.zero1 and self.st.dp > 1) else "allreduce"
+        self.reducer = GradReducer(self.model.groups, self.st.dp_group, self.st.dp,
+                                   bucket_bytes=tcfg.bucket_mb << 20, mode=mode)
+        # identical replicas: broadcast from the first rank of this DP group (C2)
+        if self.st.dp > 1:
+            src = self.st.rank - self.st.dp_rank * self.st.tp
+            self.reducer.broadcast_params(src)
+        shard = None
+        if mode == "reduce_scatter":
+            shard = {g.name: self.reducer.shard_ranges(g, self.st.dp_rank) for g in self.model.groups}
+        self.opt = FlatAdamW(self.model.groups,
+                             AdamWConfig(lr=tcfg.lr, weight_decay=tcfg.weight_decay,
+                                         max_grad_norm=tcfg.max_grad_norm),
+                             shard_ranges=shard, dp_group=self.st.dp_group)
+        self.step_idx = 0
+
+    @property
+    def tokens_per_step(self) -> int:
+        """Tokens processed by THIS rank per step."""
+        return self.tcfg.micro_batch * self.tcfg.seq_len * self.tcfg.grad_accum
+
+    def train_step(self, micro_batches: List[Tuple[torch.Tensor, torch.Tensor]]) -> torch.Tensor:
+        n = len(micro_batches)
+        ntok = sum(t.numel() for t, _ in micro_batches)
+        scale = 1.0 / ntok
+        self.reducer.start_step()
+        total = None
+        for j, (tok, lab) in enumerate(micro_batches):
+            self.model.on_grad_ready = self.reducer.grad_ready if j == n - 1 else None
+            loss = self.model.forward_backward(tok, lab, accumulate=j > 0, scale=scale)
+            total = loss if total is None else total + loss
+        self.model.on_grad_ready = None
+        self.reducer.finish()
+        self.opt.step(grad_scale=1.0 / self.st.dp)
+        self.reducer.all_gather_params()
+        self.step_idx += 1
+        return total
+
+
+class SyntheticData:
+    """Deterministic synthetic token batches (random ids, labels = next token)."""
+
+    def __init__(self, vocab: int, micro_batch: int, seq_len: int, device, seed: int = 0,
+                 rank: int = 0):
+        self.vocab, self.mb, self.S = vocab, micro_batch, seq_len
+        self.device = device
+        self.g = torch.Generator(device="cpu").manual_seed(seed * 7919 + rank)
+
+    def next(self):
+        x = torch.randint(0, self.vocab, (self.mb, self.S + 1), generator=self.g)
+        x = x.to(self.device, non_blocking=True)
+        return x[:, :-1].contiguous(), x[:, 1:].contiguous()

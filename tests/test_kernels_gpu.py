@@ -1,0 +1,141 @@
+"""Numerics of every gfx950 HIP kernel against the plain-PyTorch fp32 reference of the
+same op (ops/reference.py).  All tests run the HIP path (torch.ops.kfamd) on cuda:0."""
+import math
+
+import pytest
+import torch
+
+from service_account_auth_improvements_amd import ops
+from service_account_auth_improvements_amd.ops import _ext, reference
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    assert _ext.load(), "HIP library must load on a GPU box"
+    assert hasattr(torch.ops.kfamd, "rmsnorm_fwd")
+
+
+def _rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-6)).item()
+
+
+@pytest.mark.parametrize("rows,H", [(7, 4096), (64, 4096), (33, 8192), (5, 1000), (128, 256)])
+@pytest.mark.parametrize("residual", [False, True])
+def test_rmsnorm_fwd_bwd(rows, H, residual):
+    torch.manual_seed(0)
+    a = torch.randn(rows, H, device=DEV, dtype=torch.bfloat16)
+    b = torch.randn(rows, H, device=DEV, dtype=torch.bfloat16) if residual else None
+    w = (1 + 0.1 * torch.randn(H, device=DEV)).to(torch.bfloat16)
+    y, h, rstd = ops.rmsnorm_fwd(a, w, 1e-5, residual=b)
+    yr, hr, rr = reference.rmsnorm_fwd(a, b, w, 1e-5)
+    assert _rel(y, yr) < 1e-2
+    assert torch.allclose(rstd, rr, rtol=1e-4)
+    if residual:
+        assert torch.equal(h, hr)
+    dy = torch.randn_like(a)
+    dres = torch.randn_like(a) if residual else None
+    dw = torch.zeros(H, device=DEV, dtype=torch.bfloat16)
+    dh = ops.rmsnorm_bwd(dy, h, rstd, w, dw, dres=dres)
+    dhr, dwr = reference.rmsnorm_bwd(dy, h, rr, w, dres)
+    assert _rel(dh, dhr) < 1e-2
+    assert _rel(dw, dwr) < 1e-2
+    # accumulate mode adds into the existing gradient
+    dw2 = dw.clone()
+    ops.rmsnorm_bwd(dy, h, rstd, w, dw2, accumulate=True, dres=dres)
+    assert _rel(dw2, 2 * dwr) < 1e-2
+
+
+@pytest.mark.parametrize("T,S,Hq,Hkv,D", [(64, 32, 4, 2, 128), (512, 256, 32, 8, 128), (96, 96, 8, 8, 64)])
+def test_rope(T, S, Hq, Hkv, D):
+    torch.manual_seed(1)
+    cos, sin = reference.rope_tables(S, D, 500000.0, device=DEV)
+    qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device=DEV, dtype=torch.bfloat16)
+    x = qkv.clone()
+    ops.rope_(x, Hq + Hkv, D, cos, sin, seq_len=S)
+    xr = reference.rope_(qkv.clone(), Hq + Hkv, D, cos, sin, seq_len=S)
+    assert _rel(x, xr) < 1e-2
+    assert torch.equal(x[:, (Hq + Hkv) * D:], qkv[:, (Hq + Hkv) * D:])  # v untouched
+    ops.rope_(x, Hq + Hkv, D, cos, sin, seq_len=S, inverse=True)     # inverse restores
+    assert _rel(x, qkv) < 2e-2
+    pos = torch.randint(0, S, (T,), device=DEV, dtype=torch.int32)
+    x = qkv.clone()
+    ops.rope_(x, Hq + Hkv, D, cos, sin, pos=pos)
+    xr = reference.rope_(qkv.clone(), Hq + Hkv, D, cos, sin, pos=pos)
+    assert _rel(x, xr) < 1e-2
+
+
+@pytest.mark.parametrize("rows,F", [(17, 14336), (256, 512), (3, 8)])
+def test_swiglu(rows, F):
+    torch.manual_seed(2)
+    gu = torch.randn(rows, 2 * F, device=DEV, dtype=torch.bfloat16) * 3
+    out = ops.swiglu_fwd(gu)
+    assert _rel(out, reference.swiglu_fwd(gu)) < 1e-2
+    d = torch.randn(rows, F, device=DEV, dtype=torch.bfloat16)
+    assert _rel(ops.swiglu_bwd(gu, d), reference.swiglu_bwd(gu, d)) < 1e-2
+
+
+@pytest.mark.parametrize("T,V", [(16, 128256), (64, 1024), (5, 16032)])
+def test_cross_entropy_fused(T, V):
+    torch.manual_seed(3)
+    logits = (torch.randn(T, V, device=DEV) * 4).to(torch.bfloat16)
+    labels = torch.randint(0, V, (T,), device=DEV)
+    labels[1] = -100
+    loss_r, lse_r, g_r = reference.cross_entropy(logits, labels, -100, 1.0 / T)
+    x = logits.clone()
+    loss, lse = ops.cross_entropy_fused_(x, labels, 1.0 / T)
+    assert torch.allclose(loss, loss_r, atol=2e-3, rtol=1e-3)
+    assert torch.allclose(lse, lse_r, atol=2e-3, rtol=1e-4)
+    assert _rel(x, g_r) < 2e-2
+    assert x[1].abs().max().item() == 0.0
+    # device-tensor scale path
+    x2 = logits.clone()
+    ops.cross_entropy_fused_(x2, labels, torch.tensor([1.0 / T], device=DEV))
+    assert torch.equal(x2, x)
+
+
+def test_cross_entropy_vocab_parallel_matches_fused():
+    torch.manual_seed(4)
+    T, V, tp = 32, 4096, 4
+    logits = (torch.randn(T, V, device=DEV) * 3).to(torch.bfloat16)
+    labels = torch.randint(0, V, (T,), device=DEV)
+    full = logits.clone()
+    loss_f, lse_f = ops.cross_entropy_fused_(full, labels, 0.5)
+    Vl = V // tp
+    stats = [ops.cross_entropy_stats(logits[:, r * Vl:(r + 1) * Vl].contiguous(), labels, r * Vl)
+             for r in range(tp)]
+    M = torch.stack([s[0] for s in stats]).max(0).values
+    S = sum(s[1] * torch.exp(s[0] - M) for s in stats)
+    lse = M + torch.log(S)
+    xy = sum(s[2] for s in stats)
+    assert torch.allclose(lse, lse_f, atol=1e-3)
+    assert torch.allclose(lse - xy, loss_f, atol=1e-3)
+    for r in range(tp):
+        sh = logits[:, r * Vl:(r + 1) * Vl].contiguous()
+        ops.cross_entropy_grad_(sh, labels, lse, 0.5, r * Vl)
+        assert _rel(sh, full[:, r * Vl:(r + 1) * Vl]) < 2e-2
+
+
+def test_adamw_flat_and_sumsq():
+    torch.manual_seed(5)
+    n = 1 << 20
+    g = torch.randn(n, device=DEV).to(torch.bfloat16)
+    w = torch.randn(n, device=DEV)
+    p = w.to(torch.bfloat16)
+    m = torch.zeros(n, device=DEV)
+    v = torch.zeros(n, device=DEV)
+    w2, m2, v2, p2 = w.clone(), m.clone(), v.clone(), p.clone()
+    ss = torch.zeros(1, device=DEV)
+    ops.sumsq_(g, ss)
+    assert math.isclose(float(ss), float(g.float().pow(2).sum()), rel_tol=1e-4)
+    for step in (1, 2, 3):
+        ops.adamw_(p, w, m, v, g, n // 2, 1e-3, 0.9, 0.95, 1e-8, 0.1, step, 0.5, ss, 1.0)
+        reference.adamw_(p2, w2, m2, v2, g, n // 2, 1e-3, 0.9, 0.95, 1e-8, 0.1, step, 0.5,
+                         float(ss), 1.0)
+    assert torch.allclose(w, w2, atol=1e-6, rtol=1e-5)
+    assert torch.allclose(m, m2, atol=1e-7, rtol=1e-5)
+    assert torch.allclose(v, v2, atol=1e-9, rtol=1e-5)
+    assert torch.equal(p, w.to(torch.bfloat16))
