@@ -8,7 +8,8 @@
 #include <torch/library.h>
 #include <ATen/ATen.h>
 #include <c10/hip/HIPStream.h>
-#include <c10/hip/HIPGuard.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <hip/hip_runtime.h>
 
 #include <tuple>
@@ -27,8 +28,8 @@ int kf_adamw(void*, float*, float*, float*, const void*, size_t, size_t, float, 
 int kf_sumsq(const void*, size_t, float*, float*, int, hipStream_t);
 int kf_cross_entropy(void*, long, int, int, const long*, long, long, float*, float*, float*, float*,
                      float*, const float*, float, int, hipStream_t);
-int kf_flash_fwd(const void*, const void*, const void*, void*, float*, int, int, int, int, int, int,
-                 long, long, long, long, float, int, hipStream_t);
+int kf_flash_fwd(const void*, long, void*, long, float*, int, int, int, int, int, float, int,
+                 hipStream_t);
 int kf_flash_bwd(const void*, const void*, const void*, const void*, const void*, const float*,
                  void*, void*, void*, float*, float*, int, int, int, int, int, int, long, long,
                  long, long, long, long, float, int, hipStream_t);
@@ -38,7 +39,7 @@ int kf_decode_attn(const void*, const void*, const void*, const int*, void*, flo
 
 namespace {
 
-hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
 
 void check_bf16_cuda(const at::Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
@@ -56,7 +57,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> rmsnorm_fwd(const at::Tensor& a,
   const int64_t H = a.size(-1);
   TORCH_CHECK(w.numel() == H, "rmsnorm: weight size mismatch");
   const int64_t rows = a.numel() / H;
-  c10::hip::HIPGuard g(a.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(a.device());
   auto y = at::empty_like(a);
   auto rstd = at::empty({rows}, a.options().dtype(at::kFloat));
   at::Tensor h;
@@ -87,7 +88,7 @@ at::Tensor rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& h, const at::Tens
   TORCH_CHECK(dw.is_contiguous() && dw.numel() == h.size(-1), "rmsnorm_bwd: dw shape");
   const int64_t H = h.size(-1), rows = h.numel() / H;
   TORCH_CHECK(rstd.numel() == rows, "rmsnorm_bwd: rstd shape");
-  c10::hip::HIPGuard g(h.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(h.device());
   auto dh = at::empty_like(h);
   const void* dr = nullptr;
   if (dres.has_value()) {
@@ -121,7 +122,7 @@ void rope_(at::Tensor x, int64_t nheads, int64_t head_dim, const at::Tensor& cos
   } else {
     TORCH_CHECK(seq_len > 0 && seq_len <= cos_t.size(0), "rope: seq_len exceeds table");
   }
-  c10::hip::HIPGuard g(x.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   check_rc(kf_rope(x.data_ptr(), x.stride(0), (int)x.size(0), (int)nheads, (int)head_dim,
                    cos_t.data_ptr<float>(), sin_t.data_ptr<float>(), pp, (int)seq_len,
                    inverse ? 1 : 0, cur_stream()),
@@ -135,7 +136,7 @@ at::Tensor swiglu_fwd(const at::Tensor& gu) {
   const int64_t F = gu.size(-1) / 2, rows = gu.numel() / gu.size(-1);
   auto sizes = gu.sizes().vec();
   sizes.back() = F;
-  c10::hip::HIPGuard g(gu.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(gu.device());
   auto out = at::empty(sizes, gu.options());
   check_rc(kf_swiglu_fwd(gu.data_ptr(), out.data_ptr(), (int)rows, (int)F, cur_stream()), "swiglu_fwd");
   return out;
@@ -146,7 +147,7 @@ at::Tensor swiglu_bwd(const at::Tensor& gu, const at::Tensor& dout) {
   check_bf16_cuda(dout, "dout");
   const int64_t F = gu.size(-1) / 2, rows = gu.numel() / gu.size(-1);
   TORCH_CHECK(gu.is_contiguous() && dout.is_contiguous() && dout.numel() == rows * F, "swiglu_bwd: shapes");
-  c10::hip::HIPGuard g(gu.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(gu.device());
   auto dgu = at::empty_like(gu);
   check_rc(kf_swiglu_bwd(gu.data_ptr(), dout.data_ptr(), dgu.data_ptr(), (int)rows, (int)F, cur_stream()),
            "swiglu_bwd");
@@ -167,7 +168,7 @@ void adamw_(at::Tensor p, at::Tensor w, at::Tensor m, at::Tensor v, const at::Te
                   g.is_contiguous(), "adamw: contiguous flat buffers required");
   const float* sp = nullptr;
   if (sumsq.has_value()) sp = sumsq->data_ptr<float>();
-  c10::hip::HIPGuard gd(p.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA gd(p.device());
   check_rc(kf_adamw(p.data_ptr(), w.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
                     g.data_ptr(), (size_t)n, (size_t)n_decay, (float)lr, (float)b1, (float)b2,
                     (float)eps, (float)wd, (int)step, (float)gscale, sp, (float)max_norm, cur_stream()),
@@ -177,7 +178,7 @@ void adamw_(at::Tensor p, at::Tensor w, at::Tensor m, at::Tensor v, const at::Te
 void sumsq(const at::Tensor& g, at::Tensor out, bool accumulate) {
   check_bf16_cuda(g, "g");
   TORCH_CHECK(g.is_contiguous() && out.scalar_type() == at::kFloat, "sumsq: args");
-  c10::hip::HIPGuard gd(g.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA gd(g.device());
   auto part = at::empty({2048}, g.options().dtype(at::kFloat));
   check_rc(kf_sumsq(g.data_ptr(), (size_t)g.numel(), part.data_ptr<float>(), out.data_ptr<float>(),
                     accumulate ? 1 : 0, cur_stream()),
@@ -202,11 +203,27 @@ void cross_entropy_(at::Tensor logits, const at::Tensor& labels, int64_t vocab_s
     pm = sm->data_ptr<float>(); ps = ss->data_ptr<float>(); pxy = sxy->data_ptr<float>();
   }
   const float* scp = scale.has_value() ? scale->data_ptr<float>() : nullptr;
-  c10::hip::HIPGuard g(logits.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(logits.device());
   check_rc(kf_cross_entropy(logits.data_ptr(), logits.stride(0), (int)rows, (int)logits.size(1),
                             labels.data_ptr<int64_t>(), vocab_start, ignore_index, loss.data_ptr<float>(),
                             lse.data_ptr<float>(), pm, ps, pxy, scp, (float)scale_h, (int)mode, cur_stream()),
            "cross_entropy");
+}
+
+// ---------------- Flash attention (K3) ----------------
+std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& qkv, int64_t B, int64_t S, int64_t Hq,
+                                             int64_t Hkv, int64_t D, double scale, bool causal) {
+  check_bf16_cuda(qkv, "qkv");
+  TORCH_CHECK(qkv.dim() == 2 && qkv.stride(1) == 1 && qkv.size(0) == B * S &&
+                  qkv.size(1) >= (Hq + 2 * Hkv) * D, "flash_fwd: qkv must be [B*S, >=(Hq+2Hkv)*D]");
+  TORCH_CHECK(D == 128 && S % 128 == 0 && Hq % Hkv == 0, "flash_fwd: needs D=128, S%128==0, Hq%Hkv==0");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(qkv.device());
+  auto o = at::empty({B * S, Hq * D}, qkv.options());
+  auto lse = at::empty({B, Hq, S}, qkv.options().dtype(at::kFloat));
+  check_rc(kf_flash_fwd(qkv.data_ptr(), qkv.stride(0), o.data_ptr(), o.stride(0), lse.data_ptr<float>(),
+                        (int)B, (int)S, (int)Hq, (int)Hkv, (int)D, (float)scale, causal ? 1 : 0, cur_stream()),
+           "flash_fwd");
+  return {o, lse};
 }
 
 }  // namespace
@@ -220,4 +237,5 @@ TORCH_LIBRARY(kfamd, m) {
   m.def("adamw_", &adamw_);
   m.def("sumsq", &sumsq);
   m.def("cross_entropy_", &cross_entropy_);
+  m.def("flash_fwd", &flash_fwd);
 }

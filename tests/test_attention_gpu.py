@@ -1,0 +1,44 @@
+"""Flash attention (K3) numerics vs an fp32 PyTorch reference (full tensors)."""
+import math
+
+import pytest
+import torch
+
+from service_account_auth_improvements_amd.ops import _ext, reference
+from service_account_auth_improvements_amd.ops.attention import _split
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _qkv(B, S, Hq, Hkv, D=128, seed=0, scale=1.0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    x = torch.randn(B * S, (Hq + 2 * Hkv) * D, generator=g) * scale
+    return x.to(DEV, torch.bfloat16)
+
+
+@pytest.mark.parametrize("B,S,Hq,Hkv,causal", [
+    (1, 128, 2, 1, True), (2, 256, 8, 2, True), (1, 1024, 32, 8, True),
+    (1, 384, 4, 4, False), (2, 512, 8, 1, True)])
+def test_flash_fwd(B, S, Hq, Hkv, causal):
+    assert _ext.load()
+    qkv = _qkv(B, S, Hq, Hkv, seed=S + Hq)
+    o, lse = torch.ops.kfamd.flash_fwd(qkv, B, S, Hq, Hkv, 128, 1 / math.sqrt(128), causal)
+    q, k, v = _split(qkv, B, S, Hq, Hkv, 128)
+    o_ref, lse_ref = reference.attention(q, k, v, causal)
+    o_ref = o_ref.transpose(1, 2).reshape(B * S, Hq * 128)
+    err = (o.float() - o_ref).abs().max().item()
+    assert err < 2e-2, err
+    assert torch.allclose(lse, lse_ref, atol=2e-3, rtol=1e-4), (lse - lse_ref).abs().max().item()
+
+
+def test_flash_fwd_spiky_scores():
+    """Large-magnitude inputs force big running-max jumps inside the online softmax."""
+    B, S, Hq, Hkv = 1, 512, 4, 2
+    qkv = _qkv(B, S, Hq, Hkv, seed=7, scale=4.0)
+    o, lse = torch.ops.kfamd.flash_fwd(qkv, B, S, Hq, Hkv, 128, 1 / math.sqrt(128), True)
+    q, k, v = _split(qkv, B, S, Hq, Hkv, 128)
+    o_ref, lse_ref = reference.attention(q, k, v, True)
+    o_ref = o_ref.transpose(1, 2).reshape(B * S, Hq * 128)
+    assert (o.float() - o_ref).abs().max().item() < 8e-2
+    assert torch.allclose(lse, lse_ref, atol=2e-2, rtol=1e-3)
