@@ -19,7 +19,7 @@ import torch.nn.functional as F
 
 from . import _ext, reference
 
-_BACKEND = "sdpa"  # flipped to "hip" once flash_attn.hip lands
+_BACKEND = "hip"
 
 
 def set_attention_backend(name: str) -> None:

@@ -42,3 +42,25 @@ def test_flash_fwd_spiky_scores():
     o_ref = o_ref.transpose(1, 2).reshape(B * S, Hq * 128)
     assert (o.float() - o_ref).abs().max().item() < 8e-2
     assert torch.allclose(lse, lse_ref, atol=2e-2, rtol=1e-3)
+
+
+@pytest.mark.parametrize("B,S,Hq,Hkv,causal", [
+    (1, 256, 2, 1, True), (2, 512, 8, 2, True), (1, 1024, 32, 8, True),
+    (1, 512, 4, 4, False), (1, 768, 8, 1, True)])
+def test_flash_bwd(B, S, Hq, Hkv, causal):
+    qkv = _qkv(B, S, Hq, Hkv, seed=S + 3 * Hq)
+    sc = 1 / math.sqrt(128)
+    o, lse = torch.ops.kfamd.flash_fwd(qkv, B, S, Hq, Hkv, 128, sc, causal)
+    g = torch.Generator(device="cpu").manual_seed(11)
+    do = torch.randn(o.shape, generator=g).to(DEV, torch.bfloat16)
+    dqkv = torch.ops.kfamd.flash_bwd(qkv, o, lse, do, B, S, Hq, Hkv, 128, sc, causal)
+    x = qkv.float().detach().requires_grad_(True)
+    q, k, v = _split(x, B, S, Hq, Hkv, 128)
+    o_ref, _ = reference.attention(q, k, v, causal)
+    o_ref = o_ref.transpose(1, 2).reshape(B * S, Hq * 128)
+    (ref,) = torch.autograd.grad(o_ref, x, do.float())
+    for name, lo, hi in (("dq", 0, Hq * 128), ("dk", Hq * 128, (Hq + Hkv) * 128),
+                         ("dv", (Hq + Hkv) * 128, (Hq + 2 * Hkv) * 128)):
+        a, r = dqkv[:, lo:hi].float(), ref[:, lo:hi]
+        rel = ((a - r).abs().max() / r.abs().max()).item()
+        assert rel < 3e-2, (name, rel)
