@@ -31,7 +31,7 @@ int kf_cross_entropy(void*, long, int, int, const long*, long, long, float*, flo
 int kf_flash_fwd(const void*, long, void*, long, float*, int, int, int, int, int, float, int,
                  hipStream_t);
 int kf_flash_bwd(const void*, long, const void*, long, const void*, long, const float*, float*,
-                 float*, float*, float*, void*, long, int, int, int, int, int, float, int, hipStream_t);
+                 float*, float*, void*, long, int, int, int, int, int, float, int, hipStream_t);
 int kf_decode_attn(const void*, const void*, const void*, const int*, void*, float*, int, int, int,
                    int, int, long, long, long, long, float, int, hipStream_t);
 }
@@ -236,17 +236,16 @@ at::Tensor flash_bwd(const at::Tensor& qkv, const at::Tensor& o, const at::Tenso
   TORCH_CHECK(o.dim() == 2 && o.stride(1) == 1 && o.size(0) == B * S && o.size(1) == Hq * D, "flash_bwd: o shape");
   TORCH_CHECK(dout.sizes() == o.sizes() && dout.stride(1) == 1, "flash_bwd: dout shape");
   TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.is_contiguous() && lse.numel() == B * Hq * S, "flash_bwd: lse");
-  TORCH_CHECK(D == 128 && S % 256 == 0 && Hq % Hkv == 0, "flash_bwd: needs D=128, S%256==0");
+  TORCH_CHECK(D == 128 && S % 128 == 0 && Hq % Hkv == 0, "flash_bwd: needs D=128, S%128==0");
   c10::hip::HIPGuardMasqueradingAsCUDA g(qkv.device());
   auto f32 = qkv.options().dtype(at::kFloat);
   auto delta = at::empty({B, Hq, S}, f32);
-  auto acc = at::zeros({B * S * (Hq + 2 * Hkv) * D}, f32);
-  float* dq = acc.data_ptr<float>();
-  float* dk = dq + B * S * Hq * D;
+  auto acc = at::zeros({2 * B * S * Hkv * D}, f32);
+  float* dk = acc.data_ptr<float>();
   float* dv = dk + B * S * Hkv * D;
   auto dqkv = at::empty({B * S, (Hq + 2 * Hkv) * D}, qkv.options());
   check_rc(kf_flash_bwd(qkv.data_ptr(), qkv.stride(0), o.data_ptr(), o.stride(0), dout.data_ptr(),
-                        dout.stride(0), lse.data_ptr<float>(), delta.data_ptr<float>(), dq, dk, dv,
+                        dout.stride(0), lse.data_ptr<float>(), delta.data_ptr<float>(), dk, dv,
                         dqkv.data_ptr(), dqkv.stride(0), (int)B, (int)S, (int)Hq, (int)Hkv, (int)D,
                         (float)scale, causal ? 1 : 0, cur_stream()),
            "flash_bwd");
