@@ -39,7 +39,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--model", default="llama3-8b")
     ap.add_argument("--seq-len", type=int, default=8192)
-    ap.add_argument("--micro-batch", type=int, default=1)
+    ap.add_argument("--micro-batch", type=int, default=2)
     ap.add_argument("--grad-accum", type=int, default=1)
     ap.add_argument("--zero1", action="store_true", help="ZeRO-1 (reduce-scatter + sharded AdamW)")
     ap.add_argument("--bucket-mb", type=int, default=256)

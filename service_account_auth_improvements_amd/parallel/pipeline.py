@@ -1,0 +1,177 @@
+"""Pipeline parallelism: 1F1B schedule over point-to-point RCCL send/recv (C5).
+
+Each pipeline stage is a :class:`..models.llama.Llama` shard holding a contiguous layer
+range (stage 0 also the embedding, the last stage the final norm + LM head + CE).  The
+boundary activation is one [micro_batch * seq, hidden] bf16 tensor; on an xGMI mesh every
+stage pair has a direct link, so a stage hop is a single point-to-point transfer.
+
+Schedule (non-interleaved 1F1B): stage r runs ``pp - r - 1`` warm-up forwards, then
+alternates one forward / one backward, then drains the remaining backwards.  Send and
+receive of opposite directions are posted together through ``batch_isend_irecv`` so no
+ordering of blocking calls can deadlock.  Only ``pp - r`` micro-batches of activations
+are ever alive on stage r.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+from ..models.llama import Llama, LlamaConfig
+from .ddp import GradReducer
+from .state import ParallelState
+
+
+def stage_layers(n_layers: int, pp: int, rank: int) -> range:
+    """Even split of layers; the remainder goes to the middle stages (the first stage
+    also owns the embedding, the last the 128k-vocab LM head)."""
+    base, rem = divmod(n_layers, pp)
+    sizes = [base] * pp
+    order = list(range(1, pp - 1)) + [0, pp - 1] if pp > 2 else list(range(pp))
+    for i in range(rem):
+        sizes[order[i % len(order)]] += 1
+    start = sum(sizes[:rank])
+    return range(start, start + sizes[rank])
+
+
+class P2P:
+    def __init__(self, st: ParallelState, shape, dtype, device):
+        self.st, self.shape, self.dtype, self.device = st, shape, dtype, device
+
+    def _buf(self):
+        return torch.empty(self.shape, dtype=self.dtype, device=self.device)
+
+    def _run(self, ops):
+        if ops:
+            for r in dist.batch_isend_irecv(ops):
+                r.wait()
+
+    def recv_forward(self):
+        if self.st.pp_prev is None:
+            return None
+        x = self._buf()
+        self._run([dist.P2POp(dist.irecv, x, self.st.pp_prev)])
+        return x
+
+    def send_forward(self, y):
+        if self.st.pp_next is not None:
+            self._run([dist.P2POp(dist.isend, y.contiguous(), self.st.pp_next)])
+
+    def recv_backward(self):
+        if self.st.pp_next is None:
+            return None
+        g = self._buf()
+        self._run([dist.P2POp(dist.irecv, g, self.st.pp_next)])
+        return g
+
+    def send_backward(self, g):
+        if self.st.pp_prev is not None and g is not None:
+            self._run([dist.P2POp(dist.isend, g.contiguous(), self.st.pp_prev)])
+
+    def send_forward_recv_backward(self, y):
+        if self.st.pp_next is None:
+            return None
+        g = self._buf()
+        self._run([dist.P2POp(dist.isend, y.contiguous(), self.st.pp_next),
+                   dist.P2POp(dist.irecv, g, self.st.pp_next)])
+        return g
+
+    def send_backward_recv_forward(self, g):
+        if self.st.pp_prev is None:
+            return None
+        x = self._buf()
+        ops = [dist.P2POp(dist.irecv, x, self.st.pp_prev)]
+        if g is not None:
+            ops.insert(0, dist.P2POp(dist.isend, g.contiguous(), self.st.pp_prev))
+        self._run(ops)
+        return x
+
+
+def one_f_one_b(model: Llama, p2p: P2P, micro_batches: List[Tuple[torch.Tensor, torch.Tensor]],
+                scale: float, on_last_backward=None) -> Optional[torch.Tensor]:
+    """Run one optimizer step's worth of micro-batches through this stage.
+    Returns the summed (scaled) loss on the last stage, None elsewhere."""
+    st = p2p.st
+    M = len(micro_batches)
+    B, S = micro_batches[0][0].shape
+    warm = min(st.pp - st.pp_rank - 1, M)
+    steady = M - warm
+    ctxs, total = [], None
+    n_bwd = 0
+
+    def fwd(i, x):
+        nonlocal total
+        tok, lab = micro_batches[i]
+        inp = tok.reshape(-1) if model.first else x
+        out, ctx = model.stage_forward(inp, B, S, lab.reshape(-1), scale)
+        ctxs.append(ctx)
+        if model.last:
+            total = out if total is None else total + out
+            return None
+        return out
+
+    def bwd(g):
+        nonlocal n_bwd
+        ctx = ctxs.pop(0)
+        if n_bwd == M - 1 and on_last_backward is not None:
+            on_last_backward(True)
+        gin = model.stage_backward(ctx, g, B, S, accumulate=n_bwd > 0)
+        n_bwd += 1
+        return gin
+
+    for i in range(warm):
+        x = p2p.recv_forward()
+        p2p.send_forward(fwd(i, x))
+    x = p2p.recv_forward() if steady > 0 else None
+    for j in range(steady):
+        y = fwd(warm + j, x)
+        g = p2p.send_forward_recv_backward(y) if not model.last else None
+        gin = bwd(g)
+        if j == steady - 1:
+            p2p.send_backward(gin)
+        else:
+            x = p2p.send_backward_recv_forward(gin)
+    for _ in range(warm):
+        g = p2p.recv_backward()
+        p2p.send_backward(bwd(g))
+    if on_last_backward is not None:
+        on_last_backward(False)
+    return total
+
+
+class PipelineTrainer:
+    """DP x PP (x TP) training with 1F1B; same optimizer / reducer as the DP trainer."""
+
+    def __init__(self, tcfg, st: ParallelState, mcfg: Optional[LlamaConfig] = None,
+                 full_init: bool = False):
+        from ..runtime.optim import AdamWConfig, FlatAdamW
+        self.tcfg, self.st = tcfg, st
+        mcfg = mcfg or LlamaConfig.preset(tcfg.model)
+        if tcfg.n_layers is not None:
+            mcfg = mcfg.with_(n_layers=tcfg.n_layers)
+        if tcfg.seq_len > mcfg.max_seq:
+            mcfg = mcfg.with_(max_seq=tcfg.seq_len)
+        self.mcfg = mcfg
+        lr = stage_layers(mcfg.n_layers, st.pp, st.pp_rank)
+        self.model = Llama(mcfg, st, layer_range=lr, seed=tcfg.seed, full_init=full_init)
+        self.model.allocate()
+        self.reducer = GradReducer(self.model.groups, st.dp_group, st.dp,
+                                   bucket_bytes=tcfg.bucket_mb << 20)
+        self.opt = FlatAdamW(self.model.groups,
+                             AdamWConfig(lr=tcfg.lr, weight_decay=tcfg.weight_decay,
+                                         max_grad_norm=tcfg.max_grad_norm),
+                             norm_groups=[st.pp_group] if st.pp > 1 else None)
+        T = tcfg.micro_batch * tcfg.seq_len
+        self.p2p = P2P(st, (T, mcfg.hidden), torch.bfloat16, st.device)
+
+    def _hook(self, on: bool):
+        self.model.on_grad_ready = self.reducer.grad_ready if on else None
+
+    def train_step(self, micro_batches):
+        ntok = sum(t.numel() for t, _ in micro_batches)
+        self.reducer.start_step()
+        loss = one_f_one_b(self.model, self.p2p, micro_batches, 1.0 / ntok, self._hook)
+        self.reducer.finish()
+        self.opt.step(grad_scale=1.0 / self.st.dp)
+        return loss

@@ -16,6 +16,8 @@ buckets can be launched as soon as the prefix crosses a bucket boundary.
 """
 from __future__ import annotations
 
+import zlib
+
 from dataclasses import dataclass, field
 from typing import Dict, List, Tuple
 
@@ -93,7 +95,9 @@ class FlatGroup:
             elif s.init == "zeros":
                 p.zero_()
             else:
-                g = torch.Generator(device="cpu").manual_seed(seed * 1000003 + i)
+                # seed by NAME so every TP/PP partitioning draws identical weights
+                key = seed * 1000003 + zlib.crc32(s.name.encode())
+                g = torch.Generator(device="cpu").manual_seed(key)
                 if full_shapes and s.name in full_shapes:
                     fshape, slicer = full_shapes[s.name]
                     full = torch.empty(fshape, dtype=torch.float32).normal_(0.0, s.std, generator=g)
@@ -102,7 +106,7 @@ class FlatGroup:
                     p.copy_(torch.empty(s.shape, dtype=torch.float32).normal_(0.0, s.std, generator=g))
                 else:
                     # large tensors: draw on device in chunks (fast; still seeded)
-                    dg = torch.Generator(device=p.device).manual_seed(seed * 1000003 + i)
+                    dg = torch.Generator(device=p.device).manual_seed(key)
                     flat = p.view(-1)
                     step = 1 << 26
                     for o in range(0, flat.numel(), step):

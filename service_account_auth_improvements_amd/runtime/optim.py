@@ -40,13 +40,16 @@ class _Shard:
 
 class FlatAdamW:
     def __init__(self, groups: List[FlatGroup], cfg: AdamWConfig = AdamWConfig(),
-                 shard_ranges: Optional[dict] = None, dp_group=None):
+                 shard_ranges: Optional[dict] = None, dp_group=None, norm_groups=None):
         """``shard_ranges[group.name] = [(lo, hi), ...]`` restricts state to this rank's
         ZeRO-1 shard; None keeps full state."""
         self.cfg = cfg
         self.groups = groups
         self.step_count = 0
         self.dp_group = dp_group
+        # extra groups whose members hold DISJOINT parameters (pipeline stages): the
+        # squared gradient norm is summed over them too
+        self.norm_groups = [g for g in (norm_groups or []) if g is not None]
         self.sharded = shard_ranges is not None
         self.shards: List[_Shard] = []
         for g in groups:
@@ -69,6 +72,8 @@ class FlatAdamW:
             dist.all_reduce(self._sumsq, group=self.dp_group)
         elif self.sharded and dist.is_initialized() and dist.get_world_size() > 1:
             dist.all_reduce(self._sumsq)
+        for g in self.norm_groups:
+            dist.all_reduce(self._sumsq, group=g)
         return self._sumsq
 
     def step(self, grad_scale: float = 1.0, lr: Optional[float] = None):
