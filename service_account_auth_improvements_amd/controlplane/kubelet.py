@@ -259,9 +259,15 @@ class Kubelet(Controller):
         ctr = pod["spec"]["containers"][0]
         env = dict(os.environ)
         env.update(self.extra_env)
+        # single-host cluster DNS: a value naming a Service of the pod's namespace
+        # (e.g. MASTER_ADDR=<job>-master-0) resolves to this host
+        ns = pod["metadata"]["namespace"]
+        svcs = {s["metadata"]["name"] for s in self.client.list("v1", "Service", ns)}
         for e in ctr.get("env") or []:
             if "value" in e:
-                env[e["name"]] = str(e["value"])
+                v = str(e["value"])
+                host = v.split(".")[0]
+                env[e["name"]] = "127.0.0.1" if (v in svcs or (host in svcs and ".svc" in v)) else v
         if gpu_ids:
             env["HIP_VISIBLE_DEVICES"] = ",".join(map(str, gpu_ids))
         env["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"

@@ -109,6 +109,7 @@ class Manager:
         self.controllers: Dict[str, Controller] = {}
         self._queue: List[Tuple[str, Request]] = []
         self._queued: set = set()
+        self._processing: set = set()
         self._timers: List[Tuple[float, int, str, Request]] = []
         self._seq = 0
         self._cv = threading.Condition()
@@ -160,10 +161,22 @@ class Manager:
     def _process_one(self) -> bool:
         with self._cv:
             self._pop_due()
-            if not self._queue:
+            # a key is never reconciled by two workers at once (client-go workqueue
+            # "processing" set): skip keys in flight, they are re-queued as dirty
+            idx = next((i for i, it in enumerate(self._queue) if it not in self._processing), None)
+            if idx is None:
                 return False
-            cname, req = self._queue.pop(0)
+            cname, req = self._queue.pop(idx)
             self._queued.discard((cname, req))
+            self._processing.add((cname, req))
+        try:
+            return self._reconcile_one(cname, req)
+        finally:
+            with self._cv:
+                self._processing.discard((cname, req))
+                self._cv.notify()
+
+    def _reconcile_one(self, cname, req) -> bool:
         ctrl = self.controllers[cname]
         self.reconciles += 1
         try:

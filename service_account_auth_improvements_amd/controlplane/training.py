@@ -1,0 +1,335 @@
+"""PyTorchJob (kubeflow.org/v1) and MPIJob (kubeflow.org/v2beta1) operators -- the
+north-star job CRDs.  API-compatible with the training-operator /
+mpi-operator shapes, MI355X-native in what they put into pods:
+
+* every replica pod runs ``kfamd-launch`` (native/src/kfamd_launch.cpp) which spawns one
+  worker per GPU (``nprocPerNode``, default = the pod's ``amd.com/gpu`` limit), performs
+  the node-level rendezvous and supervises worker health;
+* per-replica env: ``MASTER_ADDR`` / ``MASTER_PORT`` (the master replica's headless
+  Service), ``WORLD_SIZE`` / ``RANK`` (node-level, training-operator convention) and the
+  ``PET_*`` torchrun variables consumed by the launcher, plus ``HSA_ENABLE_IPC_MODE_LEGACY=0``
+  for RCCL's dmabuf IPC.  ``HIP_VISIBLE_DEVICES`` is set by the node's device plugin from
+  the ``amd.com/gpu`` allocation -- no ``CUDA_VISIBLE_DEVICES`` / NVIDIA assumptions;
+* status: ``Created`` / ``Running`` / ``Restarting`` / ``Succeeded`` / ``Failed``
+  conditions, ``replicaStatuses``, ``startTime`` / ``completionTime``; ``runPolicy``
+  ``backoffLimit`` (pod restarts for ``OnFailure`` / ``ExitCode``) and ``cleanPodPolicy``.
+"""
+from __future__ import annotations
+
+import copy
+import logging
+import os
+import sys
+from typing import Dict, List, Optional
+
+from .apiserver import ApiError, now_rfc3339, set_controller_reference
+from .client import Client
+from .runtime import Controller, Request, Result, for_kind, owns
+
+log = logging.getLogger("training-operator")
+
+PT_API, MPI_API = "kubeflow.org/v1", "kubeflow.org/v2beta1"
+LBL_JOB = "training.kubeflow.org/job-name"
+LBL_RTYPE = "training.kubeflow.org/replica-type"
+LBL_RINDEX = "training.kubeflow.org/replica-index"
+LBL_ROLE = "training.kubeflow.org/job-role"
+DEFAULT_PORT = 23456
+GPU = "amd.com/gpu"
+
+
+def launcher_path() -> str:
+    from ..native import binary
+    return binary("kfamd_launch")
+
+
+def _cond(ctype, reason, msg):
+    t = now_rfc3339()
+    return {"type": ctype, "status": "True", "reason": reason, "message": msg,
+            "lastUpdateTime": t, "lastTransitionTime": t}
+
+
+def _set_condition(status: dict, ctype: str, reason: str, msg: str):
+    conds = status.setdefault("conditions", [])
+    for c in conds:
+        if c["type"] == ctype and c.get("status") == "True":
+            return
+    # Running / Restarting are mutually exclusive and end at a terminal condition
+    for c in conds:
+        if ctype in ("Succeeded", "Failed") and c["type"] in ("Running", "Restarting"):
+            c["status"] = "False"
+        if ctype == "Running" and c["type"] == "Restarting":
+            c["status"] = "False"
+        if ctype == "Restarting" and c["type"] == "Running":
+            c["status"] = "False"
+    conds.append(_cond(ctype, reason, msg))
+
+
+def _has(status: dict, ctype: str) -> bool:
+    return any(c["type"] == ctype and c.get("status") == "True" for c in status.get("conditions") or [])
+
+
+def _gpus(tpl: dict) -> int:
+    n = 0
+    for c in tpl.get("spec", {}).get("containers") or []:
+        v = ((c.get("resources") or {}).get("limits") or {}).get(GPU)
+        n += int(v) if v else 0
+    return n
+
+
+class _JobBase(Controller):
+    api = ""
+    kind = ""
+    specs_key = ""
+    job_label_kind = ""
+
+    def sources(self):
+        return [for_kind(self.api, self.kind), owns("v1", "Pod", self.kind)]
+
+    # --- pods / services
+    def _replica_order(self, specs: dict) -> List[str]:
+        raise NotImplementedError
+
+    def _pod_env(self, job, rtype, index, specs, tpl) -> List[dict]:
+        raise NotImplementedError
+
+    def _desired_pods(self, job: dict) -> List[dict]:
+        specs = job["spec"].get(self.specs_key) or {}
+        name, ns = job["metadata"]["name"], job["metadata"]["namespace"]
+        out = []
+        for rtype in self._replica_order(specs):
+            rs = specs[rtype]
+            for i in range(int(rs.get("replicas", 1))):
+                tpl = copy.deepcopy(rs["template"])
+                pn = f"{name}-{rtype.lower()}-{i}"
+                labels = dict(tpl.get("metadata", {}).get("labels") or {})
+                labels.update({LBL_JOB: name, LBL_RTYPE: rtype.lower(), LBL_RINDEX: str(i)})
+                if rtype in ("Master", "Launcher"):
+                    labels[LBL_ROLE] = "master"
+                spec = tpl.get("spec", {})
+                restart = rs.get("restartPolicy", "OnFailure")
+                spec["restartPolicy"] = "Never" if restart == "ExitCode" else (
+                    "OnFailure" if restart == "OnFailure" else restart)
+                env_add = self._pod_env(job, rtype, i, specs, tpl)
+                for c in spec.get("containers") or []:
+                    if c.get("name") in ("pytorch", "mpi", "launcher", "worker") or len(spec["containers"]) == 1:
+                        names = {e["name"] for e in c.get("env") or []}
+                        c["env"] = list(c.get("env") or []) + [e for e in env_add if e["name"] not in names]
+                pod = {"apiVersion": "v1", "kind": "Pod",
+                       "metadata": {"name": pn, "namespace": ns, "labels": labels,
+                                    "annotations": dict(tpl.get("metadata", {}).get("annotations") or {})},
+                       "spec": spec}
+                out.append(set_controller_reference(job, pod))
+        return out
+
+    def _service(self, job, pod) -> dict:
+        m = pod["metadata"]
+        return set_controller_reference(job, {
+            "apiVersion": "v1", "kind": "Service",
+            "metadata": {"name": m["name"], "namespace": m["namespace"], "labels": dict(m["labels"])},
+            "spec": {"clusterIP": "None", "selector": {LBL_JOB: m["labels"][LBL_JOB],
+                                                       LBL_RTYPE: m["labels"][LBL_RTYPE],
+                                                       LBL_RINDEX: m["labels"][LBL_RINDEX]},
+                     "ports": [{"name": f"{self.kind.lower()}-port", "port": self._port(job)}]}})
+
+    def _port(self, job) -> int:
+        return int((job.get("metadata", {}).get("annotations") or {}).get("kfamd.io/master-port", DEFAULT_PORT))
+
+    # --- reconcile
+    def reconcile(self, req: Request) -> Result:
+        c = self.client
+        job = c.get_or_none(self.api, self.kind, req.name, req.namespace)
+        if job is None or job["metadata"].get("deletionTimestamp"):
+            return Result()
+        status = copy.deepcopy(job.get("status") or {})
+        run_policy = job["spec"].get("runPolicy") or {}
+        if not _has(status, "Created"):
+            _set_condition(status, "Created", f"{self.kind}Created",
+                           f'{self.kind} {req.name} is created.')
+        terminal = _has(status, "Succeeded") or _has(status, "Failed")
+        pods = {p["metadata"]["name"]: p for p in c.list("v1", "Pod", req.namespace,
+                                                         label_selector=f"{LBL_JOB}={req.name}")}
+        desired = self._desired_pods(job)
+        if not terminal:
+            for pod in desired:
+                pn = pod["metadata"]["name"]
+                if pn not in pods:
+                    pods[pn] = c.create(pod)
+                if c.get_or_none("v1", "Service", pn, req.namespace) is None and self._wants_service(pod):
+                    c.create(self._service(job, pod))
+        # replica statuses
+        rstat: Dict[str, dict] = {}
+        restarts = int(status.get("restartCount", 0))
+        backoff = run_policy.get("backoffLimit")
+        failed_msg = None
+        specs = job["spec"].get(self.specs_key) or {}
+        for pod in desired:
+            rtype = next(k for k in specs if k.lower() == pod["metadata"]["labels"][LBL_RTYPE])
+            live = pods.get(pod["metadata"]["name"])
+            rs = rstat.setdefault(rtype, {"active": 0, "succeeded": 0, "failed": 0})
+            phase = (live or {}).get("status", {}).get("phase")
+            if phase == "Succeeded":
+                rs["succeeded"] += 1
+            elif phase == "Failed":
+                policy = specs[rtype].get("restartPolicy", "OnFailure")
+                code = self._exit_code(live)
+                retryable = policy == "OnFailure" or (policy == "ExitCode" and code is not None and code >= 128)
+                if retryable and not terminal and (backoff is None or restarts < int(backoff)):
+                    restarts += 1
+                    c.delete("v1", "Pod", live["metadata"]["name"], req.namespace)
+                    _set_condition(status, "Restarting", f"{self.kind}Restarting",
+                                   f'{self.kind} {req.name} is restarting because {rtype} replica(s) failed.')
+                    rs["active"] += 1
+                else:
+                    rs["failed"] += 1
+                    failed_msg = f'{self.kind} {req.name} has failed because {rtype} replica(s) failed.'
+            elif phase in ("Running", "Pending", None) and live is not None:
+                rs["active"] += 1
+        status["replicaStatuses"] = rstat
+        status["restartCount"] = restarts
+        if not terminal:
+            if failed_msg:
+                _set_condition(status, "Failed", f"{self.kind}Failed", failed_msg)
+                status["completionTime"] = now_rfc3339()
+            elif self._succeeded(rstat, specs):
+                _set_condition(status, "Succeeded", f"{self.kind}Succeeded",
+                               f'{self.kind} {req.name} is successfully completed.')
+                status["completionTime"] = now_rfc3339()
+            elif any(p.get("status", {}).get("phase") == "Running" for p in pods.values()):
+                if not _has(status, "Running"):
+                    _set_condition(status, "Running", f"{self.kind}Running", f'{self.kind} {req.name} is running.')
+                status.setdefault("startTime", now_rfc3339())
+        if _has(status, "Succeeded") or _has(status, "Failed"):
+            clean = run_policy.get("cleanPodPolicy", "None")
+            for p in pods.values():
+                ph = p.get("status", {}).get("phase")
+                if clean == "All" or (clean == "Running" and ph in ("Running", "Pending")):
+                    try:
+                        c.delete("v1", "Pod", p["metadata"]["name"], req.namespace)
+                    except ApiError:
+                        pass
+        if status != (job.get("status") or {}):
+            job["status"] = status
+            c.update_status(job)
+        return Result()
+
+    @staticmethod
+    def _exit_code(pod):
+        for cs in (pod or {}).get("status", {}).get("containerStatuses") or []:
+            t = (cs.get("state") or {}).get("terminated")
+            if t:
+                return int(t.get("exitCode", 1))
+        return None
+
+    def _wants_service(self, pod) -> bool:
+        return True
+
+    def _succeeded(self, rstat, specs) -> bool:
+        raise NotImplementedError
+
+
+class PyTorchJobReconciler(_JobBase):
+    name = "pytorchjob-controller"
+    api, kind, specs_key = PT_API, "PyTorchJob", "pytorchReplicaSpecs"
+
+    def _replica_order(self, specs):
+        return [k for k in ("Master", "Worker") if k in specs]
+
+    def _nproc(self, job, tpl) -> int:
+        v = job["spec"].get("nprocPerNode")
+        if v in (None, "auto", "gpu"):
+            return max(1, _gpus(tpl))
+        return int(v)
+
+    def _pod_env(self, job, rtype, index, specs, tpl):
+        name = job["metadata"]["name"]
+        master = f"{name}-master-0" if "Master" in specs else f"{name}-worker-0"
+        nnodes = sum(int(s.get("replicas", 1)) for s in specs.values())
+        rank = index if rtype == "Master" else index + (1 if "Master" in specs else 0)
+        port = self._port(job)
+        nproc = self._nproc(job, tpl)
+        return [{"name": "MASTER_ADDR", "value": master}, {"name": "MASTER_PORT", "value": str(port)},
+                {"name": "WORLD_SIZE", "value": str(nnodes)}, {"name": "RANK", "value": str(rank)},
+                {"name": "PET_MASTER_ADDR", "value": master}, {"name": "PET_MASTER_PORT", "value": str(port)},
+                {"name": "PET_NNODES", "value": str(nnodes)}, {"name": "PET_NODE_RANK", "value": str(rank)},
+                {"name": "PET_NPROC_PER_NODE", "value": str(nproc)},
+                {"name": "HSA_ENABLE_IPC_MODE_LEGACY", "value": "0"},
+                {"name": "PYTHONUNBUFFERED", "value": "1"}]
+
+    def _succeeded(self, rstat, specs):
+        if "Master" in specs:
+            return rstat.get("Master", {}).get("succeeded", 0) >= int(specs["Master"].get("replicas", 1))
+        w = specs.get("Worker", {})
+        return rstat.get("Worker", {}).get("succeeded", 0) >= int(w.get("replicas", 1))
+
+
+class MPIJobReconciler(_JobBase):
+    """MPIJob v2beta1: Launcher + Workers.  Workers run a kfamd-launch agent each (node
+    rank = replica index); the Launcher runs node 0's agent over the job's hostfile.
+    A ConfigMap ``<job>-config`` carries the ``hostfile`` (``slotsPerWorker`` slots each),
+    as mpi-operator does."""
+    name = "mpijob-controller"
+    api, kind, specs_key = MPI_API, "MPIJob", "mpiReplicaSpecs"
+
+    def _replica_order(self, specs):
+        return [k for k in ("Launcher", "Worker") if k in specs]
+
+    def _pod_env(self, job, rtype, index, specs, tpl):
+        name = job["metadata"]["name"]
+        slots = int(job["spec"].get("slotsPerWorker", 1))
+        nworkers = int(specs.get("Worker", {}).get("replicas", 0))
+        port = self._port(job)
+        base = [{"name": "OMPI_MCA_orte_default_hostfile", "value": "/etc/mpi/hostfile"},
+                {"name": "K_MPI_JOB_ROLE", "value": rtype.lower()},
+                {"name": "PET_MASTER_ADDR", "value": f"{name}-worker-0"},
+                {"name": "PET_MASTER_PORT", "value": str(port)},
+                {"name": "PET_NNODES", "value": str(max(nworkers, 1))},
+                {"name": "PET_NPROC_PER_NODE", "value": str(slots)},
+                {"name": "HSA_ENABLE_IPC_MODE_LEGACY", "value": "0"},
+                {"name": "PYTHONUNBUFFERED", "value": "1"}]
+        if rtype == "Worker":
+            base.append({"name": "PET_NODE_RANK", "value": str(index)})
+        return base
+
+    def reconcile(self, req: Request) -> Result:
+        job = self.client.get_or_none(self.api, self.kind, req.name, req.namespace)
+        if job is not None and not job["metadata"].get("deletionTimestamp"):
+            specs = job["spec"].get(self.specs_key) or {}
+            slots = int(job["spec"].get("slotsPerWorker", 1))
+            hosts = "".join(f"{req.name}-worker-{i}.{req.name}.{req.namespace}.svc slots={slots}\n"
+                            for i in range(int(specs.get("Worker", {}).get("replicas", 0))))
+            cm = set_controller_reference(job, {"apiVersion": "v1", "kind": "ConfigMap",
+                                                "metadata": {"name": f"{req.name}-config", "namespace": req.namespace},
+                                                "data": {"hostfile": hosts}})
+            cur = self.client.get_or_none("v1", "ConfigMap", cm["metadata"]["name"], req.namespace)
+            if cur is None:
+                self.client.create(cm)
+            elif cur.get("data") != cm["data"]:
+                cur["data"] = cm["data"]
+                self.client.update(cur)
+        return super().reconcile(req)
+
+    def _wants_service(self, pod):
+        return pod["metadata"]["labels"][LBL_RTYPE] == "worker"
+
+    def _succeeded(self, rstat, specs):
+        return rstat.get("Launcher", {}).get("succeeded", 0) >= 1
+
+
+def pytorchjob_manifest(name: str, namespace: str, image: str, command: List[str], n_nodes: int = 1,
+                        gpus_per_node: int = 8, master_port: Optional[int] = None,
+                        restart_policy: str = "OnFailure", backoff_limit: int = 3) -> dict:
+    """A PyTorchJob for the kfamd trainer: each replica runs kfamd-launch over its GPUs."""
+    def tpl():
+        return {"metadata": {"annotations": {"sidecar.istio.io/inject": "false"}},
+                "spec": {"containers": [{"name": "pytorch", "image": image,
+                                         "command": [launcher_path(), "--"] + list(command),
+                                         "resources": {"limits": {GPU: str(gpus_per_node)}} if gpus_per_node else {}}]}}
+    specs = {"Master": {"replicas": 1, "restartPolicy": restart_policy, "template": tpl()}}
+    if n_nodes > 1:
+        specs["Worker"] = {"replicas": n_nodes - 1, "restartPolicy": restart_policy, "template": tpl()}
+    ann = {"kfamd.io/master-port": str(master_port)} if master_port else {}
+    return {"apiVersion": PT_API, "kind": "PyTorchJob",
+            "metadata": {"name": name, "namespace": namespace, "annotations": ann},
+            "spec": {"nprocPerNode": str(gpus_per_node) if gpus_per_node else "1",
+                     "runPolicy": {"backoffLimit": backoff_limit, "cleanPodPolicy": "None"},
+                     "pytorchReplicaSpecs": specs}}

@@ -1,0 +1,85 @@
+"""Sharded safetensors checkpoints for the flat-buffer trainer (SURVEY.md §5 "Checkpoint /
+resume": bf16 params + fp32 master + AdamW moments, resume restores step and RNG).
+
+Layout of a checkpoint directory::
+
+    meta.json                      step, model config, parallel layout, per-file index
+    tp{t}-pp{p}-dp{d}.safetensors  one file per (tp, pp, dp) shard that owns unique state
+
+Each file holds the flat bf16 parameter buffers of its stage/TP shard (``param/<group>``)
+and its optimizer shard(s) (``opt/<group>/<lo>-<hi>/{master,m,v}``).  Without ZeRO only
+dp rank 0 writes (replicas are identical); with ZeRO-1 every dp rank writes its slices.
+Tensors are written straight from device memory via safetensors (no pickling), and are
+loaded with the safe loader only.
+"""
+from __future__ import annotations
+
+import json
+import os
+from typing import Optional
+
+import torch
+
+
+def _fname(st) -> str:
+    return f"tp{st.tp_rank}-pp{st.pp_rank}-dp{st.dp_rank}.safetensors"
+
+
+def save_checkpoint(path: str, trainer, extra: Optional[dict] = None):
+    from safetensors.torch import save_file
+    import torch.distributed as dist
+    st = trainer.st
+    os.makedirs(path, exist_ok=True)
+    opt = trainer.opt
+    writes_params = st.dp_rank == 0
+    writes_opt = opt.sharded or st.dp_rank == 0
+    tensors = {}
+    if writes_params:
+        for g in trainer.model.groups:
+            tensors[f"param/{g.name}"] = g.params.detach().contiguous()
+    if writes_opt:
+        for sh in opt.shards:
+            k = f"opt/{sh.group.name}/{sh.lo}-{sh.hi}"
+            tensors[k + "/master"] = sh.master
+            tensors[k + "/m"] = sh.m
+            tensors[k + "/v"] = sh.v
+    if tensors:
+        save_file({k: v.cpu() for k, v in tensors.items()}, os.path.join(path, _fname(st)))
+    if dist.is_initialized():
+        dist.barrier()
+    if st.rank == 0:
+        meta = {"step": opt.step_count, "model": trainer.mcfg.__dict__,
+                "parallel": {"tp": st.tp, "pp": st.pp, "dp": st.dp, "zero1": opt.sharded},
+                "torch_rng": torch.get_rng_state().tolist()[:16], "format": "kfamd-flat-v1"}
+        meta.update(extra or {})
+        with open(os.path.join(path, "meta.json"), "w") as f:
+            json.dump(meta, f)
+    if dist.is_initialized():
+        dist.barrier()
+
+
+def load_checkpoint(path: str, trainer) -> dict:
+    from safetensors.torch import load_file
+    st = trainer.st
+    with open(os.path.join(path, "meta.json")) as f:
+        meta = json.load(f)
+    p = meta["parallel"]
+    if (p["tp"], p["pp"]) != (st.tp, st.pp):
+        raise ValueError(f"checkpoint layout tp{p['tp']}/pp{p['pp']} != current tp{st.tp}/pp{st.pp}")
+    dev = trainer.model.groups[0].params.device
+    pfile = os.path.join(path, f"tp{st.tp_rank}-pp{st.pp_rank}-dp0.safetensors")
+    ptens = load_file(pfile, device="cpu")
+    for g in trainer.model.groups:
+        g.params.copy_(ptens[f"param/{g.name}"].to(dev))
+    opt = trainer.opt
+    ofile = os.path.join(path, _fname(st) if p.get("zero1") else os.path.basename(pfile))
+    otens = ptens if ofile == pfile else load_file(ofile, device="cpu")
+    for sh in opt.shards:
+        k = f"opt/{sh.group.name}/{sh.lo}-{sh.hi}"
+        if k + "/master" not in otens:
+            raise KeyError(f"optimizer shard {k} not in {ofile}")
+        sh.master.copy_(otens[k + "/master"].to(dev))
+        sh.m.copy_(otens[k + "/m"].to(dev))
+        sh.v.copy_(otens[k + "/v"].to(dev))
+    opt.step_count = int(meta["step"])
+    return meta

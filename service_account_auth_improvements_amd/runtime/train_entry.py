@@ -1,0 +1,98 @@
+"""Worker entry point run inside PyTorchJob / MPIJob pods (one process per GPU, started by
+kfamd-launch).  Emits JSON event lines (``first_step`` carries the wall-clock timestamp
+used for the CRD-to-first-step metric), touches the launcher heartbeat file every step,
+and saves a sharded checkpoint at the end when asked.
+
+  python -m service_account_auth_improvements_amd.runtime.train_entry \
+      --model llama3-8b --seq-len 8192 --micro-batch 2 --steps 100
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+
+def _event(kind: str, **kw):
+    rec = {"event": kind, "ts": time.time(), "rank": int(os.environ.get("RANK", "0")), **kw}
+    line = json.dumps(rec)
+    print(line, flush=True)
+    path = os.environ.get("KFAMD_EVENTS_FILE")
+    if path:
+        with open(path, "a") as f:
+            f.write(line + "\n")
+
+
+def _heartbeat():
+    hb = os.environ.get("KFAMD_HEARTBEAT_FILE")
+    if hb:
+        with open(hb, "a"):
+            os.utime(hb, None)
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--seq-len", type=int, default=8192)
+    ap.add_argument("--micro-batch", type=int, default=1)
+    ap.add_argument("--grad-accum", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--tp", type=int, default=1)
+    ap.add_argument("--pp", type=int, default=1)
+    ap.add_argument("--zero1", action="store_true")
+    ap.add_argument("--layers", type=int, default=None)
+    ap.add_argument("--device", default="auto", choices=["auto", "cpu", "cuda"])
+    ap.add_argument("--save", default=None, help="checkpoint directory written at the end")
+    ap.add_argument("--resume", default=None, help="checkpoint directory to resume from")
+    a = ap.parse_args(argv)
+
+    t_start = time.time()
+    _event("process_start")
+    import torch
+    from ..parallel.state import init_distributed
+    from .trainer import SyntheticData, TrainConfig, Trainer
+
+    dev = None if a.device == "auto" else a.device
+    if dev == "cuda" or (dev is None and torch.cuda.is_available()):
+        dev = "cuda"
+    else:
+        dev = "cpu"
+    st = init_distributed(tp=a.tp, pp=a.pp, device=dev)
+    tcfg = TrainConfig(model=a.model, seq_len=a.seq_len, micro_batch=a.micro_batch, grad_accum=a.grad_accum,
+                       zero1=a.zero1, n_layers=a.layers)
+    if a.pp > 1:
+        from ..parallel.pipeline import PipelineTrainer
+        tr = PipelineTrainer(tcfg, st)
+    else:
+        tr = Trainer(tcfg, st)
+    if a.resume:
+        from .checkpoint import load_checkpoint
+        load_checkpoint(a.resume, tr)
+    data = SyntheticData(tr.mcfg.vocab_size, a.micro_batch, a.seq_len, st.device, seed=17, rank=st.dp_rank)
+    _event("init_done", seconds=time.time() - t_start)
+    for step in range(a.steps):
+        batch = [data.next() for _ in range(a.grad_accum)]
+        loss = tr.train_step(batch)
+        if st.device.type == "cuda":
+            torch.cuda.synchronize()
+        lv = float(loss) if loss is not None else None
+        if step == 0:
+            _event("first_step", loss=lv)
+        _event("step", step=step, loss=lv)
+        _heartbeat()
+    if a.save:
+        from .checkpoint import save_checkpoint
+        save_checkpoint(a.save, tr)
+        _event("checkpoint_saved", path=a.save)
+    _event("done")
+    import torch.distributed as dist
+    if dist.is_initialized():
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
