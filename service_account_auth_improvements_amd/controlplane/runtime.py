@@ -138,6 +138,12 @@ class Manager:
                 for req in src.mapper(et, obj):
                     self.enqueue(cname, req)
             self._cancels.append(self.client.watch(handler, src.api_version, src.kind))
+            # informer initial LIST: objects that existed before the watch started
+            try:
+                for obj in self.client.list(src.api_version, src.kind):
+                    handler("ADDED", obj)
+            except ApiError:
+                pass
         return self
 
     def enqueue(self, cname: str, req: Request, after: float = 0.0):
