@@ -62,7 +62,7 @@ class LlamaConfig:
                                n_kv_heads=8, ffn=28672)
         if name in ("tiny", "llama3-tiny"):
             return LlamaConfig(name="llama3-tiny", vocab_size=512, hidden=256, n_layers=2,
-                               n_heads=4, n_kv_heads=2, head_dim=64, ffn=512, max_seq=256)
+                               n_heads=4, n_kv_heads=2, head_dim=128, ffn=512, max_seq=256)
         if name in ("small", "llama3-small"):
             return LlamaConfig(name="llama3-small", vocab_size=32000, hidden=1024, n_layers=4,
                                n_heads=8, n_kv_heads=2, head_dim=128, ffn=3584, max_seq=2048)

@@ -9,12 +9,12 @@ def cat(n):
     if n.startswith('Cijk') or 'Custom_Cijk' in n: return 'GEMM (hipBLASLt)'
     if 'flash_fwd' in n: return 'attention fwd (HIP)'
     if 'flash_bwd' in n: return 'attention bwd (HIP)'
-    if 'attn_fwd' in n or 'bwd_kernel' in n or 'bwd_preprocess' in n: return 'attention (SDPA/AOTriton)'
     if 'adamw' in n or 'sumsq' in n or 'sum_final' in n: return 'optimizer (HIP)'
     if 'rmsnorm' in n or 'colsum' in n: return 'rmsnorm (HIP)'
     if 'swiglu' in n: return 'swiglu (HIP)'
     if 'rope' in n: return 'rope (HIP)'
     if 'ce_kernel' in n: return 'cross-entropy (HIP)'
+    if 'attn_fwd' in n or 'bwd_kernel' in n or 'bwd_preprocess' in n: return 'attention (SDPA/AOTriton)'
     return 'other (torch/runtime)'
 for r in rows:
     c = cat(r['Name']); cats[c] = cats.get(c, 0) + float(r['TotalDurationNs'])
