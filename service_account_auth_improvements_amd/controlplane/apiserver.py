@@ -468,6 +468,9 @@ class APIServer:
         obj = copy.deepcopy(obj)
         t = self.type_for(obj.get("apiVersion", ""), obj.get("kind", ""))
         meta = obj.setdefault("metadata", {})
+        if t.kind == "SubjectAccessReview":   # virtual: evaluated, never stored
+            obj["status"] = self.evaluate_sar(obj.get("spec", {}))
+            return obj
         with self._lock:
             if not meta.get("name"):
                 gen = meta.get("generateName")
@@ -485,9 +488,6 @@ class APIServer:
                     raise Forbidden(f"namespace {ns} is being terminated")
             else:
                 meta.pop("namespace", None)
-            if t.kind == "SubjectAccessReview":
-                obj["status"] = self.evaluate_sar(obj.get("spec", {}))
-                return obj
             bucket = self._bucket(t)
             key = self._key(t, ns, meta["name"])
             if key in bucket:
