@@ -1,0 +1,113 @@
+"""Central dashboard API (reference: components/centraldashboard/app/api_test.ts,
+api_workgroup_test.ts, attach_user_middleware_test.ts) against in-process KFAM."""
+import json
+
+import pytest
+
+from service_account_auth_improvements_amd.controlplane.apiserver import APIServer
+from service_account_auth_improvements_amd.controlplane.client import InMemoryClient
+from service_account_auth_improvements_amd.controlplane.kfam import Kfam
+from service_account_auth_improvements_amd.webapps import dashboard
+
+HDR = "X-Goog-Authenticated-User-Email"
+PFX = "accounts.google.com:"
+
+
+def _as(u):
+    return {HDR: PFX + u}
+
+
+@pytest.fixture
+def dash():
+    from prometheus_client import CollectorRegistry
+    srv = APIServer()
+    c = InMemoryClient(srv)
+    c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "kubeflow"}})
+    c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "alice"}})
+    c.create({"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "centraldashboard-config",
+                                                                    "namespace": "kubeflow"},
+              "data": {"links": json.dumps({"menuLinks": [{"link": "/jupyter/", "text": "Notebooks"}]}),
+                       "settings": json.dumps({"DASHBOARD_FORCE_IFRAME": True})}})
+    c.create({"apiVersion": "kubeflow.org/v1beta1", "kind": "Profile", "metadata": {"name": "alice"},
+              "spec": {"owner": {"kind": "User", "name": "alice@example.com"}}})
+    kf = Kfam(c, cluster_admin="root@example.com", registry=CollectorRegistry()).app().test_client()
+
+    def transport(method, path, body, headers):
+        r = kf.open("/kfam" + path, method=method, data=body, headers=headers)
+        return r.status_code, r.data
+
+    # the owner binding the profile controller would create (namespaceAdmin is not KFAM-annotated,
+    # so add an annotated owner binding the way KFAM does)
+    prof = dashboard.ProfilesService(transport)
+    prof.create_binding({"user": {"kind": "User", "name": "alice@example.com"}, "referredNamespace": "alice",
+                         "roleRef": {"kind": "ClusterRole", "name": "admin"}}, _as("alice@example.com"))
+    m = dashboard.LocalMetricsService(start=False)
+    m.sample()
+    app = dashboard.create_app(c, prof, m, env={}).test_client()
+    return c, app
+
+
+def test_env_info_and_exists(dash):
+    c, app = dash
+    info = app.get("/api/workgroup/env-info", headers=_as("alice@example.com")).json
+    assert info["user"] == "alice@example.com" and info["isClusterAdmin"] is False
+    assert info["namespaces"] == [{"user": "alice@example.com", "namespace": "alice", "role": "owner"}]
+    assert info["platform"]["providerName"] == "other"
+    ex = app.get("/api/workgroup/exists", headers=_as("alice@example.com")).json
+    assert ex == {"hasAuth": True, "user": "alice", "hasWorkgroup": True, "registrationFlowAllowed": True}
+    anon = app.get("/api/workgroup/exists").json
+    assert anon["hasAuth"] is False and anon["user"] == "anonymous"
+    assert app.get("/api/workgroup/get-all-namespaces").status_code == 405
+
+
+def test_contributors_flow(dash):
+    c, app = dash
+    h = _as("alice@example.com")
+    r = app.post("/api/workgroup/add-contributor/alice", json={"contributor": "bob@example.com"}, headers=h)
+    assert r.status_code == 200 and r.json == ["bob@example.com"]
+    assert app.get("/api/workgroup/get-contributors/alice", headers=h).json == ["bob@example.com"]
+    tab = app.get("/api/workgroup/get-all-namespaces", headers=h).json
+    assert tab == [["alice", "alice@example.com", "bob@example.com"]]
+    r = app.post("/api/workgroup/add-contributor/alice", json={"contributor": "not-an-email"}, headers=h)
+    assert r.status_code == 400 and "valid email" in r.json["error"]
+    r = app.post("/api/workgroup/add-contributor/alice", json={}, headers=h)
+    assert r.json["error"] == "Missing contributor field."
+    # a non-owner cannot add (KFAM 403 surfaced)
+    r = app.post("/api/workgroup/add-contributor/alice", json={"contributor": "eve@example.com"},
+                 headers=_as("mallory@example.com"))
+    assert r.status_code == 403
+    r = app.delete("/api/workgroup/remove-contributor/alice", json={"contributor": "bob@example.com"}, headers=h)
+    assert r.status_code == 200 and r.json == []
+
+
+def test_create_and_nuke_profile(dash):
+    c, app = dash
+    h = _as("carol@example.com")
+    assert app.post("/api/workgroup/create", json={}, headers=h).json == {"message": "Created namespace carol"}
+    assert c.get("kubeflow.org/v1beta1", "Profile", "carol")["spec"]["owner"]["name"] == "carol@example.com"
+    r = app.delete("/api/workgroup/nuke-self", headers=h)
+    assert r.status_code == 200 and c.get_or_none("kubeflow.org/v1beta1", "Profile", "carol") is None
+
+
+def test_api_misc(dash):
+    c, app = dash
+    assert app.get("/api/dashboard-links").json["menuLinks"][0]["link"] == "/jupyter/"
+    assert app.get("/api/dashboard-settings").json == {"DASHBOARD_FORCE_IFRAME": True}
+    assert [n["metadata"]["name"] for n in app.get("/api/namespaces").json] == ["alice", "kubeflow"]
+    assert app.get("/api/nope").status_code == 404
+    assert app.get("/healthz").json["message"] == "I tick, therfore I am!"
+    node = app.get("/api/metrics/node?interval=Last5m").json
+    assert len(node) == 1 and node[0]["label"] == "instance=localhost"
+    assert app.get("/api/metrics").json["resourceChartsLinkText"] == "View in dashboard"
+
+
+def test_prometheus_metrics_service():
+    payload = {"status": "success", "data": {"resultType": "matrix", "result": [
+        {"metric": {"instance": "n1"}, "values": [[1700000000, "50"], [1700000010, "25"]]}]}}
+    seen = []
+    svc = dashboard.PrometheusMetricsService("http://prom:9090", "http://grafana",
+                                             fetch=lambda u: (seen.append(u), json.dumps(payload).encode())[1])
+    pts = svc.node_cpu(15)
+    assert pts == [{"timestamp": 1700000000.0, "label": "instance=n1", "value": 0.5},
+                   {"timestamp": 1700000010.0, "label": "instance=n1", "value": 0.25}]
+    assert "node_cpu_seconds_total" in seen[0] and "step=10" in seen[0]
