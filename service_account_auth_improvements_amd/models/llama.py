@@ -137,9 +137,9 @@ class Llama:
         self.sin = sin.to(self.device)
 
     # ------------------------------------------------------------------ storage
-    def allocate(self, pad_to: int = 1):
+    def allocate(self, pad_to: int = 1, grads: bool = True):
         for g in self.groups:
-            g.allocate(self.device, pad_to=pad_to)
+            g.allocate(self.device, pad_to=pad_to, grads=grads)
         self._init()
         return self
 

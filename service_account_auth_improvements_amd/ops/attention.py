@@ -92,23 +92,44 @@ def attention(qkv, B, S, Hq, Hkv, D, causal=True):
     return _AttnFn.apply(qkv, B, S, Hq, Hkv, D, causal)
 
 
-def decode_attention(q, k_cache, v_cache, lengths, scale=None):
-    """Single-query GQA attention over a KV cache (K8, InferenceService decode).
+def decode_attention(q2d, k_cache, v_cache, slots, lengths, Hq, scale=None):
+    """Single-query GQA attention over a slot-major KV cache (K8, InferenceService decode).
 
-    q [B, Hq, D]; k_cache/v_cache [B, Lmax, Hkv, D]; lengths int32 [B] (valid keys per
-    sequence, including the current token). Returns o [B, Hq, D]."""
-    B, Hq, D = q.shape
+    q2d [B, >=Hq*D] rows (the q columns of fused qkv rows are used in place);
+    k_cache/v_cache [n_slots, Hkv, Lmax, D]; slots/lengths int32 [B] (cache slot of each
+    row and its number of valid keys, including the current token). Returns [B, Hq*D]."""
+    D = k_cache.shape[3]
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
-    if q.is_cuda:
-        return _ext.ops().decode_attn(q.contiguous(), k_cache, v_cache, lengths, scale)
-    Hkv = k_cache.shape[2]
+    if q2d.is_cuda:
+        return _ext.ops().decode_attn(q2d, k_cache, v_cache, slots, lengths, Hq, scale)
+    B, Hkv = q2d.shape[0], k_cache.shape[1]
     rep = Hq // Hkv
-    out = torch.empty_like(q)
+    out = torch.empty(B, Hq * D, dtype=q2d.dtype)
     for b in range(B):
-        L = int(lengths[b])
-        k = k_cache[b, :L].float().permute(1, 0, 2).repeat_interleave(rep, 0)  # [Hq, L, D]
-        v = v_cache[b, :L].float().permute(1, 0, 2).repeat_interleave(rep, 0)
-        s = torch.einsum("hd,hld->hl", q[b].float(), k) * scale
-        p = torch.softmax(s, -1)
-        out[b] = torch.einsum("hl,hld->hd", p, v).to(q.dtype)
+        L, sl = int(lengths[b]), int(slots[b])
+        q = q2d[b, : Hq * D].float().view(Hq, D)
+        k = k_cache[sl, :, :L].float().repeat_interleave(rep, 0)   # [Hq, L, D]
+        v = v_cache[sl, :, :L].float().repeat_interleave(rep, 0)
+        p = torch.softmax(torch.einsum("hd,hld->hl", q, k) * scale, -1)
+        out[b] = torch.einsum("hl,hld->hd", p, v).reshape(-1).to(q2d.dtype)
     return out
+
+
+def kv_append_(qkv, Hq, slots, pos, k_cache, v_cache):
+    """Write each row's (post-RoPE) K/V into position pos[b] of slot slots[b]."""
+    if qkv.is_cuda:
+        return _ext.ops().kv_append_(qkv, Hq, slots, pos, k_cache, v_cache)
+    Hkv, D = k_cache.shape[1], k_cache.shape[3]
+    for b in range(qkv.shape[0]):
+        sl, p = int(slots[b]), int(pos[b])
+        k_cache[sl, :, p] = qkv[b, Hq * D:(Hq + Hkv) * D].view(Hkv, D)
+        v_cache[sl, :, p] = qkv[b, (Hq + Hkv) * D:(Hq + 2 * Hkv) * D].view(Hkv, D)
+
+
+def kv_fill_(qkv, S, Hq, slot, k_cache, v_cache):
+    """Prefill: rows [0, S) of one sequence's fused qkv -> positions [0, S) of `slot`."""
+    if qkv.is_cuda:
+        return _ext.ops().kv_fill_(qkv, S, Hq, slot, k_cache, v_cache)
+    Hkv, D = k_cache.shape[1], k_cache.shape[3]
+    k_cache[slot, :, :S] = qkv[:S, Hq * D:(Hq + Hkv) * D].reshape(S, Hkv, D).transpose(0, 1)
+    v_cache[slot, :, :S] = qkv[:S, (Hq + Hkv) * D:(Hq + 2 * Hkv) * D].reshape(S, Hkv, D).transpose(0, 1)

@@ -32,8 +32,12 @@ int kf_flash_fwd(const void*, long, void*, long, float*, int, int, int, int, int
                  hipStream_t);
 int kf_flash_bwd(const void*, long, const void*, long, const void*, long, const float*, float*,
                  float*, float*, void*, long, int, int, int, int, int, float, int, hipStream_t);
-int kf_decode_attn(const void*, const void*, const void*, const int*, void*, float*, int, int, int,
-                   int, int, long, long, long, long, float, int, hipStream_t);
+int kf_decode_splits(int, int, int);
+int kf_decode_attn(const void*, long, const void*, const void*, const int*, const int*, void*, long,
+                   float*, float*, int, int, int, int, int, int, float, hipStream_t);
+int kf_kv_append(const void*, long, int, int, int, int, const int*, const int*, void*, void*, int,
+                 hipStream_t);
+int kf_kv_fill(const void*, long, int, int, int, int, int, void*, void*, int, hipStream_t);
 }
 
 namespace {
@@ -252,6 +256,72 @@ at::Tensor flash_bwd(const at::Tensor& qkv, const at::Tensor& o, const at::Tenso
   return dqkv;
 }
 
+// ---------------- decode attention + KV cache (InferenceService) ----------------
+void check_cache(const at::Tensor& kc, const at::Tensor& vc, int64_t Hkv, int64_t D) {
+  check_bf16_cuda(kc, "k_cache");
+  check_bf16_cuda(vc, "v_cache");
+  TORCH_CHECK(kc.dim() == 4 && kc.is_contiguous() && vc.sizes() == kc.sizes() && vc.is_contiguous(),
+              "kv cache must be contiguous [slots, Hkv, Lmax, D]");
+  TORCH_CHECK(kc.size(1) == Hkv && kc.size(3) == D && D == 128, "kv cache: head shape mismatch (D=128)");
+}
+void check_rows_i32(const at::Tensor& t, int64_t B, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kInt && t.is_contiguous() && t.numel() == B, name,
+              " must be int32 [B] on the GPU");
+}
+
+// q2d: [B, >=Hq*D] rows (e.g. the q columns of fused qkv rows). Returns o [B, Hq*D].
+at::Tensor decode_attn(const at::Tensor& q2d, const at::Tensor& kc, const at::Tensor& vc,
+                       const at::Tensor& slots, const at::Tensor& lengths, int64_t Hq, double scale) {
+  check_bf16_cuda(q2d, "q");
+  TORCH_CHECK(q2d.dim() == 2 && q2d.stride(1) == 1, "decode_attn: q must be 2-D row-major");
+  const int64_t B = q2d.size(0), Hkv = kc.size(1), D = kc.size(3), Lmax = kc.size(2);
+  check_cache(kc, vc, Hkv, D);
+  TORCH_CHECK(q2d.size(1) >= Hq * D && Hq % Hkv == 0 && Hq / Hkv <= 8, "decode_attn: q heads");
+  check_rows_i32(slots, B, "slots");
+  check_rows_i32(lengths, B, "lengths");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(q2d.device());
+  const int splits = kf_decode_splits((int)B, (int)Hkv, (int)Lmax);
+  auto f32 = q2d.options().dtype(at::kFloat);
+  auto po = at::empty({B * Hq * splits * D}, f32);
+  auto pml = at::empty({B * Hq * splits * 2}, f32);
+  auto out = at::empty({B, Hq * D}, q2d.options());
+  check_rc(kf_decode_attn(q2d.data_ptr(), q2d.stride(0), kc.data_ptr(), vc.data_ptr(), slots.data_ptr<int>(),
+                          lengths.data_ptr<int>(), out.data_ptr(), out.stride(0), po.data_ptr<float>(),
+                          pml.data_ptr<float>(), (int)B, (int)Hq, (int)Hkv, (int)D, (int)Lmax, splits,
+                          (float)scale, cur_stream()),
+           "decode_attn");
+  return out;
+}
+
+// Append one token per row (K/V columns of fused qkv rows) at pos[b] of slot slots[b].
+void kv_append_(const at::Tensor& qkv, int64_t Hq, const at::Tensor& slots, const at::Tensor& pos,
+                at::Tensor& kc, at::Tensor& vc) {
+  check_bf16_cuda(qkv, "qkv");
+  const int64_t B = qkv.size(0), Hkv = kc.size(1), D = kc.size(3);
+  check_cache(kc, vc, Hkv, D);
+  TORCH_CHECK(qkv.dim() == 2 && qkv.stride(1) == 1 && qkv.size(1) >= (Hq + 2 * Hkv) * D, "kv_append: qkv");
+  check_rows_i32(slots, B, "slots");
+  check_rows_i32(pos, B, "pos");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(qkv.device());
+  check_rc(kf_kv_append(qkv.data_ptr(), qkv.stride(0), (int)B, (int)Hq, (int)Hkv, (int)D, slots.data_ptr<int>(),
+                        pos.data_ptr<int>(), kc.data_ptr(), vc.data_ptr(), (int)kc.size(2), cur_stream()),
+           "kv_append");
+}
+
+// Prefill: rows [0, S) of one sequence's fused qkv -> positions [0, S) of `slot`.
+void kv_fill_(const at::Tensor& qkv, int64_t S, int64_t Hq, int64_t slot, at::Tensor& kc, at::Tensor& vc) {
+  check_bf16_cuda(qkv, "qkv");
+  const int64_t Hkv = kc.size(1), D = kc.size(3);
+  check_cache(kc, vc, Hkv, D);
+  TORCH_CHECK(qkv.dim() == 2 && qkv.stride(1) == 1 && qkv.size(0) >= S && qkv.size(1) >= (Hq + 2 * Hkv) * D,
+              "kv_fill: qkv");
+  TORCH_CHECK(slot >= 0 && slot < kc.size(0) && S <= kc.size(2), "kv_fill: slot/length out of range");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(qkv.device());
+  check_rc(kf_kv_fill(qkv.data_ptr(), qkv.stride(0), (int)S, (int)Hq, (int)Hkv, (int)D, (int)slot, kc.data_ptr(),
+                      vc.data_ptr(), (int)kc.size(2), cur_stream()),
+           "kv_fill");
+}
+
 }  // namespace
 
 TORCH_LIBRARY(kfamd, m) {
@@ -265,4 +335,7 @@ TORCH_LIBRARY(kfamd, m) {
   m.def("cross_entropy_", &cross_entropy_);
   m.def("flash_fwd", &flash_fwd);
   m.def("flash_bwd", &flash_bwd);
+  m.def("decode_attn", &decode_attn);
+  m.def("kv_append_(Tensor qkv, int Hq, Tensor slots, Tensor pos, Tensor(a!) kc, Tensor(b!) vc) -> ()", &kv_append_);
+  m.def("kv_fill_(Tensor qkv, int S, int Hq, int slot, Tensor(a!) kc, Tensor(b!) vc) -> ()", &kv_fill_);
 }

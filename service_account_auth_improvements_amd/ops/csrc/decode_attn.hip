@@ -1,0 +1,276 @@
+// K8: single-query GQA decode attention over a slot-major KV cache (InferenceService).
+//
+// Cache layout per layer: k/v [n_slots, Hkv, Lmax, 128] bf16 -- one contiguous 256-byte
+// row per (slot, head, position), so a head's keys stream linearly from HBM.  Each decode
+// row b reads the slot slots[b] up to lengths[b] keys.  288 GB of HBM holds ~2M tokens of
+// Llama-3-8B KV (128 KB/token), so slots are preallocated at full context length and no
+// paging indirection sits on the memory-bound path.
+//
+// Split-K ("flash decoding"): grid (splits, Hkv, B), 256 threads.  One workgroup owns one
+// (row, kv head, key chunk) and serves all G = Hq/Hkv query heads of the group, so every
+// K/V byte is read exactly once.  A 16-lane quarter-wave owns one key row (16 lanes x 16 B);
+// a wave covers 4 keys per load, the block 16.
+//   phase 1: s[h][j] = q_h . k_j (fp32, log2 domain) -> LDS
+//   phase 2: per head max / exp2 / sum over the chunk (one wave per head)
+//   phase 3: o[h] += p[h][j] v_j with 16 independent key streams, reduced via LDS
+// Partial (o, m, l) per split go to an fp32 workspace; decode_combine merges the splits.
+// Decode is HBM-bound (2 flops/byte), so VALU dot products are the right tool: MFMA would
+// pad the G<=8 query rows to 16/32 and buy nothing.
+#include "common.h"
+
+using namespace kf;
+
+namespace {
+
+constexpr int D = 128;
+constexpr int NT = 256;
+constexpr int MAXG = 8;
+constexpr int MAXCHUNK = 1024;
+constexpr float LOG2E = 1.4426950408889634f;
+
+template <int G>
+__global__ __launch_bounds__(NT) void decode_split_kernel(
+    const bf16_t* __restrict__ q, long q_ld, int hq_total,
+    const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
+    const int* __restrict__ slots, const int* __restrict__ lengths,
+    long slot_stride, long head_stride, int splits, float scale_log2,
+    float* __restrict__ part_o, float* __restrict__ part_ml) {
+  __shared__ float sc[G][MAXCHUNK];
+  __shared__ float red[4][G][D];
+  __shared__ float hm[G], hl[G];
+
+  const int s = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int sub = lane & 15;            // 16-byte column within the key row
+  const int grp = tid >> 4;             // 0..15: key stream within the block
+  const int len = min(lengths[b], (int)(head_stride / D));   // never read past the slot
+  const int chunk = ((len + splits - 1) / splits + 15) & ~15;
+  const int start = s * chunk;
+  const int end = min(len, start + chunk);
+  const long obase = ((long)b * hq_total + (long)hk * G) * splits + s;   // index of (b, h0, s)
+
+  if (start >= end) {   // empty split: neutral element for the combine
+    if (tid < G) {
+      part_ml[(obase + (long)tid * splits) * 2 + 0] = -INFINITY;
+      part_ml[(obase + (long)tid * splits) * 2 + 1] = 0.f;
+    }
+    return;
+  }
+  const int n = end - start;
+
+  // q for the G heads of this kv head: 8 dims per lane, pre-scaled into the log2 domain
+  float qf[G][8];
+#pragma unroll
+  for (int h = 0; h < G; ++h) {
+    const u32x4 v = ld16(q + (long)b * q_ld + (long)(hk * G + h) * D + sub * 8);
+    unpack8(v, qf[h]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) qf[h][i] *= scale_log2;
+  }
+
+  const long kvbase = (long)slots[b] * slot_stride + (long)hk * head_stride;
+  const bf16_t* kp = kc + kvbase;
+  const bf16_t* vp = vc + kvbase;
+
+  // ---- phase 1: scores
+  for (int j0 = 0; j0 < n; j0 += 16) {
+    const int j = j0 + grp;
+    float kf_[8];
+    if (j < n) {
+      unpack8(ld16(kp + (long)(start + j) * D + sub * 8), kf_);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) kf_[i] = 0.f;
+    }
+#pragma unroll
+    for (int h = 0; h < G; ++h) {
+      float a = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a = fmaf(qf[h][i], kf_[i], a);
+      a += __shfl_xor(a, 1, 64);
+      a += __shfl_xor(a, 2, 64);
+      a += __shfl_xor(a, 4, 64);
+      a += __shfl_xor(a, 8, 64);
+      if (sub == 0 && j < n) sc[h][j] = a;
+    }
+  }
+  __syncthreads();
+
+  // ---- phase 2: softmax statistics per head (wave w handles heads w, w+4)
+  for (int h = wave; h < G; h += 4) {
+    float m = -INFINITY;
+    for (int j = lane; j < n; j += 64) m = fmaxf(m, sc[h][j]);
+    m = wave_max(m);
+    float l = 0.f;
+    for (int j = lane; j < n; j += 64) {
+      const float p = exp2f(sc[h][j] - m);
+      sc[h][j] = p;
+      l += p;
+    }
+    l = wave_sum(l);
+    if (lane == 0) { hm[h] = m; hl[h] = l; }
+  }
+  __syncthreads();
+
+  // ---- phase 3: P.V with 16 key streams
+  float acc[G][8];
+#pragma unroll
+  for (int h = 0; h < G; ++h)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[h][i] = 0.f;
+  for (int j = grp; j < n; j += 16) {
+    float vf[8];
+    unpack8(ld16(vp + (long)(start + j) * D + sub * 8), vf);
+#pragma unroll
+    for (int h = 0; h < G; ++h) {
+      const float p = sc[h][j];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[h][i] = fmaf(p, vf[i], acc[h][i]);
+    }
+  }
+  // reduce the 4 streams of a wave (lanes l, l^16, l^32, l^48 share a column)
+#pragma unroll
+  for (int h = 0; h < G; ++h)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float a = acc[h][i];
+      a += __shfl_xor(a, 16, 64);
+      a += __shfl_xor(a, 32, 64);
+      acc[h][i] = a;
+    }
+  if (lane < 16) {
+#pragma unroll
+    for (int h = 0; h < G; ++h)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) red[wave][h][sub * 8 + i] = acc[h][i];
+  }
+  __syncthreads();
+  for (int e = tid; e < G * D; e += NT) {
+    const int h = e / D, d = e % D;
+    const float o = red[0][h][d] + red[1][h][d] + red[2][h][d] + red[3][h][d];
+    part_o[(obase + (long)h * splits) * D + d] = o;
+  }
+  if (tid < G) {
+    part_ml[(obase + (long)tid * splits) * 2 + 0] = hm[tid];
+    part_ml[(obase + (long)tid * splits) * 2 + 1] = hl[tid];
+  }
+}
+
+// one block per (b, q head): merge the split partials, normalise, write bf16
+__global__ __launch_bounds__(D) void decode_combine_kernel(const float* __restrict__ part_o,
+                                                           const float* __restrict__ part_ml,
+                                                           int splits, bf16_t* __restrict__ out,
+                                                           long out_ld, int hq) {
+  const int bh = blockIdx.x, d = threadIdx.x;
+  const int b = bh / hq, h = bh % hq;
+  const float* ml = part_ml + (long)bh * splits * 2;
+  float M = -INFINITY;
+  for (int s = 0; s < splits; ++s) M = fmaxf(M, ml[2 * s]);
+  float num = 0.f, den = 0.f;
+  for (int s = 0; s < splits; ++s) {
+    const float m = ml[2 * s];
+    if (m == -INFINITY) continue;
+    const float w = exp2f(m - M);
+    num = fmaf(w, part_o[((long)bh * splits + s) * D + d], num);
+    den = fmaf(w, ml[2 * s + 1], den);
+  }
+  out[(long)b * out_ld + (long)h * D + d] = f2bf(den > 0.f ? num / den : 0.f);
+}
+
+template <int G>
+void launch_split(dim3 grid, hipStream_t st, const bf16_t* q, long q_ld, int hq, const bf16_t* kc,
+                  const bf16_t* vc, const int* slots, const int* lengths, long slot_stride,
+                  long head_stride, int splits, float sl2, float* po, float* pml) {
+  hipLaunchKernelGGL(decode_split_kernel<G>, grid, dim3(NT), 0, st, q, q_ld, hq, kc, vc, slots, lengths,
+                     slot_stride, head_stride, splits, sl2, po, pml);
+}
+
+}  // namespace
+
+// Number of key splits for a batch: enough workgroups to cover 256 CUs ~4x, chunks of at
+// most MAXCHUNK keys (LDS score buffer) and at least 64 keys.
+extern "C" int kf_decode_splits(int B, int Hkv, int Lmax) {
+  int want = std::max(1, (1024 + B * Hkv - 1) / (B * Hkv));
+  int max_by_len = std::max(1, Lmax / 64);
+  int min_by_lds = (Lmax + MAXCHUNK - 1) / MAXCHUNK;
+  return std::max(min_by_lds, std::min(want, max_by_len));
+}
+
+// q: rows of [Hq*D] bf16 with row stride q_ld (the q columns of a fused qkv row work).
+// k/v cache: [n_slots, Hkv, Lmax, D]. workspace: part_o fp32 [B*Hq*splits*D],
+// part_ml fp32 [B*Hq*splits*2]. out: rows of [Hq*D] with stride out_ld.
+extern "C" int kf_decode_attn(const void* q, long q_ld, const void* kc, const void* vc, const int* slots,
+                              const int* lengths, void* out, long out_ld, float* part_o, float* part_ml,
+                              int B, int Hq, int Hkv, int Dh, int Lmax, int splits, float scale,
+                              hipStream_t st) {
+  if (Dh != D || Hkv <= 0 || Hq % Hkv != 0) return 1;
+  const int G = Hq / Hkv;
+  if (G > MAXG || splits <= 0) return 2;
+  if ((Lmax + splits - 1) / splits > MAXCHUNK - 16) return 3;
+  if (B == 0) return 0;
+  const long head_stride = (long)Lmax * D, slot_stride = (long)Hkv * head_stride;
+  const float sl2 = scale * LOG2E;
+  dim3 grid(splits, Hkv, B);
+  auto q16 = (const bf16_t*)q;
+  auto k16 = (const bf16_t*)kc;
+  auto v16 = (const bf16_t*)vc;
+  switch (G) {
+    case 1: launch_split<1>(grid, st, q16, q_ld, Hq, k16, v16, slots, lengths, slot_stride, head_stride, splits, sl2, part_o, part_ml); break;
+    case 2: launch_split<2>(grid, st, q16, q_ld, Hq, k16, v16, slots, lengths, slot_stride, head_stride, splits, sl2, part_o, part_ml); break;
+    case 4: launch_split<4>(grid, st, q16, q_ld, Hq, k16, v16, slots, lengths, slot_stride, head_stride, splits, sl2, part_o, part_ml); break;
+    case 8: launch_split<8>(grid, st, q16, q_ld, Hq, k16, v16, slots, lengths, slot_stride, head_stride, splits, sl2, part_o, part_ml); break;
+    default: return 4;
+  }
+  hipLaunchKernelGGL(decode_combine_kernel, dim3(B * Hq), dim3(D), 0, st, part_o, part_ml, splits,
+                     (bf16_t*)out, out_ld, Hq);
+  KF_CHECK_LAUNCH();
+  return 0;
+}
+
+// Append the current token's K/V (post-RoPE, taken from the fused qkv rows) into the cache at
+// position pos[b] of slot slots[b].  One 16-lane group per (row, kv head, k|v).
+__global__ void kv_append_kernel(const bf16_t* __restrict__ qkv, long ld, int Hq, int Hkv,
+                                 const int* __restrict__ slots, const int* __restrict__ pos,
+                                 bf16_t* __restrict__ kc, bf16_t* __restrict__ vc, int Lmax, int B) {
+  const int g = (blockIdx.x * blockDim.x + threadIdx.x) >> 4;   // (b, kv, h)
+  const int sub = threadIdx.x & 15;
+  if (g >= B * 2 * Hkv) return;
+  const int b = g / (2 * Hkv), r = g % (2 * Hkv), which = r / Hkv, h = r % Hkv;
+  const bf16_t* src = qkv + (long)b * ld + (long)(Hq + which * Hkv + h) * D + sub * 8;
+  bf16_t* dst = (which ? vc : kc) + (((long)slots[b] * Hkv + h) * Lmax + pos[b]) * D + sub * 8;
+  st16(dst, ld16(src));
+}
+
+extern "C" int kf_kv_append(const void* qkv, long ld, int B, int Hq, int Hkv, int Dh, const int* slots,
+                            const int* pos, void* kc, void* vc, int Lmax, hipStream_t st) {
+  if (Dh != D) return 1;
+  if (B == 0) return 0;
+  const int threads = B * 2 * Hkv * 16;
+  hipLaunchKernelGGL(kv_append_kernel, dim3(cdiv(threads, 256)), dim3(256), 0, st, (const bf16_t*)qkv, ld,
+                     Hq, Hkv, slots, pos, (bf16_t*)kc, (bf16_t*)vc, Lmax, B);
+  KF_CHECK_LAUNCH();
+  return 0;
+}
+
+// Prefill: copy rows [0, S) of one sequence's fused qkv into slot `slot` (positions 0..S-1).
+__global__ void kv_fill_kernel(const bf16_t* __restrict__ qkv, long ld, int S, int Hq, int Hkv, int slot,
+                               bf16_t* __restrict__ kc, bf16_t* __restrict__ vc, int Lmax) {
+  const long g = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 4;   // (t, kv, h)
+  const int sub = threadIdx.x & 15;
+  if (g >= (long)S * 2 * Hkv) return;
+  const int t = g / (2 * Hkv), r = g % (2 * Hkv), which = r / Hkv, h = r % Hkv;
+  const bf16_t* src = qkv + (long)t * ld + (long)(Hq + which * Hkv + h) * D + sub * 8;
+  bf16_t* dst = (which ? vc : kc) + (((long)slot * Hkv + h) * Lmax + t) * D + sub * 8;
+  st16(dst, ld16(src));
+}
+
+extern "C" int kf_kv_fill(const void* qkv, long ld, int S, int Hq, int Hkv, int Dh, int slot, void* kc,
+                          void* vc, int Lmax, hipStream_t st) {
+  if (Dh != D || S > Lmax) return 1;
+  if (S == 0) return 0;
+  const long threads = (long)S * 2 * Hkv * 16;
+  hipLaunchKernelGGL(kv_fill_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st,
+                     (const bf16_t*)qkv, ld, S, Hq, Hkv, slot, (bf16_t*)kc, (bf16_t*)vc, Lmax);
+  KF_CHECK_LAUNCH();
+  return 0;
+}

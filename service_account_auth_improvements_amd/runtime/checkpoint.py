@@ -83,3 +83,23 @@ def load_checkpoint(path: str, trainer) -> dict:
         sh.v.copy_(otens[k + "/v"].to(dev))
     opt.step_count = int(meta["step"])
     return meta
+
+
+def load_params(model, path: str) -> dict:
+    """Inference load: the flat bf16 parameter buffers of this (tp, pp) shard only (the
+    optimizer state in the file is never read)."""
+    from safetensors import safe_open
+    st = model.st
+    with open(os.path.join(path, "meta.json")) as f:
+        meta = json.load(f)
+    p = meta["parallel"]
+    if (p["tp"], p["pp"]) != (st.tp, st.pp):
+        raise ValueError(f"checkpoint layout tp{p['tp']}/pp{p['pp']} != current tp{st.tp}/pp{st.pp}")
+    pfile = os.path.join(path, f"tp{st.tp_rank}-pp{st.pp_rank}-dp0.safetensors")
+    with safe_open(pfile, framework="pt", device="cpu") as f:
+        for g in model.groups:
+            t = f.get_tensor(f"param/{g.name}")
+            if t.numel() != g.params.numel():
+                raise ValueError(f"param/{g.name}: {t.numel()} elements, model expects {g.params.numel()}")
+            g.params.copy_(t.to(g.params.device))
+    return meta

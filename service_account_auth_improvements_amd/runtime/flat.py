@@ -61,12 +61,13 @@ class FlatGroup:
         self.numel = _round(self.numel + n)
         return spec
 
-    def allocate(self, device, dtype=torch.bfloat16, pad_to: int = 1):
-        """Allocate storage; ``pad_to`` rounds the total so it divides evenly into DP shards."""
+    def allocate(self, device, dtype=torch.bfloat16, pad_to: int = 1, grads: bool = True):
+        """Allocate storage; ``pad_to`` rounds the total so it divides evenly into DP shards.
+        ``grads=False`` (inference) allocates no gradient buffer."""
         total = _round(self.numel, max(ALIGN, pad_to))
         self.numel = total
         self.params = torch.zeros(total, device=device, dtype=dtype)
-        self.grads = torch.zeros(total, device=device, dtype=dtype)
+        self.grads = torch.zeros(total, device=device, dtype=dtype) if grads else None
         return self
 
     def param(self, name) -> torch.Tensor:

@@ -1,0 +1,303 @@
+"""Llama-3 inference engine for the InferenceService predictor (BASELINE configs[2]).
+
+MI355X-first design:
+
+* Weights live in the same flat bf16 buffer the trainer uses (``Llama.allocate(grads=False)``)
+  so a training checkpoint loads with zero re-layout.
+* KV cache: one slot-major tensor per layer, ``[n_slots, Hkv, max_len, 128]`` bf16.  Slots
+  are preallocated at full context length -- 288 GB of HBM holds ~2M tokens of Llama-3-8B
+  KV (128 KB/token) -- so there is no paging indirection on the memory-bound decode path.
+* Prefill runs the training forward kernels (fused residual+RMSNorm, fused QKV GEMM, in-place
+  RoPE, MFMA flash attention, SwiGLU) and streams K/V into the slot with ``kv_fill_``.
+* Decode appends K/V (``kv_append_``) and runs the split-K GQA decode kernel (K8).  Every
+  decode step for a batch-size bucket is captured once in a HIP graph (static input
+  buffers, padded rows point at a scratch slot), so a token costs one graph launch instead
+  of ~350 kernel launches.
+* Continuous batching: ``Scheduler`` admits requests into free slots between decode steps
+  (prefill one sequence at a time), retires finished sequences immediately.
+* TP > 1 (one process per GPU over RCCL): Megatron split via the model's ``tp_all_reduce``;
+  vocab-parallel logits are all-gathered for sampling.
+"""
+from __future__ import annotations
+
+import math
+import queue
+import threading
+import time
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from .. import ops
+from ..models.llama import Llama, LlamaConfig
+from ..ops.attention import attention_fwd, decode_attention, kv_append_, kv_fill_
+from ..parallel.state import ParallelState, tp_all_reduce
+
+BUCKETS = (1, 2, 4, 8, 16, 32, 64, 128, 256)
+
+
+class Engine:
+    def __init__(self, model: Llama, n_slots: int = 64, max_len: int = 4096, use_graphs: Optional[bool] = None):
+        self.m = model
+        cfg = model.cfg
+        self.cfg = cfg
+        self.dev = model.device
+        self.n_slots = n_slots + 1            # last slot = scratch for padded graph rows
+        self.scratch = n_slots
+        self.max_len = max_len
+        assert max_len <= cfg.max_seq, "max_len exceeds the RoPE table"
+        L = len(model.layers)
+        shape = (L, self.n_slots, model.hkv, max_len, cfg.head_dim)
+        self.kc = torch.zeros(shape, dtype=torch.bfloat16, device=self.dev)
+        self.vc = torch.zeros(shape, dtype=torch.bfloat16, device=self.dev)
+        self.use_graphs = (self.dev.type == "cuda") if use_graphs is None else use_graphs
+        self._graphs: Dict[int, tuple] = {}
+
+    # ------------------------------------------------------------------ helpers
+    def _logits_full(self, y):
+        m = self.m
+        logits = torch.mm(y, m.P("lm_head").t())
+        if m.tp > 1:
+            parts = [torch.empty_like(logits) for _ in range(m.tp)]
+            dist.all_gather(parts, logits, group=m.st.tp_group)
+            logits = torch.cat(parts, -1)
+        return logits
+
+    def _embed(self, tokens):
+        return self.m.embed_fwd(tokens)
+
+    def _mlp(self, i, h1, da):
+        m, cfg = self.m, self.cfg
+        mm, h2, _ = ops.rmsnorm_fwd(h1, m.P(f"l{i}.norm2"), cfg.norm_eps, residual=da)
+        s = ops.swiglu_fwd(torch.mm(mm, m.P(f"l{i}.wgu").t()))
+        return h2, tp_all_reduce(torch.mm(s, m.P(f"l{i}.wd").t()), m.st)
+
+    # ------------------------------------------------------------------ prefill
+    @torch.no_grad()
+    def prefill(self, slot: int, tokens: List[int]) -> torch.Tensor:
+        """Run the prompt through the model, fill the slot's KV; returns last-position logits."""
+        m, cfg = self.m, self.cfg
+        S = len(tokens)
+        assert 0 < S <= self.max_len
+        Sp = S if self.dev.type != "cuda" else ((S + 127) // 128) * 128   # flash kernel tiles of 128
+        tok = torch.zeros(Sp, dtype=torch.long, device=self.dev)
+        tok[:S] = torch.tensor(tokens, dtype=torch.long, device=self.dev)
+        r = self._embed(tok)
+        d = None
+        for li, i in enumerate(m.layers):
+            a, h1, _ = ops.rmsnorm_fwd(r, m.P(f"l{i}.norm1"), cfg.norm_eps, residual=d)
+            qkv = torch.mm(a, m.P(f"l{i}.wqkv").t())
+            ops.rope_(qkv, m.hq + m.hkv, cfg.head_dim, m.cos, m.sin, seq_len=Sp)
+            o, _ = attention_fwd(qkv, 1, Sp, m.hq, m.hkv, cfg.head_dim)
+            kv_fill_(qkv, S, m.hq, slot, self.kc[li], self.vc[li])
+            da = tp_all_reduce(torch.mm(o, m.P(f"l{i}.wo").t()), m.st)
+            r, d = self._mlp(i, h1, da)
+        y, _, _ = ops.rmsnorm_fwd(r[S - 1:S].contiguous(), m.P("final_norm"), cfg.norm_eps,
+                                  residual=d[S - 1:S].contiguous())
+        return self._logits_full(y)[0]
+
+    # ------------------------------------------------------------------ decode
+    def _decode_body(self, tokens, slots, pos, lengths):
+        m, cfg = self.m, self.cfg
+        r = self._embed(tokens)
+        d = None
+        for li, i in enumerate(m.layers):
+            a, h1, _ = ops.rmsnorm_fwd(r, m.P(f"l{i}.norm1"), cfg.norm_eps, residual=d)
+            qkv = torch.mm(a, m.P(f"l{i}.wqkv").t())
+            ops.rope_(qkv, m.hq + m.hkv, cfg.head_dim, m.cos, m.sin, pos=pos)
+            kv_append_(qkv, m.hq, slots, pos, self.kc[li], self.vc[li])
+            o = decode_attention(qkv, self.kc[li], self.vc[li], slots, lengths, m.hq)
+            da = tp_all_reduce(torch.mm(o, m.P(f"l{i}.wo").t()), m.st)
+            r, d = self._mlp(i, h1, da)
+        y, _, _ = ops.rmsnorm_fwd(r, m.P("final_norm"), cfg.norm_eps, residual=d)
+        return self._logits_full(y)
+
+    def _graph_for(self, Bb: int):
+        g = self._graphs.get(Bb)
+        if g is not None:
+            return g
+        dev = self.dev
+        tokens = torch.zeros(Bb, dtype=torch.long, device=dev)
+        slots = torch.full((Bb,), self.scratch, dtype=torch.int32, device=dev)
+        pos = torch.zeros(Bb, dtype=torch.int32, device=dev)
+        lengths = torch.ones(Bb, dtype=torch.int32, device=dev)
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):          # warm-up (allocator, hipBLASLt heuristics)
+            for _ in range(2):
+                self._decode_body(tokens, slots, pos, lengths)
+        torch.cuda.current_stream(dev).wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            out = self._decode_body(tokens, slots, pos, lengths)
+        g = (graph, tokens, slots, pos, lengths, out)
+        self._graphs[Bb] = g
+        return g
+
+    @torch.no_grad()
+    def decode(self, tokens: List[int], slots: List[int], pos: List[int]) -> torch.Tensor:
+        """One decode step: token t_b at position pos_b of slot s_b.  Returns logits [B, V]."""
+        B = len(tokens)
+        if not self.use_graphs:
+            dev = self.dev
+            t = torch.tensor(tokens, dtype=torch.long, device=dev)
+            sl = torch.tensor(slots, dtype=torch.int32, device=dev)
+            p = torch.tensor(pos, dtype=torch.int32, device=dev)
+            return self._decode_body(t, sl, p, p + 1)
+        Bb = next((b for b in BUCKETS if b >= B), None)
+        if Bb is None:
+            raise ValueError(f"decode batch {B} exceeds the largest graph bucket {BUCKETS[-1]}")
+        graph, gt, gs, gp, gl, out = self._graph_for(Bb)
+        pad = Bb - B
+        host = torch.tensor([tokens + [0] * pad, slots + [self.scratch] * pad, pos + [0] * pad],
+                            dtype=torch.int64).pin_memory()
+        dev_rows = host.to(self.dev, non_blocking=True)
+        gt.copy_(dev_rows[0])
+        gs.copy_(dev_rows[1])
+        gp.copy_(dev_rows[2])
+        gl.copy_(dev_rows[2] + 1)
+        graph.replay()
+        return out[:B]
+
+    def release(self, slot: int):
+        pass   # slots are overwritten in place; nothing to free
+
+
+def sample(logits: torch.Tensor, temperature: float = 0.0, top_p: float = 1.0,
+           generator: Optional[torch.Generator] = None) -> torch.Tensor:
+    """Greedy (temperature 0) or nucleus sampling over fp32 logits [B, V] -> [B]."""
+    if temperature <= 0:
+        return logits.argmax(-1)
+    probs = torch.softmax(logits.float() / temperature, -1)
+    if top_p < 1.0:
+        sp, idx = probs.sort(-1, descending=True)
+        keep = sp.cumsum(-1) - sp < top_p
+        sp = sp * keep
+        choice = torch.multinomial(sp / sp.sum(-1, keepdim=True), 1, generator=generator)
+        return idx.gather(-1, choice).squeeze(-1)
+    return torch.multinomial(probs, 1, generator=generator).squeeze(-1)
+
+
+# ------------------------------------------------------------------ continuous batching
+@dataclass
+class Request:
+    prompt: List[int]
+    max_new_tokens: int = 64
+    temperature: float = 0.0
+    top_p: float = 1.0
+    stop: Optional[List[int]] = None
+    output: List[int] = field(default_factory=list)
+    done: threading.Event = field(default_factory=threading.Event)
+    t_submit: float = field(default_factory=time.time)
+    t_first: float = 0.0
+    t_done: float = 0.0
+    error: Optional[str] = None
+
+
+class Scheduler:
+    """Admit -> prefill -> joint decode steps; one engine loop thread."""
+
+    def __init__(self, engine: Engine, max_batch: int = 64):
+        self.e = engine
+        self.max_batch = min(max_batch, engine.scratch)
+        self.q: "queue.Queue[Request]" = queue.Queue()
+        self.active: Dict[int, Request] = {}           # slot -> request
+        self.free = list(range(engine.scratch))
+        self._stop = threading.Event()
+        self._thread: Optional[threading.Thread] = None
+        self.tokens_generated = 0
+        self.steps = 0
+
+    def submit(self, req: Request) -> Request:
+        if len(req.prompt) + req.max_new_tokens > self.e.max_len:
+            req.error = f"prompt + max_new_tokens exceeds max_len {self.e.max_len}"
+            req.done.set()
+            return req
+        self.q.put(req)
+        return req
+
+    def _finish(self, slot, req):
+        req.t_done = time.time()
+        req.done.set()
+        del self.active[slot]
+        self.free.append(slot)
+
+    def step(self) -> bool:
+        """One scheduling iteration; returns False when idle."""
+        admitted = False
+        while self.free and len(self.active) < self.max_batch:
+            try:
+                req = self.q.get_nowait()
+            except queue.Empty:
+                break
+            slot = self.free.pop()
+            logits = self.e.prefill(slot, req.prompt)
+            tok = int(sample(logits[None], req.temperature, req.top_p)[0])
+            req.output.append(tok)
+            req.t_first = time.time()
+            self.active[slot] = req
+            admitted = True
+            if len(req.output) >= req.max_new_tokens or (req.stop and tok in req.stop):
+                self._finish(slot, req)
+        if not self.active:
+            return admitted
+        slots = sorted(self.active)
+        reqs = [self.active[s] for s in slots]
+        toks = [r.output[-1] for r in reqs]
+        pos = [len(r.prompt) + len(r.output) - 1 for r in reqs]
+        logits = self.e.decode(toks, slots, pos)
+        temps = {r.temperature for r in reqs}
+        if temps == {0.0}:
+            nxt = logits.argmax(-1).tolist()
+        else:
+            nxt = [int(sample(logits[j:j + 1], r.temperature, r.top_p)[0]) for j, r in enumerate(reqs)]
+        self.steps += 1
+        for s, r, t in zip(slots, reqs, nxt):
+            r.output.append(t)
+            self.tokens_generated += 1
+            if len(r.output) >= r.max_new_tokens or (r.stop and t in r.stop):
+                self._finish(s, r)
+        return True
+
+    def run_until_idle(self):
+        while self.step() or not self.q.empty():
+            pass
+
+    def start(self):
+        def loop():
+            while not self._stop.is_set():
+                try:
+                    busy = self.step()
+                except Exception as ex:     # fail the in-flight requests, keep serving
+                    for s, r in list(self.active.items()):
+                        r.error = str(ex)
+                        self._finish(s, r)
+                    busy = False
+                if not busy:
+                    time.sleep(0.001)
+        self._thread = threading.Thread(target=loop, daemon=True)
+        self._thread.start()
+        return self
+
+    def stop(self):
+        self._stop.set()
+        if self._thread:
+            self._thread.join(timeout=5)
+
+
+def build_engine(model_name: str = "llama3-8b", device=None, n_slots: int = 64, max_len: int = 4096,
+                 checkpoint: Optional[str] = None, n_layers: Optional[int] = None, seed: int = 1234,
+                 st: Optional[ParallelState] = None, use_graphs: Optional[bool] = None) -> Engine:
+    cfg = LlamaConfig.preset(model_name)
+    if n_layers:
+        cfg = cfg.with_(n_layers=n_layers)
+    if device is None:
+        device = "cuda" if torch.cuda.is_available() else "cpu"
+    st = st or ParallelState(device=torch.device(device))
+    model = Llama(cfg, st=st, device=device, seed=seed).allocate(grads=False)
+    if checkpoint:
+        from ..runtime.checkpoint import load_params
+        load_params(model, checkpoint)
+    return Engine(model, n_slots=n_slots, max_len=max_len, use_graphs=use_graphs)

@@ -1,0 +1,157 @@
+"""InferenceService: engine (prefill/decode vs full forward), continuous batching,
+predictor HTTP API, and the InferenceService controller (object level + CPU end to end)."""
+import json
+import os
+import socket
+import sys
+import time
+import urllib.request
+
+import pytest
+import torch
+
+from service_account_auth_improvements_amd.controlplane import inferenceservice as isvcmod
+from service_account_auth_improvements_amd.controlplane.apiserver import APIServer
+from service_account_auth_improvements_amd.controlplane.client import InMemoryClient
+from service_account_auth_improvements_amd.controlplane.kubelet import DeploymentController, Kubelet
+from service_account_auth_improvements_amd.controlplane.runtime import Manager
+from service_account_auth_improvements_amd.serving.engine import Request, Scheduler, build_engine
+from service_account_auth_improvements_amd.serving.server import create_app
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def eng():
+    return build_engine("tiny", device="cpu", n_slots=4, max_len=64)
+
+
+def test_prefill_decode_match_full_forward(eng):
+    prompt = [5, 17, 99, 3, 42, 7]
+    cont = [11, 12, 13]
+    full = eng.m.forward_logits(torch.tensor([prompt + cont]))[0].float()
+    lg = eng.prefill(2, prompt).float()
+    assert torch.allclose(lg, full[len(prompt) - 1], atol=1e-2)
+    for j, t in enumerate(cont):
+        out = eng.decode([t], [2], [len(prompt) + j])[0].float()
+        assert torch.allclose(out, full[len(prompt) + j], atol=1e-2)
+
+
+def test_continuous_batching_is_order_independent(eng):
+    s = Scheduler(eng, max_batch=3)
+    a = s.submit(Request(prompt=[1, 2, 3, 4], max_new_tokens=6))
+    b = s.submit(Request(prompt=[9, 8], max_new_tokens=3))
+    c = s.submit(Request(prompt=[1, 2, 3, 4], max_new_tokens=6))
+    d = s.submit(Request(prompt=[7] * 10, max_new_tokens=4))    # waits for a free slot
+    s.run_until_idle()
+    assert a.output == c.output and len(a.output) == 6 and len(b.output) == 3 and len(d.output) == 4
+    solo = Scheduler(eng, max_batch=1)
+    e = solo.submit(Request(prompt=[1, 2, 3, 4], max_new_tokens=6))
+    solo.run_until_idle()
+    assert e.output == a.output
+    bad = s.submit(Request(prompt=[1] * 60, max_new_tokens=10))
+    assert bad.error and bad.done.is_set()
+
+
+def test_predictor_http_api(eng):
+    s = Scheduler(eng, max_batch=4).start()
+    try:
+        app = create_app(s, "llama").test_client()
+        assert app.get("/v1/models/llama").json == {"name": "llama", "ready": True}
+        assert app.get("/v1/models/other").status_code == 404
+        r = app.post("/v1/models/llama:predict", json={"instances": [{"token_ids": [1, 2, 3], "max_new_tokens": 4},
+                                                                     {"prompt": "hi", "max_new_tokens": 2}]})
+        preds = r.json["predictions"]
+        assert len(preds[0]["token_ids"]) == 4 and len(preds[1]["token_ids"]) == 2
+        r = app.post("/v2/models/llama/infer", json={"inputs": [{"name": "input_ids", "datatype": "INT64",
+                                                                  "shape": [3], "data": [1, 2, 3]}],
+                                                      "parameters": {"max_new_tokens": 4}})
+        assert r.json["outputs"][0]["data"] == preds[0]["token_ids"]
+        r = app.post("/v1/completions", json={"prompt": "hello", "max_tokens": 3})
+        assert r.json["usage"] == {"prompt_tokens": 5, "completion_tokens": 3}
+        assert b"predictor_generated_tokens_total" in app.get("/metrics").data
+    finally:
+        s.stop()
+
+
+def _isvc(name="llama", **model):
+    m = {"modelFormat": {"name": "kfamd-llama"}, "resources": {"limits": {"amd.com/gpu": "1"}}}
+    m.update(model)
+    return {"apiVersion": "serving.kserve.io/v1beta1", "kind": "InferenceService",
+            "metadata": {"name": name, "namespace": "team"}, "spec": {"predictor": {"model": m}}}
+
+
+def test_isvc_controller_objects_and_status():
+    srv = APIServer()
+    c = InMemoryClient(srv)
+    c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "team"}})
+    mgr = Manager(c).add(isvcmod.InferenceServiceReconciler(c))
+    c.create(_isvc(storageUri="pvc://models/llama3-8b"))
+    mgr.run_until_idle()
+    dep = c.get("apps/v1", "Deployment", "llama-predictor", "team")
+    ctr = dep["spec"]["template"]["spec"]["containers"][0]
+    assert ctr["resources"]["limits"]["amd.com/gpu"] == "1"
+    assert "--checkpoint" in ctr["args"] and "/mnt/pvc/llama3-8b" in ctr["args"]
+    assert dep["spec"]["template"]["spec"]["volumes"][0]["persistentVolumeClaim"]["claimName"] == "models"
+    assert c.get("v1", "Service", "llama-predictor", "team")["spec"]["ports"][0]["targetPort"] == 8080
+    st = c.get("serving.kserve.io/v1beta1", "InferenceService", "llama", "team")["status"]
+    assert {x["type"]: x["status"] for x in st["conditions"]}["Ready"] == "False"
+    assert st["url"] == "http://llama-predictor.team.svc.cluster.local"
+    dep["status"] = {"readyReplicas": 1}
+    c.update_status(dep)
+    mgr.run_until_idle()
+    st = c.get("serving.kserve.io/v1beta1", "InferenceService", "llama", "team")["status"]
+    assert {x["type"]: x["status"] for x in st["conditions"]}["Ready"] == "True"
+    assert st["modelStatus"]["states"]["activeModelState"] == "Loaded"
+    c.create(_isvc("bad", modelFormat={"name": "tensorflow"}))
+    mgr.run_until_idle()
+    st = c.get("serving.kserve.io/v1beta1", "InferenceService", "bad", "team")["status"]
+    assert st["conditions"][1]["reason"] == "InvalidPredictorSpec"
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_isvc_end_to_end_cpu(tmp_path):
+    """InferenceService CR -> Deployment -> Pod -> predictor process -> HTTP predict."""
+    srv = APIServer()
+    c = InMemoryClient(srv)
+    c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "team"}})
+    kub = Kubelet(c, n_gpus=0, exec_pods=True, workdir=ROOT, log_dir=str(tmp_path),
+                  extra_env={"PYTHONPATH": ROOT, "OMP_NUM_THREADS": "1"})
+    mgr = Manager(c).add(isvcmod.InferenceServiceReconciler(c)).add(DeploymentController(c)).add(kub)
+    port = _free_port()
+    isvc = _isvc(args=["--model", "tiny", "--slots", "2", "--max-len", "64", "--port", str(port),
+                       "--host", "127.0.0.1"], resources={})
+    c.create(isvc)
+    mgr.start(workers=2)
+    try:
+        deadline = time.time() + 120
+        out = None
+        while time.time() < deadline:
+            try:
+                req = urllib.request.Request(f"http://127.0.0.1:{port}/v1/models/llama:predict",
+                                             data=json.dumps({"instances": [{"token_ids": [1, 2, 3],
+                                                                             "max_new_tokens": 3}]}).encode(),
+                                             headers={"Content-Type": "application/json"})
+                out = json.loads(urllib.request.urlopen(req, timeout=10).read())
+                break
+            except OSError:
+                time.sleep(0.5)
+        assert out is not None, kub.pod_log("team", c.list("v1", "Pod", "team")[0]["metadata"]["name"])
+        assert len(out["predictions"][0]["token_ids"]) == 3
+        deadline = time.time() + 20
+        while time.time() < deadline:
+            st = c.get("serving.kserve.io/v1beta1", "InferenceService", "llama", "team").get("status") or {}
+            if {x["type"]: x["status"] for x in st.get("conditions", [])}.get("Ready") == "True":
+                break
+            time.sleep(0.2)
+        assert {x["type"]: x["status"] for x in st["conditions"]}["Ready"] == "True"
+    finally:
+        mgr.stop()
+        kub.shutdown()
