@@ -192,7 +192,7 @@ void launch_split(dim3 grid, hipStream_t st, const bf16_t* q, long q_ld, int hq,
 extern "C" int kf_decode_splits(int B, int Hkv, int Lmax) {
   int want = std::max(1, (1024 + B * Hkv - 1) / (B * Hkv));
   int max_by_len = std::max(1, Lmax / 64);
-  int min_by_lds = (Lmax + MAXCHUNK - 1) / MAXCHUNK;
+  int min_by_lds = (Lmax + MAXCHUNK - 17) / (MAXCHUNK - 16);
   return std::max(min_by_lds, std::min(want, max_by_len));
 }
 
