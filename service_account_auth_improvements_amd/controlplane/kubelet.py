@@ -286,6 +286,11 @@ class Kubelet(Controller):
         with self._lock:
             self.procs[key] = p
 
+    def pod_pids(self) -> Dict[str, int]:
+        """Running pod processes (``ns/name`` -> pid), for the dashboard's metrics sampler."""
+        with self._lock:
+            return {k: p.pid for k, p in self.procs.items() if p.poll() is None}
+
     def pod_log(self, namespace: str, name: str) -> str:
         path = self.logs.get(f"{namespace}/{name}")
         if path and os.path.exists(path):
