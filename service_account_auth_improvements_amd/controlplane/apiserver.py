@@ -114,6 +114,11 @@ BUILTIN_TYPES = [
     ResourceType("networking.istio.io", "VirtualService", "virtualservices", True, ("v1alpha3", "v1beta1")),
     ResourceType("security.istio.io", "AuthorizationPolicy", "authorizationpolicies", True, ("v1beta1",)),
     ResourceType("app.k8s.io", "Application", "applications", True, ("v1beta1",)),
+    ResourceType("apiextensions.k8s.io", "CustomResourceDefinition", "customresourcedefinitions", False, ("v1",)),
+    ResourceType("admissionregistration.k8s.io", "MutatingWebhookConfiguration",
+                 "mutatingwebhookconfigurations", False, ("v1",), False),
+    ResourceType("admissionregistration.k8s.io", "ValidatingWebhookConfiguration",
+                 "validatingwebhookconfigurations", False, ("v1",), False),
     # kubeflow CRDs (reference)
     ResourceType("kubeflow.org", "Notebook", "notebooks", True, ("v1alpha1", "v1beta1", "v1")),
     ResourceType("kubeflow.org", "Profile", "profiles", False, ("v1beta1", "v1")),
@@ -125,6 +130,41 @@ BUILTIN_TYPES = [
     ResourceType("kubeflow.org", "MPIJob", "mpijobs", True, ("v2beta1",)),
     ResourceType("serving.kserve.io", "InferenceService", "inferenceservices", True, ("v1beta1",)),
 ]
+
+
+def _check_schema(v, sch: dict, path: str, errs: List[str]):
+    """Structural openAPI subset used by CRD validation."""
+    if not sch or sch.get("x-kubernetes-preserve-unknown-fields") and "properties" not in sch:
+        return
+    if sch.get("x-kubernetes-int-or-string"):
+        if not isinstance(v, (int, str)) or isinstance(v, bool):
+            errs.append(f"{path or '.'}: must be an integer or a string")
+        return
+    typ = sch.get("type")
+    ok = {"object": lambda x: isinstance(x, dict), "array": lambda x: isinstance(x, list),
+          "string": lambda x: isinstance(x, str), "boolean": lambda x: isinstance(x, bool),
+          "integer": lambda x: isinstance(x, int) and not isinstance(x, bool),
+          "number": lambda x: isinstance(x, (int, float)) and not isinstance(x, bool)}.get(typ)
+    if ok is not None and not ok(v):
+        errs.append(f"{path or '.'}: must be of type {typ}")
+        return
+    if "enum" in sch and v not in sch["enum"]:
+        errs.append(f"{path}: unsupported value {v!r}, supported: {sch['enum']}")
+    if "minimum" in sch and isinstance(v, (int, float)) and v < sch["minimum"]:
+        errs.append(f"{path}: must be >= {sch['minimum']}")
+    if "minLength" in sch and isinstance(v, str) and len(v) < sch["minLength"]:
+        errs.append(f"{path}: must be at least {sch['minLength']} characters")
+    if typ == "object" and isinstance(v, dict):
+        for r in sch.get("required") or []:
+            if r not in v:
+                errs.append(f"{path}.{r}: Required value")
+        props = sch.get("properties") or {}
+        for k, sub in props.items():
+            if k in v and v[k] is not None:
+                _check_schema(v[k], sub, f"{path}.{k}", errs)
+    if typ == "array" and isinstance(v, list) and sch.get("items"):
+        for i, x in enumerate(v):
+            _check_schema(x, sch["items"], f"{path}[{i}]", errs)
 
 
 def split_api_version(api_version: str) -> Tuple[str, str]:
@@ -357,6 +397,7 @@ class APIServer:
         self._store: Dict[Tuple[str, str], Dict[Tuple[str, str], dict]] = {}
         self._rv = itertools.count(1)
         self._watchers: List[Tuple[Optional[str], Optional[str], WatchFn]] = []
+        self._schemas: Dict[Tuple[str, str], Dict[str, Optional[dict]]] = {}
         self.mutating: List[Webhook] = []
         self.validating: List[Webhook] = []
         self.clock = lambda: now_rfc3339()
@@ -365,6 +406,39 @@ class APIServer:
     def register_type(self, t: ResourceType):
         self._types[(t.group, t.kind)] = t
         self._by_plural[(t.group, t.plural)] = t
+
+    def _register_crd(self, crd: dict):
+        """A CustomResourceDefinition makes its kind servable and its per-version
+        openAPIV3Schema enforced on create/update (structural subset: type, required,
+        properties, items, enum, minimum, minLength, preserve-unknown-fields)."""
+        sp = crd.get("spec") or {}
+        names = sp.get("names") or {}
+        vers = [v for v in sp.get("versions") or [] if v.get("served", True)]
+        if not (sp.get("group") and names.get("kind") and names.get("plural") and vers):
+            raise Invalid("CustomResourceDefinition needs spec.group, spec.names.{kind,plural}, spec.versions")
+        storage = [v["name"] for v in vers if v.get("storage")]
+        order = [v["name"] for v in vers if v["name"] not in storage] + storage   # storage version last
+        self.register_type(ResourceType(sp["group"], names["kind"], names["plural"],
+                                        sp.get("scope", "Namespaced") == "Namespaced", tuple(order),
+                                        "status" in ((vers[0].get("subresources") or {}))))
+        self._schemas[(sp["group"], names["kind"])] = {
+            v["name"]: (v.get("schema") or {}).get("openAPIV3Schema") for v in vers}
+
+    def _validate_schema(self, t: ResourceType, obj: dict):
+        schemas = self._schemas.get((t.group, t.kind))
+        if not schemas:
+            return
+        _, ver = split_api_version(obj.get("apiVersion", ""))
+        sch = schemas.get(ver) or schemas.get(t.storage_version)
+        if not sch:
+            return
+        errs: List[str] = []
+        body = {k: v for k, v in obj.items() if k not in ("metadata", "apiVersion", "kind")}
+        _check_schema(body, {k: v for k, v in sch.items() if k != "properties"} | {
+            "type": "object", "properties": {k: v for k, v in (sch.get("properties") or {}).items()
+                                             if k not in ("metadata", "apiVersion", "kind")}}, "", errs)
+        if errs:
+            raise Invalid(f'{t.kind}.{t.group} "{obj.get("metadata", {}).get("name")}" is invalid: ' + "; ".join(errs))
 
     def type_for(self, api_version: str, kind: str) -> ResourceType:
         g, _ = split_api_version(api_version)
@@ -493,6 +567,9 @@ class APIServer:
             if key in bucket:
                 raise AlreadyExists(f'{t.plural} "{meta["name"]}" already exists')
             obj = self._admit("CREATE", t, obj, None, dry_run, user)
+            self._validate_schema(t, obj)
+            if t.kind == "CustomResourceDefinition" and not dry_run:
+                self._register_crd(obj)
             meta = obj["metadata"]
             meta["uid"] = str(uuid.uuid4())
             meta["creationTimestamp"] = self.clock()
@@ -551,6 +628,9 @@ class APIServer:
                 else:
                     out.pop("status", None)
             out = self._admit("UPDATE", t, out, cur, dry_run, user)
+            self._validate_schema(t, out)
+            if t.kind == "CustomResourceDefinition" and not dry_run:
+                self._register_crd(out)
             strip = lambda o: {k: v for k, v in o.items() if k not in ("metadata", "status", "apiVersion")}  # noqa
             if strip(out) != strip(cur):
                 out["metadata"]["generation"] = cmeta.get("generation", 1) + 1

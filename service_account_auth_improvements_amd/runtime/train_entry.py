@@ -60,6 +60,11 @@ def main(argv=None):
     else:
         dev = "cpu"
     st = init_distributed(tp=a.tp, pp=a.pp, device=dev)
+    if a.model == "mnist":     # BASELINE configs[0]: operator/launcher plumbing job
+        from ..models.mnist import MnistTrainer, SyntheticMnist
+        tr = MnistTrainer(st.device)
+        data = SyntheticMnist(a.micro_batch, st.device, seed=17, rank=st.dp_rank)
+        return _loop(a, tr, data, st, t_start)
     tcfg = TrainConfig(model=a.model, seq_len=a.seq_len, micro_batch=a.micro_batch, grad_accum=a.grad_accum,
                        zero1=a.zero1, n_layers=a.layers)
     if a.pp > 1:
@@ -71,6 +76,11 @@ def main(argv=None):
         from .checkpoint import load_checkpoint
         load_checkpoint(a.resume, tr)
     data = SyntheticData(tr.mcfg.vocab_size, a.micro_batch, a.seq_len, st.device, seed=17, rank=st.dp_rank)
+    return _loop(a, tr, data, st, t_start)
+
+
+def _loop(a, tr, data, st, t_start):
+    import torch
     _event("init_done", seconds=time.time() - t_start)
     for step in range(a.steps):
         batch = [data.next() for _ in range(a.grad_accum)]
