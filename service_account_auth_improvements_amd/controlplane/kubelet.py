@@ -274,6 +274,9 @@ class Kubelet(Controller):
         env["POD_NAME"] = pod["metadata"]["name"]
         env["POD_NAMESPACE"] = pod["metadata"]["namespace"]
         cmd = list(ctr.get("command") or []) + list(ctr.get("args") or [])
+        if cmd and cmd[0] == "kfamd-launch":      # the image's /usr/local/bin launcher == our build
+            from ..native import binary
+            cmd[0] = binary("kfamd_launch")
         key = f'{pod["metadata"]["namespace"]}/{pod["metadata"]["name"]}'
         out = subprocess.DEVNULL
         if self.log_dir:

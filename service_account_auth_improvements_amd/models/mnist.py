@@ -48,10 +48,13 @@ class MnistTrainer:
             self.model = nn.parallel.DistributedDataParallel(self.model)
         self.opt = torch.optim.SGD(self.model.parameters(), lr=lr, momentum=0.9)
 
-    def train_step(self, batch):
-        x, y = batch
+    def train_step(self, batches):
+        """One optimizer step over a list of micro-batches (gradient accumulation)."""
         self.opt.zero_grad(set_to_none=True)
-        loss = F.cross_entropy(self.model(x), y)
-        loss.backward()
+        tot = 0.0
+        for x, y in batches:
+            loss = F.cross_entropy(self.model(x), y) / len(batches)
+            loss.backward()
+            tot += float(loss)
         self.opt.step()
-        return loss.detach()
+        return torch.tensor(tot)

@@ -53,6 +53,7 @@ def main(argv=None):
     import torch
     from ..parallel.state import init_distributed
     from .trainer import SyntheticData, TrainConfig, Trainer
+    _event("imported", seconds=time.time() - t_start)
 
     dev = None if a.device == "auto" else a.device
     if dev == "cuda" or (dev is None and torch.cuda.is_available()):
@@ -60,6 +61,7 @@ def main(argv=None):
     else:
         dev = "cpu"
     st = init_distributed(tp=a.tp, pp=a.pp, device=dev)
+    _event("dist_ready", seconds=time.time() - t_start)
     if a.model == "mnist":     # BASELINE configs[0]: operator/launcher plumbing job
         from ..models.mnist import MnistTrainer, SyntheticMnist
         tr = MnistTrainer(st.device)

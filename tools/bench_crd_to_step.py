@@ -1,0 +1,116 @@
+"""CRD-to-first-step latency (the second half of BASELINE.json's metric).
+
+Brings up the LocalCluster with an exec kubelet (pods are processes on this node, GPUs
+handed out by the amd.com/gpu device plugin as HIP_VISIBLE_DEVICES), then submits N
+PyTorchJobs one after another and measures, per job, the wall-clock time from the CR
+``create`` call to the first completed optimizer step reported by rank 0 of the job
+(the worker's ``first_step`` event).  Breakdown: CR -> pod Running (control plane),
+pod -> worker process start (kfamd-launch + Python), process -> init done (torch import,
+RCCL init, model allocation + init), init -> first step (first train step incl. kernel
+loads / hipBLASLt heuristics).  Prints one JSON line with p50/p90 and the breakdown.
+
+  python tools/bench_crd_to_step.py --jobs 5 --model llama3-8b --gpus 1
+  python tools/bench_crd_to_step.py --jobs 3 --model mnist --gpus 0 --nodes 2   # configs[0]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--jobs", type=int, default=5)
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--gpus", type=int, default=1, help="GPUs per node (nprocPerNode)")
+    ap.add_argument("--nodes", type=int, default=1, help="replicas (Master + Workers)")
+    ap.add_argument("--seq-len", type=int, default=8192)
+    ap.add_argument("--micro-batch", type=int, default=1)
+    ap.add_argument("--layers", type=int, default=None)
+    ap.add_argument("--timeout", type=float, default=300)
+    a = ap.parse_args()
+
+    from service_account_auth_improvements_amd.cluster import LocalCluster
+    from service_account_auth_improvements_amd.controlplane import training
+    from service_account_auth_improvements_amd.native import build_native
+    build_native()
+    tmp = tempfile.mkdtemp(prefix="crd2step-")
+    events = os.path.join(tmp, "events.jsonl")
+    n_gpus = a.gpus * a.nodes
+    cl = LocalCluster(n_gpus=n_gpus, exec_pods=True, api_port=None, log_dir=tmp,
+                      extra_env={"KFAMD_EVENTS_FILE": events, "OMP_NUM_THREADS": "4"}).start()
+    cl.server.ensure_namespace("bench")
+    dev = "cuda" if a.gpus else "cpu"
+    cmd = [sys.executable, "-m", "service_account_auth_improvements_amd", "train", "--model", a.model,
+           "--steps", "1", "--device", dev]
+    if a.model != "mnist":
+        cmd += ["--seq-len", str(a.seq_len), "--micro-batch", str(a.micro_batch)]
+    else:
+        cmd += ["--micro-batch", "64"]
+    if a.layers:
+        cmd += ["--layers", str(a.layers)]
+    rows = []
+    try:
+        for j in range(a.jobs):
+            name = f"job{j}"
+            open(events, "w").close()
+            job = training.pytorchjob_manifest(name, "bench", "local", cmd, n_nodes=a.nodes, gpus_per_node=a.gpus,
+                                               master_port=29700 + 7 * j)
+            if not a.gpus:
+                job["spec"]["nprocPerNode"] = "1"
+            t0 = time.time()
+            cl.client.create(job)
+            t_running = None
+            first = None
+            deadline = t0 + a.timeout
+            while time.time() < deadline:
+                if t_running is None:
+                    p = cl.client.get_or_none("v1", "Pod", f"{name}-master-0", "bench")
+                    if p and (p.get("status") or {}).get("phase") == "Running":
+                        t_running = time.time()
+                evs = [json.loads(x) for x in open(events).read().splitlines() if x.strip()]
+                fs = [e for e in evs if e["event"] == "first_step" and e.get("rank") == 0]
+                if fs:
+                    first = fs[0]
+                    break
+                time.sleep(0.01)
+            if first is None:
+                log = cl.kubelet.pod_log("bench", f"{name}-master-0")
+                raise SystemExit(f"{name}: no first_step within {a.timeout}s\n{log[-3000:]}")
+            r0 = [e for e in evs if e.get("rank") == 0]
+            ps = next(e["ts"] for e in r0 if e["event"] == "process_start")
+            ini = next(e["ts"] for e in r0 if e["event"] == "init_done")
+            imp = next((e["ts"] for e in r0 if e["event"] == "imported"), ps)
+            dr = next((e["ts"] for e in r0 if e["event"] == "dist_ready"), imp)
+            rows.append({"total": first["ts"] - t0, "cr_to_running": (t_running or ps) - t0,
+                         "running_to_process": ps - (t_running or ps), "process_to_init": ini - ps,
+                         "import": imp - ps, "dist_init": dr - imp, "model_init": ini - dr,
+                         "init_to_first_step": first["ts"] - ini})
+            print(json.dumps({"job": name, **{k: round(v, 3) for k, v in rows[-1].items()}}), flush=True)
+            # wait for the job to finish so the GPUs are free for the next one
+            while time.time() < deadline:
+                jb = cl.client.get(training.PT_API, "PyTorchJob", name, "bench")
+                if any(c["type"] in ("Succeeded", "Failed") and c["status"] == "True"
+                       for c in (jb.get("status") or {}).get("conditions", [])):
+                    break
+                time.sleep(0.05)
+    finally:
+        cl.stop()
+    tot = sorted(r["total"] for r in rows)
+    out = {"metric": "CRD-to-first-step", "model": a.model, "gpus_per_node": a.gpus, "nodes": a.nodes,
+           "jobs": len(rows), "p50_s": round(statistics.median(tot), 3),
+           "p90_s": round(tot[min(len(tot) - 1, int(0.9 * len(tot)))], 3), "min_s": round(tot[0], 3),
+           "breakdown_p50_s": {k: round(statistics.median(r[k] for r in rows), 3)
+                               for k in ("cr_to_running", "running_to_process", "process_to_init", "import",
+                                         "dist_init", "model_init", "init_to_first_step")}}
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
