@@ -1,0 +1,44 @@
+"""P6/P7/P9/P10 tooling: image build plan order, manifest tag rewrite, notebook load test."""
+import os
+import shutil
+import subprocess
+import sys
+
+import yaml
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+
+def test_build_plan_dependency_order():
+    import build_images
+    cmds = build_images.commands(["predictor-rocm", "jupyter", "platform"], "reg", "v1", "docker", push=False)
+    refs = [c[c.index("-t") + 1] for c in cmds if c[:2] == ["docker", "build"]]
+    assert refs.index("reg/trainer-rocm:v1") < refs.index("reg/predictor-rocm:v1")
+    assert refs.index("reg/base:v1") < refs.index("reg/jupyter:v1")
+    tags = [c[3] for c in cmds if c[:2] == ["docker", "tag"]]
+    assert "reg/notebook-controller:v1" in tags and "reg/kfam:v1" in tags
+    for n, (ctx, df, _, _) in build_images.IMAGES.items():
+        assert os.path.exists(os.path.join(ROOT, df)), df
+
+
+def test_update_manifest_images(tmp_path):
+    import update_manifest_images as u
+    shutil.copytree(os.path.join(ROOT, "manifests"), tmp_path / "m")
+    changed = u.update(str(tmp_path / "m"), "v9.9", registry="ghcr.io/acme")
+    assert changed
+    k = yaml.safe_load(open(tmp_path / "m" / "notebook-controller" / "kustomization.yaml"))
+    assert k["images"][0] == {"name": "kfamd/notebook-controller", "newName": "ghcr.io/acme/notebook-controller",
+                              "newTag": "v9.9"}
+    assert u.update(str(tmp_path / "m"), "v9.9", registry="ghcr.io/acme", check=True) == []
+    from service_account_auth_improvements_amd import manifests
+    docs = manifests.build(str(tmp_path / "m" / "notebook-controller"))
+    dep = next(d for d in docs if d["kind"] == "Deployment")
+    assert dep["spec"]["template"]["spec"]["containers"][0]["image"] == "ghcr.io/acme/notebook-controller:v9.9"
+
+
+def test_notebook_loadtest():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "loadtest_notebooks.py"), "-n", "20"],
+                       capture_output=True, text=True, timeout=120, cwd=ROOT)
+    assert r.returncode == 0, r.stderr
+    assert '"ready": 20' in r.stdout
