@@ -10,6 +10,11 @@ Workload: full Llama-3-8B architecture (32 layers, hidden 4096, GQA 32/8, FFN 14
 vocab 128256), random init, synthetic tokens, bf16 compute with fp32 master weights and
 AdamW (grad clipping on), seq_len 8192, per-GPU micro-batch ``--micro-batch`` sequences
 x ``--grad-accum`` accumulation steps.  Weak scaling: per-GPU work is fixed as N grows.
+
+Multi-GPU (N > 1): data parallel over RCCL.  Default is ZeRO-1 -- gradient buckets are
+reduce-scattered while backward runs, AdamW updates 1/N of the fp32 state per GPU, and the
+bf16 parameter all-gather is launched right after the update and waited on per bucket by
+the next forward (runtime/trainer.py, parallel/ddp.py).  ``--no-zero1`` = all-reduce DDP.
 """
 from __future__ import annotations
 
@@ -41,7 +46,10 @@ def main():
     ap.add_argument("--seq-len", type=int, default=8192)
     ap.add_argument("--micro-batch", type=int, default=2)
     ap.add_argument("--grad-accum", type=int, default=1)
-    ap.add_argument("--zero1", action="store_true", help="ZeRO-1 (reduce-scatter + sharded AdamW)")
+    ap.add_argument("--zero1", dest="zero1", action="store_true", default=None,
+                    help="ZeRO-1: reduce-scatter grads, 1/N-sharded AdamW, parameter all-gather hidden "
+                         "behind the next forward (default when N > 1)")
+    ap.add_argument("--no-zero1", dest="zero1", action="store_false", help="classic all-reduce DDP")
     ap.add_argument("--bucket-mb", type=int, default=256)
     ap.add_argument("--attn", default="hip", choices=["hip", "sdpa"])
     ap.add_argument("--layers", type=int, default=None, help="DEBUG ONLY: invalid for reporting")
@@ -51,6 +59,8 @@ def main():
     set_attention_backend(a.attn)
     st = init_distributed(tp=1, pp=1)
     world = st.world_size
+    if a.zero1 is None:
+        a.zero1 = world > 1
     if world != a.gpus and st.rank == 0:
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     tcfg = TrainConfig(model=a.model, seq_len=a.seq_len, micro_batch=a.micro_batch,
@@ -106,7 +116,8 @@ def main():
                 "model": "Llama-3-8B" if a.model == "llama3-8b" else a.model,
                 "global_batch": world * a.micro_batch * a.grad_accum,
                 "seq_len": a.seq_len,
-                "parallelism": f"dp{world}" + ("-zero1" if a.zero1 else ""),
+                "parallelism": f"dp{world}",
+                "optimizer_sharding": "zero1" if a.zero1 else "none",
                 "micro_batch": a.micro_batch,
                 "grad_accum": a.grad_accum,
                 "n_layers": tr.mcfg.n_layers,

@@ -132,6 +132,9 @@ class Llama:
         self._full_init = full_init
         self._seed = seed
         self.on_grad_ready: Optional[Callable[[FlatGroup, int], None]] = None
+        # ZeRO-1 overlap: called with (group, lo, hi) before a parameter range is first
+        # read in forward, so the async all-gather of that range can be waited on lazily
+        self.param_wait: Optional[Callable[[FlatGroup, int, int], None]] = None
         cos, sin = ops.rope_tables(cfg.max_seq, D, cfg.rope_theta)
         self.cos = cos.to(self.device)
         self.sin = sin.to(self.device)
@@ -301,19 +304,37 @@ class Llama:
         return dh
 
     # ------------------------------------------------------------------ stage-level API
+    def _wait(self, first: str, last: str, group: Optional[FlatGroup] = None):
+        """Tell the ZeRO-1 engine that params ``first``..``last`` (one contiguous range of
+        one flat group, reverse-registration order) are about to be read."""
+        if self.param_wait is None:
+            return
+        g = group or self.mats
+        lo = g.spec(first).offset
+        self.param_wait(g, lo, g.end_offset(last))
+
+    def _wait_layer(self, i: int):
+        if self.param_wait is not None:
+            self._wait(f"l{i}.wd", f"l{i}.wqkv")
+            self._wait(f"l{i}.norm2", f"l{i}.norm1", self.norms)
+
     def stage_forward(self, inp, B: int, S: int, labels=None, scale: float = 1.0):
         """inp: tokens [B*S] (first stage) or activation [B*S, H].  Returns (out, ctx) where
         out is the loss (last stage) or the activation handed to the next stage."""
         ctx = {"layers": []}
         if self.first:
             ctx["tokens"] = inp
+            self._wait("embed", "embed")
             r, d = self.embed_fwd(inp), None
         else:
             r, d = inp, None
         for i in self.layers:
+            self._wait_layer(i)
             r, d, c = self.layer_fwd(i, r, d, B, S)
             ctx["layers"].append(c)
         if self.last:
+            self._wait("lm_head", "lm_head")
+            self._wait("final_norm", "final_norm", self.norms)
             loss, hctx = self.head_fwd(r, d, labels, scale)
             ctx["head"] = hctx
             return loss, ctx

@@ -60,6 +60,7 @@ class GradReducer:
             self.buckets[g.name] = bl
         self.enabled = dp_size > 1
         self._pending: List[Bucket] = []
+        self._gathers: dict = {}          # (group name, bucket index) -> async all-gather work
 
     # -- shard geometry (reduce_scatter mode): rank r owns [lo + r*n/dp, lo + (r+1)*n/dp) of each bucket
     def shard_ranges(self, group: FlatGroup, rank: int) -> List[Tuple[int, int]]:
@@ -111,20 +112,43 @@ class GradReducer:
                 b.work.wait()
         self._pending = []
 
-    def all_gather_params(self):
-        """ZeRO-1: after the sharded update, gather every bucket's bf16 params."""
+    def all_gather_params(self, overlap: bool = False):
+        """ZeRO-1: after the sharded update, gather every bucket's bf16 params.
+
+        ``overlap=True`` only LAUNCHES the gathers -- in forward order (the end of each flat
+        buffer holds the first layers, see runtime/flat.py) -- and returns; the model's
+        ``param_wait`` hook makes the compute stream wait on a bucket just before the next
+        forward first reads it (:meth:`wait_params`), so the gather hides behind the
+        previous layers' compute instead of sitting between optimizer and forward."""
         if not self.enabled or self.mode != "reduce_scatter":
             return
-        works = []
         r = dist.get_rank(self.dp_group) if self.dp_group is not None else dist.get_rank()
-        for bl in self.buckets.values():
-            for b in bl:
+        # small groups (norm weights) first: every layer reads one of them, and the gathers
+        # complete in launch order on the communicator's stream
+        for name, bl in sorted(self.buckets.items(), key=lambda kv: kv[1][-1].hi if kv[1] else 0):
+            for idx in reversed(range(len(bl))):
+                b = bl[idx]
                 x = b.group.params[b.lo:b.hi]
                 n = (b.hi - b.lo) // self.dp
-                works.append(dist.all_gather_into_tensor(x, x[r * n:(r + 1) * n].clone(),
-                                                         group=self.dp_group, async_op=True))
-        for w in works:
+                self._gathers[(name, idx)] = dist.all_gather_into_tensor(
+                    x, x[r * n:(r + 1) * n].clone(), group=self.dp_group, async_op=True)
+        if not overlap:
+            self.wait_all_params()
+
+    def wait_params(self, group: FlatGroup, lo: int, hi: int):
+        """Stream-wait for the pending gathers of every bucket overlapping [lo, hi)."""
+        if not self._gathers:
+            return
+        for idx, b in enumerate(self.buckets[group.name]):
+            if b.hi > lo and b.lo < hi:
+                w = self._gathers.pop((group.name, idx), None)
+                if w is not None:
+                    w.wait()
+
+    def wait_all_params(self):
+        for w in self._gathers.values():
             w.wait()
+        self._gathers = {}
 
     def broadcast_params(self, src_global_rank: int = 0):
         """C2: make every DP replica start from identical weights."""

@@ -29,6 +29,8 @@ def save_checkpoint(path: str, trainer, extra: Optional[dict] = None):
     from safetensors.torch import save_file
     import torch.distributed as dist
     st = trainer.st
+    if hasattr(trainer, "sync_params"):
+        trainer.sync_params()        # land in-flight ZeRO-1 parameter gathers first
     os.makedirs(path, exist_ok=True)
     opt = trainer.opt
     writes_params = st.dp_rank == 0

@@ -27,6 +27,7 @@ class TrainConfig:
     micro_batch: int = 1
     grad_accum: int = 1
     zero1: bool = False
+    overlap_allgather: bool = True   # ZeRO-1: hide the param all-gather behind the next forward
     bucket_mb: int = 256
     lr: float = 3e-4
     weight_decay: float = 0.1
@@ -64,6 +65,12 @@ class Trainer:
                                          max_grad_norm=tcfg.max_grad_norm),
                              shard_ranges=shard, dp_group=self.st.dp_group)
         self.step_idx = 0
+        if mode == "reduce_scatter" and tcfg.overlap_allgather:
+            self.model.param_wait = self.reducer.wait_params
+
+    def sync_params(self):
+        """Complete any in-flight ZeRO-1 parameter gathers (before checkpoint / eval)."""
+        self.reducer.wait_all_params()
 
     @property
     def tokens_per_step(self) -> int:
@@ -81,9 +88,10 @@ class Trainer:
             loss = self.model.forward_backward(tok, lab, accumulate=j > 0, scale=scale)
             total = loss if total is None else total + loss
         self.model.on_grad_ready = None
+        self.reducer.wait_all_params()     # a bucket the forward never read (padding) must land too
         self.reducer.finish()
         self.opt.step(grad_scale=1.0 / self.st.dp)
-        self.reducer.all_gather_params()
+        self.reducer.all_gather_params(overlap=self.tcfg.overlap_allgather)
         self.step_idx += 1
         return total
 

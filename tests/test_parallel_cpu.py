@@ -10,11 +10,12 @@ def _tiny_batches(vocab, n, B=2, S=32, seed=0):
             for _ in range(n)]
 
 
-def _dp_body(rank, world, zero1):
+def _dp_body(rank, world, zero1, overlap=True):
     from service_account_auth_improvements_amd.parallel.state import init_distributed
     from service_account_auth_improvements_amd.runtime.trainer import TrainConfig, Trainer
     st = init_distributed(tp=1, pp=1, device="cpu")
-    tr = Trainer(TrainConfig(model="tiny", seq_len=32, zero1=zero1, bucket_mb=1, lr=1e-3), st)
+    tr = Trainer(TrainConfig(model="tiny", seq_len=32, zero1=zero1, bucket_mb=1, lr=1e-3,
+                             overlap_allgather=overlap), st)
     batches = _tiny_batches(tr.mcfg.vocab_size, world)
     mine = [batches[rank]]
     # one step with the optimizer disabled (lr 0) exposes the reduced gradients
@@ -24,6 +25,7 @@ def _dp_body(rank, world, zero1):
     grads = tr.model.mats.grads.float().clone() / world
     tr.opt.cfg.lr = lr
     losses = [float(tr.train_step(mine)) for _ in range(3)]
+    tr.sync_params()
     return losses, tr.model.mats.params.float().clone(), tr.model.norms.params.float().clone(), grads
 
 
@@ -60,6 +62,9 @@ def test_zero1_matches_allreduce():
     assert diff.max().item() <= 2 * 1e-3 * 3 + 1e-2
     assert (diff < 1e-3).float().mean().item() > 0.99
     assert _close(z[0][2], a[0][2], 2e-2)
+    # the forward-overlapped parameter all-gather is bit-identical to the blocking one
+    zb = run_ranks(_dp_body, world=2, args=(True, False))
+    assert torch.equal(zb[0][1], z[0][1]) and zb[0][0] == z[0][0]
 
 
 def _tp_body(rank, world):
