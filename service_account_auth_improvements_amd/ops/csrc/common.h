@@ -31,8 +31,12 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   __bf16 b = (__bf16)f;
   return __builtin_bit_cast(bf16_t, b);
 }
+typedef __attribute__((ext_vector_type(2))) float f32x2_t;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+// two floats -> packed bf16 pair in ONE v_cvt_pk_bf16_f32 (RNE); the scalar-cast form
+// costs a convert per half plus a shift and an or
 __device__ __forceinline__ u32 pack2(float lo, float hi) {
-  return (u32)f2bf(lo) | ((u32)f2bf(hi) << 16);
+  return __builtin_bit_cast(u32, __builtin_convertvector(f32x2_t{lo, hi}, bf16x2_t));
 }
 
 // unpack 8 bf16 held in a u32x4 into 8 floats

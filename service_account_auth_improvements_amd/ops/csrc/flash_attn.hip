@@ -178,40 +178,45 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(
 #pragma unroll
         for (int ks = 0; ks < 8; ++ks) s[kt] = mfma32(row_read(Ks, swz(32 * kt + lr, 2 * ks + hh)), qf[ks], s[kt]);
       }
-      const bool need_mask = CAUSAL && (k0 + BK - 1 > qmin_w);
+      // scores stay unscaled; the running max m lives in the scaled log2 domain so each
+      // p = exp2(s*c - m) is one FMA + one raw v_exp_f32 (argument <= 0: exp2f's
+      // denormal fix-up is dead weight).  Only a wave's diagonal tiles mask (uniform branch).
+      if (CAUSAL && k0 + BK - 1 > qmin_w) {
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = k0 + 32 * kt + (r & 3) + 8 * (r >> 2) + 4 * hh;
+            s[kt][r] = key > q ? -INFINITY : s[kt][r];
+          }
+      }
       float mx = -INFINITY;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          float v = s[kt][r] * scale_log2;
-          if (need_mask) {
-            const int key = k0 + 32 * kt + (r & 3) + 8 * (r >> 2) + 4 * hh;
-            if (key > q) v = -INFINITY;
-          }
-          s[kt][r] = v;
-          mx = fmaxf(mx, v);
-        }
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kt][r]);
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mnew = fmaxf(m, mx);
+      const float mnew = fmaxf(m, mx * scale_log2);
       const float msafe = (mnew == -INFINITY) ? 0.f : mnew;
-      const float alpha = exp2f(m - msafe);
+      const float alpha = __builtin_amdgcn_exp2f(m - msafe);
       float rs = 0.f;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float p = exp2f(s[kt][r] - msafe);
+          const float p = __builtin_amdgcn_exp2f(fmaf(s[kt][r], scale_log2, -msafe));
           s[kt][r] = p;
           rs += p;
         }
       rs += __shfl_xor(rs, 32, 64);
       lsum = lsum * alpha + rs;
       m = mnew;
+      if (__ballot(alpha != 1.f)) {   // skip the O rescale when no row's max moved
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
+        for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
+          for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
+      }
       bf16x8 pf[2][2];
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
@@ -340,7 +345,7 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dq_kernel(
         }
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          float p = exp2f(s[r] * scale_log2 - lse2);
+          float p = __builtin_amdgcn_exp2f(s[r] * scale_log2 - lse2);
           if (need_mask) {
             const int key = k0 + 32 * kt + (r & 3) + 8 * (r >> 2) + 4 * hh;
             if (key > q) p = 0.f;
@@ -480,7 +485,7 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
       const bool need_mask = CAUSAL && (kw0 + 31 > q0);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        float p = exp2f(s[r] * c);
+        float p = __builtin_amdgcn_exp2f(s[r] * c);
         if (need_mask && key > q0 + (r & 3) + 8 * (r >> 2) + 4 * hh) p = 0.f;
         s[r] = p;
       }
