@@ -58,6 +58,19 @@ def rope_(x, nheads, head_dim, cos_t, sin_t, seq_len=None, pos=None, inverse=Fal
 rope_tables = reference.rope_tables
 
 
+# ---------------------------------------------------------------- decode GEMM
+def skinny_gemm(x, w, swiglu: bool = False):
+    """Decode-shaped GEMM x[M<=64, K] . w[N, K]^T (weight-streaming HIP kernel on the GPU).
+    ``swiglu``: w = [gate; up] -> silu(x.gate^T) * (x.up^T)."""
+    if x.is_cuda:
+        return _k().skinny_gemm(x, w, swiglu)
+    y = torch.mm(x.float(), w.float().t())
+    if swiglu:
+        F_ = y.shape[1] // 2
+        y = torch.nn.functional.silu(y[:, :F_]) * y[:, F_:]
+    return y.to(x.dtype)
+
+
 # ---------------------------------------------------------------- SwiGLU (K4)
 def swiglu_fwd(gu):
     return _k().swiglu_fwd(gu) if gu.is_cuda else reference.swiglu_fwd(gu)

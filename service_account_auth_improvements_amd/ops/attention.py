@@ -126,6 +126,16 @@ def kv_append_(qkv, Hq, slots, pos, k_cache, v_cache):
         v_cache[sl, :, p] = qkv[b, (Hq + Hkv) * D:(Hq + 2 * Hkv) * D].view(Hkv, D)
 
 
+def rope_append_(qkv, Hq, cos_t, sin_t, slots, pos, k_cache, v_cache):
+    """Decode prologue in one launch: RoPE on the q/k heads of each fused qkv row at pos[b],
+    then the rotated k and v appended at pos[b] of slot slots[b]."""
+    if qkv.is_cuda:
+        return _ext.ops().rope_append_(qkv, Hq, cos_t, sin_t, slots, pos, k_cache, v_cache)
+    Hkv, D = k_cache.shape[1], k_cache.shape[3]
+    reference.rope_(qkv, Hq + Hkv, D, cos_t, sin_t, pos=pos)
+    kv_append_(qkv, Hq, slots, pos, k_cache, v_cache)
+
+
 def kv_fill_(qkv, S, Hq, slot, k_cache, v_cache):
     """Prefill: rows [0, S) of one sequence's fused qkv -> positions [0, S) of `slot`."""
     if qkv.is_cuda:

@@ -12,6 +12,7 @@
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <hip/hip_runtime.h>
 
+#include <map>
 #include <tuple>
 
 extern "C" {
@@ -35,9 +36,12 @@ int kf_flash_bwd(const void*, long, const void*, long, const void*, long, const 
 int kf_decode_splits(int, int, int);
 int kf_decode_attn(const void*, long, const void*, const void*, const int*, const int*, void*, long,
                    float*, float*, int, int, int, int, int, int, float, hipStream_t);
+int kf_rope_append(void*, long, int, int, int, int, const float*, const float*, const int*, const int*, void*,
+                   void*, int, hipStream_t);
 int kf_kv_append(const void*, long, int, int, int, int, const int*, const int*, void*, void*, int,
                  hipStream_t);
 int kf_kv_fill(const void*, long, int, int, int, int, int, void*, void*, int, hipStream_t);
+int kf_skinny_gemm(const void*, long, int, const void*, int, int, void*, long, int, int, hipStream_t);
 }
 
 namespace {
@@ -308,6 +312,25 @@ void kv_append_(const at::Tensor& qkv, int64_t Hq, const at::Tensor& slots, cons
            "kv_append");
 }
 
+// Decode prologue: RoPE on q/k heads of each fused qkv row at pos[b] + append k, v to the cache.
+void rope_append_(at::Tensor& qkv, int64_t Hq, const at::Tensor& cos_t, const at::Tensor& sin_t,
+                  const at::Tensor& slots, const at::Tensor& pos, at::Tensor& kc, at::Tensor& vc) {
+  check_bf16_cuda(qkv, "qkv");
+  const int64_t B = qkv.size(0), Hkv = kc.size(1), D = kc.size(3);
+  check_cache(kc, vc, Hkv, D);
+  TORCH_CHECK(qkv.dim() == 2 && qkv.stride(1) == 1 && qkv.size(1) >= (Hq + 2 * Hkv) * D, "rope_append: qkv");
+  TORCH_CHECK(cos_t.scalar_type() == at::kFloat && sin_t.scalar_type() == at::kFloat && cos_t.is_contiguous() &&
+                  sin_t.is_contiguous() && cos_t.size(-1) == D / 2 && cos_t.size(0) >= kc.size(2),
+              "rope_append: cos/sin tables must be fp32 [>=Lmax, D/2]");
+  check_rows_i32(slots, B, "slots");
+  check_rows_i32(pos, B, "pos");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(qkv.device());
+  check_rc(kf_rope_append(qkv.data_ptr(), qkv.stride(0), (int)B, (int)Hq, (int)Hkv, (int)D, cos_t.data_ptr<float>(),
+                          sin_t.data_ptr<float>(), slots.data_ptr<int>(), pos.data_ptr<int>(), kc.data_ptr(),
+                          vc.data_ptr(), (int)kc.size(2), cur_stream()),
+           "rope_append");
+}
+
 // Prefill: rows [0, S) of one sequence's fused qkv -> positions [0, S) of `slot`.
 void kv_fill_(const at::Tensor& qkv, int64_t S, int64_t Hq, int64_t slot, at::Tensor& kc, at::Tensor& vc) {
   check_bf16_cuda(qkv, "qkv");
@@ -320,6 +343,25 @@ void kv_fill_(const at::Tensor& qkv, int64_t S, int64_t Hq, int64_t slot, at::Te
   check_rc(kf_kv_fill(qkv.data_ptr(), qkv.stride(0), (int)S, (int)Hq, (int)Hkv, (int)D, (int)slot, kc.data_ptr(),
                       vc.data_ptr(), (int)kc.size(2), cur_stream()),
            "kv_fill");
+}
+
+// Decode GEMM: x [M<=64, K] (unit inner stride) . w[N, K]^T -> [M, N]; swiglu: w = [gate; up]
+// (2F rows) -> silu(x.gate^T) * (x.up^T), [M, F].
+at::Tensor skinny_gemm(const at::Tensor& x, const at::Tensor& w, bool swiglu) {
+  check_bf16_cuda(x, "x");
+  check_bf16_cuda(w, "w");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && w.dim() == 2 && w.is_contiguous(), "skinny_gemm: 2-D operands");
+  const int64_t M = x.size(0), K = x.size(1), Nw = w.size(0);
+  TORCH_CHECK(w.size(1) == K, "skinny_gemm: K mismatch");
+  TORCH_CHECK(M >= 1 && M <= 64 && K % 256 == 0, "skinny_gemm: needs 1 <= M <= 64, K % 256 == 0");
+  const int64_t N = swiglu ? Nw / 2 : Nw;
+  TORCH_CHECK(N % 16 == 0 && (!swiglu || Nw % 2 == 0), "skinny_gemm: N % 16 != 0");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  auto y = at::empty({M, N}, x.options());
+  check_rc(kf_skinny_gemm(x.data_ptr(), x.stride(0), (int)M, w.data_ptr(), (int)N, (int)K, y.data_ptr(), y.stride(0),
+                          swiglu ? 1 : 0, (int)N, cur_stream()),
+           "skinny_gemm");
+  return y;
 }
 
 }  // namespace
@@ -336,6 +378,9 @@ TORCH_LIBRARY(kfamd, m) {
   m.def("flash_fwd", &flash_fwd);
   m.def("flash_bwd", &flash_bwd);
   m.def("decode_attn", &decode_attn);
+  m.def("skinny_gemm", &skinny_gemm);
+  m.def("rope_append_(Tensor(a!) qkv, int Hq, Tensor cos, Tensor sin, Tensor slots, Tensor pos, Tensor(b!) kc, "
+        "Tensor(c!) vc) -> ()", &rope_append_);
   m.def("kv_append_(Tensor qkv, int Hq, Tensor slots, Tensor pos, Tensor(a!) kc, Tensor(b!) vc) -> ()", &kv_append_);
   m.def("kv_fill_(Tensor qkv, int S, int Hq, int slot, Tensor(a!) kc, Tensor(b!) vc) -> ()", &kv_fill_);
 }

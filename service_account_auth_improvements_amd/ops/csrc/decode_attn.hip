@@ -227,6 +227,60 @@ extern "C" int kf_decode_attn(const void* q, long q_ld, const void* kc, const vo
   return 0;
 }
 
+// Decode step prologue fused into one launch: RoPE (half-split, fp32 tables) in place on the
+// q and k heads of each fused qkv row at position pos[b], and the rotated k plus v appended
+// to the cache at pos[b] of slot slots[b].  One thread per 8 rotation pairs.
+__global__ void rope_append_kernel(bf16_t* __restrict__ qkv, long ld, int Hq, int Hkv,
+                                   const float* __restrict__ cos_t, const float* __restrict__ sin_t,
+                                   const int* __restrict__ slots, const int* __restrict__ pos,
+                                   bf16_t* __restrict__ kc, bf16_t* __restrict__ vc, int Lmax, int B) {
+  constexpr int HALF = D / 2, CPH = HALF / 8;            // 8 chunks of 8 pairs per head
+  const int it = blockIdx.x * blockDim.x + threadIdx.x;
+  const int per_row = (Hq + 2 * Hkv) * CPH;
+  if (it >= B * per_row) return;
+  const int b = it / per_row, rem = it % per_row, h = rem / CPH, c = rem % CPH;
+  const int p = pos[b];
+  bf16_t* px = qkv + (long)b * ld + (long)h * D + c * 8;
+  const bool is_v = h >= Hq + Hkv;
+  u32x4 lo = ld16(px), hi = ld16(px + HALF);
+  if (!is_v) {
+    float a[8], bb[8], o1[8], o2[8];
+    unpack8(lo, a);
+    unpack8(hi, bb);
+    const float* pc = cos_t + (long)p * HALF + c * 8;
+    const float* ps = sin_t + (long)p * HALF + c * 8;
+    const f32x4 c0 = ldf4(pc), c1 = ldf4(pc + 4), s0 = ldf4(ps), s1 = ldf4(ps + 4);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float cc = j < 4 ? c0[j] : c1[j - 4], ss = j < 4 ? s0[j] : s1[j - 4];
+      o1[j] = a[j] * cc - bb[j] * ss;
+      o2[j] = bb[j] * cc + a[j] * ss;
+    }
+    lo = pack8(o1);
+    hi = pack8(o2);
+    st16(px, lo);
+    st16(px + HALF, hi);
+  }
+  if (h >= Hq) {
+    const int kh = is_v ? h - Hq - Hkv : h - Hq;
+    bf16_t* dst = (is_v ? vc : kc) + (((long)slots[b] * Hkv + kh) * Lmax + p) * D + c * 8;
+    st16(dst, lo);
+    st16(dst + HALF, hi);
+  }
+}
+
+extern "C" int kf_rope_append(void* qkv, long ld, int B, int Hq, int Hkv, int Dh, const float* cos_t,
+                              const float* sin_t, const int* slots, const int* pos, void* kc, void* vc, int Lmax,
+                              hipStream_t st) {
+  if (Dh != D) return 1;
+  if (B == 0) return 0;
+  const int threads = B * (Hq + 2 * Hkv) * (D / 16);
+  hipLaunchKernelGGL(rope_append_kernel, dim3(cdiv(threads, 256)), dim3(256), 0, st, (bf16_t*)qkv, ld, Hq, Hkv,
+                     cos_t, sin_t, slots, pos, (bf16_t*)kc, (bf16_t*)vc, Lmax, B);
+  KF_CHECK_LAUNCH();
+  return 0;
+}
+
 // Append the current token's K/V (post-RoPE, taken from the fused qkv rows) into the cache at
 // position pos[b] of slot slots[b].  One 16-lane group per (row, kv head, k|v).
 __global__ void kv_append_kernel(const bf16_t* __restrict__ qkv, long ld, int Hq, int Hkv,

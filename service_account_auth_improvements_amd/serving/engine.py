@@ -9,7 +9,9 @@ MI355X-first design:
   KV (128 KB/token) -- so there is no paging indirection on the memory-bound decode path.
 * Prefill runs the training forward kernels (fused residual+RMSNorm, fused QKV GEMM, in-place
   RoPE, MFMA flash attention, SwiGLU) and streams K/V into the slot with ``kv_fill_``.
-* Decode appends K/V (``kv_append_``) and runs the split-K GQA decode kernel (K8).  Every
+* Decode appends K/V (``kv_append_``) and runs the split-K GQA decode kernel (K8); for
+  batches <= 16 the projections use the weight-streaming skinny GEMM (ops/csrc/skinny_gemm.hip,
+  gate/up GEMM fused with SwiGLU), larger batches hipBLASLt.  Every
   decode step for a batch-size bucket is captured once in a HIP graph (static input
   buffers, padded rows point at a scratch slot), so a token costs one graph launch instead
   of ~350 kernel launches.
@@ -32,10 +34,12 @@ import torch.distributed as dist
 
 from .. import ops
 from ..models.llama import Llama, LlamaConfig
-from ..ops.attention import attention_fwd, decode_attention, kv_append_, kv_fill_
+from ..ops.attention import attention_fwd, decode_attention, kv_fill_, rope_append_
 from ..parallel.state import ParallelState, tp_all_reduce
 
 BUCKETS = (1, 2, 4, 8, 16, 32, 64, 128, 256)
+SKINNY_MAX_ROWS = 16          # decode batches up to this use the weight-streaming skinny GEMM
+SKINNY_MAX_N = 32768          # beyond this (LM head) hipBLASLt already streams at ~HBM rate
 
 
 class Engine:
@@ -99,18 +103,33 @@ class Engine:
         return self._logits_full(y)[0]
 
     # ------------------------------------------------------------------ decode
+    def _mm(self, x, w):
+        """Decode GEMM: the skinny weight-streaming kernel for small batches on the GPU."""
+        if x.is_cuda and x.shape[0] <= SKINNY_MAX_ROWS and w.shape[0] <= SKINNY_MAX_N and w.shape[1] % 256 == 0:
+            return ops.skinny_gemm(x, w)
+        return torch.mm(x, w.t())
+
+    def _decode_mlp(self, i, h1, da):
+        m, cfg = self.m, self.cfg
+        mm, h2, _ = ops.rmsnorm_fwd(h1, m.P(f"l{i}.norm2"), cfg.norm_eps, residual=da)
+        wgu = m.P(f"l{i}.wgu")
+        if mm.is_cuda and mm.shape[0] <= SKINNY_MAX_ROWS and wgu.shape[1] % 256 == 0:
+            s = ops.skinny_gemm(mm, wgu, swiglu=True)          # gate/up GEMM + SwiGLU in one kernel
+        else:
+            s = ops.swiglu_fwd(torch.mm(mm, wgu.t()))
+        return h2, tp_all_reduce(self._mm(s, m.P(f"l{i}.wd")), m.st)
+
     def _decode_body(self, tokens, slots, pos, lengths):
         m, cfg = self.m, self.cfg
         r = self._embed(tokens)
         d = None
         for li, i in enumerate(m.layers):
             a, h1, _ = ops.rmsnorm_fwd(r, m.P(f"l{i}.norm1"), cfg.norm_eps, residual=d)
-            qkv = torch.mm(a, m.P(f"l{i}.wqkv").t())
-            ops.rope_(qkv, m.hq + m.hkv, cfg.head_dim, m.cos, m.sin, pos=pos)
-            kv_append_(qkv, m.hq, slots, pos, self.kc[li], self.vc[li])
+            qkv = self._mm(a, m.P(f"l{i}.wqkv"))
+            rope_append_(qkv, m.hq, m.cos, m.sin, slots, pos, self.kc[li], self.vc[li])
             o = decode_attention(qkv, self.kc[li], self.vc[li], slots, lengths, m.hq)
-            da = tp_all_reduce(torch.mm(o, m.P(f"l{i}.wo").t()), m.st)
-            r, d = self._mlp(i, h1, da)
+            da = tp_all_reduce(self._mm(o, m.P(f"l{i}.wo")), m.st)
+            r, d = self._decode_mlp(i, h1, da)
         y, _, _ = ops.rmsnorm_fwd(r, m.P("final_norm"), cfg.norm_eps, residual=d)
         return self._logits_full(y)
 
