@@ -504,6 +504,8 @@ def create_app(kube: Client, profiles: ProfilesService, metrics: Optional[Metric
     @app.get("/")
     @app.get("/<path:path>")
     def spa(path="index.html"):
+        if path.startswith("static/"):         # the shared UI bundle (webapps/static/kfamd-ui.js)
+            return send_from_directory(os.path.join(HERE, "static"), path[len("static/"):])
         full = os.path.join(static_dir, path)
         if path != "index.html" and os.path.isfile(full):
             return send_from_directory(static_dir, path)

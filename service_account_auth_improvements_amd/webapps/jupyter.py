@@ -511,7 +511,7 @@ def delete_notebook(notebook, namespace):
 def create_app(kube, name="Jupyter Web App", cfg=None, settings_env=None, pod_log_reader=None):
     cfg = cfg or cb.Config()
     static = os.path.join(HERE, "static", "jupyter")
-    cfg.STATIC_DIR = static
-    app = cb.create_app(name, static, cfg, kube, settings_env=settings_env, pod_log_reader=pod_log_reader)
+    cfg.STATIC_DIR = static                      # index.html of this app
+    app = cb.create_app(name, os.path.join(HERE, "static"), cfg, kube, settings_env=settings_env, pod_log_reader=pod_log_reader)
     app.register_blueprint(bp)
     return app

@@ -90,7 +90,7 @@ def delete_tensorboard(tensorboard, namespace):
 def create_app(kube, name="Tensorboards Web App", cfg=None, settings_env=None):
     cfg = cfg or cb.Config()
     static = os.path.join(HERE, "static", "tensorboards")
-    cfg.STATIC_DIR = static
-    app = cb.create_app(name, static, cfg, kube, settings_env=settings_env)
+    cfg.STATIC_DIR = static                      # index.html of this app
+    app = cb.create_app(name, os.path.join(HERE, "static"), cfg, kube, settings_env=settings_env)
     app.register_blueprint(bp)
     return app

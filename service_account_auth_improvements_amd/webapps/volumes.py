@@ -221,7 +221,7 @@ def delete_viewer(viewer, namespace):
 def create_app(kube, name="Volumes Web App", cfg=None, settings_env=None):
     cfg = cfg or cb.Config()
     static = os.path.join(HERE, "static", "volumes")
-    cfg.STATIC_DIR = static
-    app = cb.create_app(name, static, cfg, kube, settings_env=settings_env)
+    cfg.STATIC_DIR = static                      # index.html of this app
+    app = cb.create_app(name, os.path.join(HERE, "static"), cfg, kube, settings_env=settings_env)
     app.register_blueprint(bp)
     return app

@@ -111,3 +111,10 @@ def test_prometheus_metrics_service():
     assert pts == [{"timestamp": 1700000000.0, "label": "instance=n1", "value": 0.5},
                    {"timestamp": 1700000010.0, "label": "instance=n1", "value": 0.25}]
     assert "node_cpu_seconds_total" in seen[0] and "step=10" in seen[0]
+
+
+def test_dashboard_serves_spa(dash):
+    c, app = dash
+    assert b"kfamd web UI" in app.get("/static/kfamd-ui.js").data
+    assert b'data-app="dashboard"' in app.get("/").data
+    assert b'data-app="dashboard"' in app.get("/some/client/route").data
