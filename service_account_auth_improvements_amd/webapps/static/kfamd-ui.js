@@ -3,7 +3,7 @@
 // Angular/Polymer frontends use (crud-web-apps/*/frontend, centraldashboard/public).
 //
 // Shared pieces (kubeflow-common-lib equivalents): namespace selector, resource table with
-// status icons, exponential-backoff poller (1 s doubling to 32 s, reset on change), snack
+// status icons, exponential-backoff poller (1 s doubling to 8 s, reset on change), snack
 // bar errors, CSRF double-submit header (X-XSRF-TOKEN from the XSRF-TOKEN cookie).
 (function () {
   "use strict";
@@ -57,9 +57,9 @@
     async function tick() {
       try {
         const sig = JSON.stringify(await fn());
-        delay = sig !== last ? 1000 : Math.min(delay * 2, 32000);
+        delay = sig !== last ? 1000 : Math.min(delay * 2, 8000);
         last = sig;
-      } catch (e) { snack(e.message, true); delay = Math.min(delay * 2, 32000); }
+      } catch (e) { snack(e.message, true); delay = Math.min(delay * 2, 8000); }
       if (!stopped) timer = setTimeout(tick, delay);
     }
     tick();
