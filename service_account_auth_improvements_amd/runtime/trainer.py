@@ -48,8 +48,12 @@ class Trainer:
             mcfg = mcfg.with_(max_seq=tcfg.seq_len)
         self.mcfg = mcfg
         assert self.st.pp == 1, "use parallel.pipeline.PipelineTrainer for pp > 1"
+        t0 = time.time()
         self.model = Llama(mcfg, self.st, seed=tcfg.seed, full_init=full_init)
         self.model.allocate(pad_to=self.st.dp * 64 if tcfg.zero1 else 1)
+        self._sync()
+        self.init_times = {"params_alloc_init_s": time.time() - t0}
+        t0 = time.time()
         mode = "reduce_scatter" if (tcfg.zero1 and self.st.dp > 1) else "allreduce"
         self.reducer = GradReducer(self.model.groups, self.st.dp_group, self.st.dp,
                                    bucket_bytes=tcfg.bucket_mb << 20, mode=mode)
@@ -64,9 +68,22 @@ class Trainer:
                              AdamWConfig(lr=tcfg.lr, weight_decay=tcfg.weight_decay,
                                          max_grad_norm=tcfg.max_grad_norm),
                              shard_ranges=shard, dp_group=self.st.dp_group)
+        self._sync()
+        self.init_times["optimizer_state_s"] = time.time() - t0
         self.step_idx = 0
         if mode == "reduce_scatter" and tcfg.overlap_allgather:
             self.model.param_wait = self.reducer.wait_params
+
+    def _sync(self):
+        if self.st.device.type == "cuda":
+            torch.cuda.synchronize()
+
+    def release(self):
+        """Drop every device buffer (params, grads, optimizer state) -- end of job."""
+        self.sync_params()
+        for g in self.model.groups:
+            g.params = g.grads = None
+        self.opt.shards = []
 
     def sync_params(self):
         """Complete any in-flight ZeRO-1 parameter gathers (before checkpoint / eval)."""

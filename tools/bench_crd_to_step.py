@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--micro-batch", type=int, default=1)
     ap.add_argument("--layers", type=int, default=None)
     ap.add_argument("--timeout", type=float, default=300)
+    ap.add_argument("--gap", type=float, default=0.0, help="idle seconds between jobs (GPU memory settle)")
     a = ap.parse_args()
 
     from service_account_auth_improvements_amd.cluster import LocalCluster
@@ -58,6 +59,8 @@ def main():
     rows = []
     try:
         for j in range(a.jobs):
+            if j and a.gap:
+                time.sleep(a.gap)
             name = f"job{j}"
             open(events, "w").close()
             job = training.pytorchjob_manifest(name, "bench", "local", cmd, n_nodes=a.nodes, gpus_per_node=a.gpus,
@@ -88,10 +91,13 @@ def main():
             ini = next(e["ts"] for e in r0 if e["event"] == "init_done")
             imp = next((e["ts"] for e in r0 if e["event"] == "imported"), ps)
             dr = next((e["ts"] for e in r0 if e["event"] == "dist_ready"), imp)
+            ie = next(e for e in r0 if e["event"] == "init_done")
             rows.append({"total": first["ts"] - t0, "cr_to_running": (t_running or ps) - t0,
                          "running_to_process": ps - (t_running or ps), "process_to_init": ini - ps,
                          "import": imp - ps, "dist_init": dr - imp, "model_init": ini - dr,
-                         "init_to_first_step": first["ts"] - ini})
+                         "init_to_first_step": first["ts"] - ini,
+                         "params_alloc_init": ie.get("params_alloc_init_s", 0.0),
+                         "optimizer_state": ie.get("optimizer_state_s", 0.0)})
             print(json.dumps({"job": name, **{k: round(v, 3) for k, v in rows[-1].items()}}), flush=True)
             # wait for the job to finish so the GPUs are free for the next one
             while time.time() < deadline:
@@ -104,11 +110,13 @@ def main():
         cl.stop()
     tot = sorted(r["total"] for r in rows)
     out = {"metric": "CRD-to-first-step", "model": a.model, "gpus_per_node": a.gpus, "nodes": a.nodes,
+           "gap_s": a.gap,
            "jobs": len(rows), "p50_s": round(statistics.median(tot), 3),
            "p90_s": round(tot[min(len(tot) - 1, int(0.9 * len(tot)))], 3), "min_s": round(tot[0], 3),
            "breakdown_p50_s": {k: round(statistics.median(r[k] for r in rows), 3)
                                for k in ("cr_to_running", "running_to_process", "process_to_init", "import",
-                                         "dist_init", "model_init", "init_to_first_step")}}
+                                         "dist_init", "model_init", "params_alloc_init", "optimizer_state",
+                                         "init_to_first_step")}}
     print(json.dumps(out), flush=True)
 
 
