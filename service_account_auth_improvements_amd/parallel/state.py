@@ -60,10 +60,13 @@ def init_distributed(tp: int = 1, pp: int = 1, backend: Optional[str] = None,
     local = int(os.environ.get("LOCAL_RANK", "0"))
     use_gpu = torch.cuda.is_available() if device is None else device.startswith("cuda")
     if backend is None:
-        backend = "nccl" if use_gpu else "gloo"
+        # KFAMD_DIST_BACKEND=gloo: rehearse multi-rank code paths with several ranks on ONE
+        # GPU (RCCL refuses duplicate devices); never for performance numbers
+        backend = os.environ.get("KFAMD_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
     if use_gpu:
-        torch.cuda.set_device(local)
-        dev = torch.device("cuda", local)
+        idx = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(idx)
+        dev = torch.device("cuda", idx)
     else:
         dev = torch.device("cpu")
     assert world % (tp * pp) == 0, f"world {world} not divisible by tp*pp={tp * pp}"

@@ -2,6 +2,7 @@
 fwd y = x @ W^T, dX = dY @ W, dW = dY^T @ x; report TFLOP/s.  Run with and without
 PYTORCH_TUNABLEOP_ENABLED=1 to compare hipBLASLt heuristics vs tuned solutions."""
 import json
+import os
 import sys
 
 import torch
@@ -9,6 +10,9 @@ import torch
 T = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
 H, F, V, Q = 4096, 14336, 128256, 6144
 SHAPES = {"wqkv": (Q, H), "wo": (H, H), "wgu": (2 * F, H), "wd": (H, F), "lm_head": (V, H)}
+if os.environ.get("GEMM_SKIP"):
+    for k in os.environ["GEMM_SKIP"].split(","):
+        SHAPES.pop(k, None)
 
 
 def timeit(fn, iters=10):
