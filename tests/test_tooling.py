@@ -42,3 +42,13 @@ def test_notebook_loadtest():
                        capture_output=True, text=True, timeout=120, cwd=ROOT)
     assert r.returncode == 0, r.stderr
     assert '"ready": 20' in r.stdout
+
+
+def test_conformance_run(tmp_path):
+    """M2: Profile + 2-replica MNIST PyTorchJob (operator -> launcher -> gloo) conformance."""
+    rep = tmp_path / "conf.json"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "conformance.py"), "--report", str(rep)],
+                       capture_output=True, text=True, timeout=280, cwd=ROOT)
+    assert r.returncode == 0, r.stdout + r.stderr
+    import json
+    assert json.load(open(rep))["passed"]
