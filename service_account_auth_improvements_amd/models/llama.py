@@ -203,27 +203,13 @@ class Llama:
 
     # ------------------------------------------------------------------ embedding
     def embed_fwd(self, tokens: torch.Tensor) -> torch.Tensor:
-        E = self.P("embed")
-        if self.tp == 1:
-            return F.embedding(tokens, E)
-        loc = tokens - self.vstart
-        mask = (loc >= 0) & (loc < self.vl)
-        x = F.embedding(loc.clamp(0, self.vl - 1), E) * mask.unsqueeze(-1).to(E.dtype)
-        return tp_all_reduce(x, self.st)
+        """K7 gather (vocab-parallel: rows outside this rank's shard are zero, then summed)."""
+        x = ops.embed_fwd(tokens, self.P("embed"), self.vstart if self.tp > 1 else 0)
+        return tp_all_reduce(x, self.st) if self.tp > 1 else x
 
     def embed_bwd(self, tokens: torch.Tensor, g: torch.Tensor, accumulate: bool):
-        idx = tokens
-        if self.tp > 1:
-            loc = tokens - self.vstart
-            mask = (loc >= 0) & (loc < self.vl)
-            idx = loc.clamp(0, self.vl - 1)
-            g = g * mask.unsqueeze(-1).to(g.dtype)
-        gE = torch.ops.aten.embedding_dense_backward(g, idx, self.vl, -1, False)
-        dst = self.G("embed")
-        if accumulate:
-            dst.add_(gE)
-        else:
-            dst.copy_(gE)
+        """K7 scatter-add straight into the flat gradient buffer's embedding slice."""
+        ops.embed_bwd_(tokens, g, self.G("embed"), self.vstart if self.tp > 1 else 0, accumulate)
         self._ready(self.mats, "embed")
 
     # ------------------------------------------------------------------ decoder layer

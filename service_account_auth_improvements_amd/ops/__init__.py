@@ -58,6 +58,29 @@ def rope_(x, nheads, head_dim, cos_t, sin_t, seq_len=None, pos=None, inverse=Fal
 rope_tables = reference.rope_tables
 
 
+# ---------------------------------------------------------------- embedding (K7)
+def embed_fwd(tokens, E, vstart: int = 0):
+    """Rows E[tok - vstart] for tokens inside this rank's vocab shard, zero elsewhere."""
+    if E.is_cuda:
+        return _k().embed_fwd(tokens.reshape(-1).contiguous(), E, vstart)
+    loc = tokens.reshape(-1) - vstart
+    mask = (loc >= 0) & (loc < E.shape[0])
+    return torch.nn.functional.embedding(loc.clamp(0, E.shape[0] - 1), E) * mask.unsqueeze(-1).to(E.dtype)
+
+
+def embed_bwd_(tokens, g, dE, vstart: int = 0, accumulate: bool = False):
+    """dE[tok - vstart] += g rows (deterministic sorted-run reduction on the GPU)."""
+    if g.is_cuda:
+        return _k().embed_bwd_(tokens.reshape(-1).contiguous(), g.contiguous(), dE, vstart, accumulate)
+    loc = tokens.reshape(-1) - vstart
+    mask = (loc >= 0) & (loc < dE.shape[0])
+    gE = torch.zeros(dE.shape, dtype=torch.float32)
+    gE.index_add_(0, loc[mask], g[mask].float())
+    if accumulate:
+        gE += dE.float()          # fp32 sum, one rounding -- as the GPU kernel
+    dE.copy_(gE)
+
+
 # ---------------------------------------------------------------- decode GEMM
 def skinny_gemm(x, w, swiglu: bool = False):
     """Decode-shaped GEMM x[M<=64, K] . w[N, K]^T (weight-streaming HIP kernel on the GPU).

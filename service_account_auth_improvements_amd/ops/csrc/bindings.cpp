@@ -41,6 +41,8 @@ int kf_rope_append(void*, long, int, int, int, int, const float*, const float*, 
 int kf_kv_append(const void*, long, int, int, int, int, const int*, const int*, void*, void*, int,
                  hipStream_t);
 int kf_kv_fill(const void*, long, int, int, int, int, int, void*, void*, int, hipStream_t);
+int kf_embed_fwd(const long*, const void*, void*, int, int, long, long, hipStream_t);
+int kf_embed_bwd(const long*, const long*, const void*, void*, int, int, long, long, int, hipStream_t);
 int kf_skinny_gemm(const void*, long, int, const void*, int, int, void*, long, int, int, hipStream_t);
 }
 
@@ -102,9 +104,10 @@ at::Tensor rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& h, const at::Tens
     TORCH_CHECK(dres->sizes() == h.sizes() && dres->is_contiguous(), "rmsnorm_bwd: dres shape");
     dr = dres->data_ptr();
   }
-  int nblocks = (int)std::min<int64_t>(256, (rows + 3) / 4);
+  // one block per row at a time; ~4 blocks per CU keep HBM busy, 1024 dW partial rows (16 MB at H=4096)
+  int nblocks = (int)std::min<int64_t>(1024, rows);
   if (nblocks < 1) nblocks = 1;
-  auto part = at::empty({(int64_t)nblocks * 4, H}, h.options().dtype(at::kFloat));
+  auto part = at::empty({(int64_t)nblocks, H}, h.options().dtype(at::kFloat));
   check_rc(kf_rmsnorm_bwd(dy.data_ptr(), h.data_ptr(), rstd.data_ptr<float>(), w.data_ptr(), dr,
                           dh.data_ptr(), part.data_ptr<float>(), nblocks, dw.data_ptr(),
                           accumulate ? 1 : 0, (int)rows, (int)H, cur_stream()),
@@ -364,6 +367,36 @@ at::Tensor skinny_gemm(const at::Tensor& x, const at::Tensor& w, bool swiglu) {
   return y;
 }
 
+// K7 embedding: tokens int64 [T]; E [vl, H] (this rank's vocab shard starting at vstart).
+at::Tensor embed_fwd(const at::Tensor& tok, const at::Tensor& E, int64_t vstart) {
+  check_bf16_cuda(E, "E");
+  TORCH_CHECK(tok.is_cuda() && tok.scalar_type() == at::kLong && tok.is_contiguous(), "embed: tokens int64");
+  TORCH_CHECK(E.dim() == 2 && E.is_contiguous() && E.size(1) % 8 == 0, "embed: E [V, H], H % 8 == 0");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(E.device());
+  auto out = at::empty({tok.numel(), E.size(1)}, E.options());
+  check_rc(kf_embed_fwd(tok.data_ptr<int64_t>(), E.data_ptr(), out.data_ptr(), (int)tok.numel(), (int)E.size(1),
+                        vstart, E.size(0), cur_stream()),
+           "embed_fwd");
+  return out;
+}
+
+// dE (bf16 [vl, H], e.g. a view into the flat gradient buffer) <- scatter-add of g [T, H] by token.
+void embed_bwd_(const at::Tensor& tok, const at::Tensor& g, at::Tensor& dE, int64_t vstart, bool accumulate) {
+  check_bf16_cuda(g, "g");
+  check_bf16_cuda(dE, "dE");
+  TORCH_CHECK(tok.is_cuda() && tok.scalar_type() == at::kLong, "embed_bwd: tokens int64");
+  TORCH_CHECK(g.dim() == 2 && g.is_contiguous() && g.size(0) == tok.numel() && dE.dim() == 2 && dE.is_contiguous() &&
+                  dE.size(1) == g.size(1) && g.size(1) % 8 == 0, "embed_bwd: shapes");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(g.device());
+  if (!accumulate) dE.zero_();
+  auto sorted = at::sort(tok.reshape({-1}));
+  auto keys = std::get<0>(sorted).contiguous();
+  auto perm = std::get<1>(sorted).contiguous();
+  check_rc(kf_embed_bwd(keys.data_ptr<int64_t>(), perm.data_ptr<int64_t>(), g.data_ptr(), dE.data_ptr(),
+                        (int)tok.numel(), (int)g.size(1), vstart, dE.size(0), accumulate ? 1 : 0, cur_stream()),
+           "embed_bwd");
+}
+
 }  // namespace
 
 TORCH_LIBRARY(kfamd, m) {
@@ -379,6 +412,8 @@ TORCH_LIBRARY(kfamd, m) {
   m.def("flash_bwd", &flash_bwd);
   m.def("decode_attn", &decode_attn);
   m.def("skinny_gemm", &skinny_gemm);
+  m.def("embed_fwd", &embed_fwd);
+  m.def("embed_bwd_(Tensor tok, Tensor g, Tensor(a!) dE, int vstart, bool accumulate) -> ()", &embed_bwd_);
   m.def("rope_append_(Tensor(a!) qkv, int Hq, Tensor cos, Tensor sin, Tensor slots, Tensor pos, Tensor(b!) kc, "
         "Tensor(c!) vc) -> ()", &rope_append_);
   m.def("kv_append_(Tensor qkv, int Hq, Tensor slots, Tensor pos, Tensor(a!) kc, Tensor(b!) vc) -> ()", &kv_append_);

@@ -61,31 +61,35 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(
   }
 }
 
+// Backward, one 256-thread block per row at a time (blocks stride over rows).  Each thread
+// owns VPT fixed 16-B column chunks of the row, so the weight and the dW partial stay in ~4*VPT*8
+// registers whatever H is (the wave-per-row form needed 312 VGPRs at H = 4096 and ran at
+// one wave per SIMD, half of HBM bandwidth).  dot(g, h) is reduced across the block.
 template <int VPT>
 __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ h, const float* __restrict__ rstd,
     const bf16_t* __restrict__ w, const bf16_t* __restrict__ dres, bf16_t* __restrict__ dh,
     float* __restrict__ dw_part, int rows, int H) {
-  const int lane = threadIdx.x & 63;
-  const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int nwaves = gridDim.x * 4;
+  __shared__ float red[2][4];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int nv = H >> 3;
   float wf[VPT][8], dwacc[VPT][8];
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
-    const int v = i * 64 + lane;
+    const int v = i * 256 + tid;
     if (v < nv) unpack8(ld16(w + v * 8), wf[i]);
 #pragma unroll
     for (int j = 0; j < 8; ++j) dwacc[i][j] = 0.f;
   }
-  for (int row = wid; row < rows; row += nwaves) {
+  int parity = 0;
+  for (int row = blockIdx.x; row < rows; row += gridDim.x, parity ^= 1) {
     const size_t base = (size_t)row * H;
     const float r = rstd[row];
     float g[VPT][8], hx[VPT][8];
     float dot = 0.f;
 #pragma unroll
     for (int i = 0; i < VPT; ++i) {
-      const int v = i * 64 + lane;
+      const int v = i * 256 + tid;
       if (v < nv) {
         float d[8];
         unpack8(ld16(dy + base + v * 8), d);
@@ -99,10 +103,13 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(
       }
     }
     dot = wave_sum(dot);
+    if (lane == 0) red[parity][wv] = dot;      // double-buffered: no second barrier per row
+    __syncthreads();
+    dot = red[parity][0] + red[parity][1] + red[parity][2] + red[parity][3];
     const float c = r * r * r * dot / (float)H;
 #pragma unroll
     for (int i = 0; i < VPT; ++i) {
-      const int v = i * 64 + lane;
+      const int v = i * 256 + tid;
       if (v < nv) {
         float o[8];
 #pragma unroll
@@ -117,10 +124,10 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(
       }
     }
   }
-  float* out = dw_part + (size_t)wid * H;
+  float* out = dw_part + (size_t)blockIdx.x * H;
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
-    const int v = i * 64 + lane;
+    const int v = i * 256 + tid;
     if (v < nv) {
       stf4(out + v * 8, f32x4{dwacc[i][0], dwacc[i][1], dwacc[i][2], dwacc[i][3]});
       stf4(out + v * 8 + 4, f32x4{dwacc[i][4], dwacc[i][5], dwacc[i][6], dwacc[i][7]});
@@ -184,16 +191,23 @@ int kf_rmsnorm_fwd(const void* a, const void* b, void* h_out, void* y, float* rs
   return 0;
 }
 
-// dw_part must hold (nblocks*4) * H floats; returns nblocks used via *nparts.
+// dw_part must hold nblocks * H floats (one dW partial row per block).
 int kf_rmsnorm_bwd(const void* dy, const void* h, const float* rstd, const void* w,
                    const void* dres, void* dh, float* dw_part, int nblocks, void* dw_out,
                    int accumulate, int rows, int H, hipStream_t s) {
   if (H % 8 != 0 || H > 8192) return 1;
-  DISPATCH_VPT(H / 8, rmsnorm_bwd_kernel<VPT><<<nblocks, 256, 0, s>>>(
-                          (const bf16_t*)dy, (const bf16_t*)h, rstd, (const bf16_t*)w,
-                          (const bf16_t*)dres, (bf16_t*)dh, dw_part, rows, H));
-  colsum_to_bf16_kernel<<<cdiv(H, 64), 1024, 0, s>>>(dw_part, nblocks * 4, H, (bf16_t*)dw_out,
-                                                      accumulate);
+  const int nv = H / 8;
+  if (nv <= 256) {
+    rmsnorm_bwd_kernel<1><<<nblocks, 256, 0, s>>>((const bf16_t*)dy, (const bf16_t*)h, rstd, (const bf16_t*)w,
+                                                 (const bf16_t*)dres, (bf16_t*)dh, dw_part, rows, H);
+  } else if (nv <= 512) {
+    rmsnorm_bwd_kernel<2><<<nblocks, 256, 0, s>>>((const bf16_t*)dy, (const bf16_t*)h, rstd, (const bf16_t*)w,
+                                                 (const bf16_t*)dres, (bf16_t*)dh, dw_part, rows, H);
+  } else {
+    rmsnorm_bwd_kernel<4><<<nblocks, 256, 0, s>>>((const bf16_t*)dy, (const bf16_t*)h, rstd, (const bf16_t*)w,
+                                                 (const bf16_t*)dres, (bf16_t*)dh, dw_part, rows, H);
+  }
+  colsum_to_bf16_kernel<<<cdiv(H, 64), 1024, 0, s>>>(dw_part, nblocks, H, (bf16_t*)dw_out, accumulate);
   return 0;
 }
 

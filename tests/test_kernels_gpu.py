@@ -139,3 +139,28 @@ def test_adamw_flat_and_sumsq():
     assert torch.allclose(m, m2, atol=1e-7, rtol=1e-5)
     assert torch.allclose(v, v2, atol=1e-9, rtol=1e-5)
     assert torch.equal(p, w.to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("vstart,vl,accumulate", [(0, 1000, False), (500, 250, True)])
+def test_embedding_fwd_bwd(vstart, vl, accumulate):
+    """K7: gather + deterministic sorted-run scatter-add vs the fp32 CPU reference (ids repeat)."""
+    from service_account_auth_improvements_amd import ops
+    g = torch.Generator().manual_seed(vl)
+    T, H = 4096, 512
+    tok = torch.randint(0, 1000, (T,), generator=g)
+    tok[:300] = 7 + vstart                        # one long run of a repeated id
+    E = torch.randn(vl, H, generator=g).to(torch.bfloat16)
+    ref = ops.embed_fwd(tok, E, vstart)
+    out = ops.embed_fwd(tok.cuda(), E.cuda(), vstart)
+    assert torch.equal(out.cpu(), ref)
+    gy = torch.randn(T, H, generator=g).to(torch.bfloat16)
+    dE0 = torch.randn(vl, H, generator=g).to(torch.bfloat16)
+    ref_dE = dE0.clone()
+    ops.embed_bwd_(tok, gy, ref_dE, vstart, accumulate)
+    dE = dE0.cuda()
+    ops.embed_bwd_(tok.cuda(), gy.cuda(), dE, vstart, accumulate)
+    err = (dE.float().cpu() - ref_dE.float()).abs().max().item()
+    assert err < 0.1, err
+    dE2 = dE0.cuda()
+    ops.embed_bwd_(tok.cuda(), gy.cuda(), dE2, vstart, accumulate)
+    assert torch.equal(dE, dE2)                   # bit-reproducible
