@@ -161,7 +161,8 @@ class PipelineTrainer:
         self.opt = FlatAdamW(self.model.groups,
                              AdamWConfig(lr=tcfg.lr, weight_decay=tcfg.weight_decay,
                                          max_grad_norm=tcfg.max_grad_norm),
-                             norm_groups=[st.pp_group] if st.pp > 1 else None)
+                             norm_groups=[st.pp_group] if st.pp > 1 else None,
+                             tp_sharded={"matrices": st.tp_group} if st.tp > 1 else None)
         T = tcfg.micro_batch * tcfg.seq_len
         self.p2p = P2P(st, (T, mcfg.hidden), torch.bfloat16, st.device)
 

@@ -40,9 +40,13 @@ class _Shard:
 
 class FlatAdamW:
     def __init__(self, groups: List[FlatGroup], cfg: AdamWConfig = AdamWConfig(),
-                 shard_ranges: Optional[dict] = None, dp_group=None, norm_groups=None):
+                 shard_ranges: Optional[dict] = None, dp_group=None, norm_groups=None,
+                 tp_sharded: Optional[dict] = None):
         """``shard_ranges[group.name] = [(lo, hi), ...]`` restricts state to this rank's
-        ZeRO-1 shard; None keeps full state."""
+        ZeRO-1 shard; None keeps full state.  ``tp_sharded[group.name] = process group``
+        marks flat groups whose parameters are split over that (tensor-parallel) group: their
+        squared gradient norm is summed over it, while replicated groups (norm weights) are
+        counted once -- so every TP rank clips with the same global norm."""
         self.cfg = cfg
         self.groups = groups
         self.step_count = 0
@@ -61,13 +65,26 @@ class FlatAdamW:
                     self.shards.append(_Shard(g, lo, hi, decay))
         dev = groups[0].params.device
         self._sumsq = torch.zeros(1, device=dev, dtype=torch.float32)
+        self.tp_sharded = dict(tp_sharded or {})
+        self._sumsq_tp = torch.zeros(1, device=dev, dtype=torch.float32)
 
     def grad_norm_sq(self) -> torch.Tensor:
         """Global sum of squared (summed-over-DP) gradients, on device."""
-        first = True
+        first, first_tp = True, True
         for sh in self.shards:
-            ops.sumsq_(sh.group.grads[sh.lo:sh.hi], self._sumsq, accumulate=not first)
-            first = False
+            if sh.group.name in self.tp_sharded:
+                ops.sumsq_(sh.group.grads[sh.lo:sh.hi], self._sumsq_tp, accumulate=not first_tp)
+                first_tp = False
+            else:
+                ops.sumsq_(sh.group.grads[sh.lo:sh.hi], self._sumsq, accumulate=not first)
+                first = False
+        if first:
+            self._sumsq.zero_()
+        if not first_tp:
+            tpg = next(iter(self.tp_sharded.values()))
+            if tpg is not None:
+                dist.all_reduce(self._sumsq_tp, group=tpg)
+            self._sumsq.add_(self._sumsq_tp)
         if self.sharded and self.dp_group is not None:
             dist.all_reduce(self._sumsq, group=self.dp_group)
         elif self.sharded and dist.is_initialized() and dist.get_world_size() > 1:

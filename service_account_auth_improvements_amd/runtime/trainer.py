@@ -67,7 +67,8 @@ class Trainer:
         self.opt = FlatAdamW(self.model.groups,
                              AdamWConfig(lr=tcfg.lr, weight_decay=tcfg.weight_decay,
                                          max_grad_norm=tcfg.max_grad_norm),
-                             shard_ranges=shard, dp_group=self.st.dp_group)
+                             shard_ranges=shard, dp_group=self.st.dp_group,
+                             tp_sharded={"matrices": self.st.tp_group} if self.st.tp > 1 else None)
         self._sync()
         self.init_times["optimizer_state_s"] = time.time() - t0
         self.step_idx = 0

@@ -125,3 +125,29 @@ def test_pipeline_1f1b_matches_single_stage():
             assert _close(g, ref.model.G(name).float(), 2e-2), name
             seen.add(name)
     assert seen == {s.name for g in ref.model.groups for s in g.specs}
+
+
+def _tp_train_body(rank, world, clip):
+    from service_account_auth_improvements_amd.parallel.state import init_distributed
+    from service_account_auth_improvements_amd.runtime.trainer import TrainConfig, Trainer
+    st = init_distributed(tp=world, pp=1, device="cpu")
+    tr = Trainer(TrainConfig(model="tiny", seq_len=32, lr=1e-3, max_grad_norm=clip), st, full_init=True)
+    batches = _tiny_batches(tr.mcfg.vocab_size, 2, seed=11)
+    losses = [float(tr.train_step([b])) for b in batches]
+    return losses, tr.model.norms.params.float().clone()
+
+
+def test_tensor_parallel_training_with_clipping_matches_tp1():
+    """TP=2 full steps (AdamW + global-norm clipping across TP shards) == TP=1."""
+    from service_account_auth_improvements_amd.parallel.state import ParallelState
+    from service_account_auth_improvements_amd.runtime.trainer import TrainConfig, Trainer
+    clip = 0.05            # small: clipping is active, so a wrong (per-rank) norm would diverge
+    res = run_ranks(_tp_train_body, world=2, args=(clip,))
+    tr = Trainer(TrainConfig(model="tiny", seq_len=32, lr=1e-3, max_grad_norm=clip), ParallelState(), full_init=True)
+    batches = _tiny_batches(tr.mcfg.vocab_size, 2, seed=11)
+    ref = [float(tr.train_step([b])) for b in batches]
+    for r in res:
+        assert abs(r[0][1] - ref[1]) < 2e-2 * abs(ref[1]), (r[0], ref)
+    # replicated norm weights: identical across TP ranks and close to TP=1
+    assert torch.equal(res[0][1], res[1][1])
+    assert _close(res[0][1], tr.model.norms.params.float(), 1e-2)
