@@ -299,6 +299,21 @@ class Llama:
         lo = g.spec(first).offset
         self.param_wait(g, lo, g.end_offset(last))
 
+    def param_segments(self):
+        """Forward-ordered parameter ranges ``(group, lo, hi)``: exactly the ranges the
+        forward's ``param_wait`` hook asks for (embedding, per-layer matrices / norms, head)."""
+        segs = []
+        rng = lambda g, a, b: (g, g.spec(a).offset, g.end_offset(b))  # noqa: E731
+        if self.first:
+            segs.append(rng(self.mats, "embed", "embed"))
+        for i in self.layers:
+            segs.append(rng(self.mats, f"l{i}.wd", f"l{i}.wqkv"))
+            segs.append(rng(self.norms, f"l{i}.norm2", f"l{i}.norm1"))
+        if self.last:
+            segs.append(rng(self.mats, "lm_head", "lm_head"))
+            segs.append(rng(self.norms, "final_norm", "final_norm"))
+        return segs
+
     def _wait_layer(self, i: int):
         if self.param_wait is not None:
             self._wait(f"l{i}.wd", f"l{i}.wqkv")

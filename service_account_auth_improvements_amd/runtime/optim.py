@@ -66,6 +66,7 @@ class FlatAdamW:
         dev = groups[0].params.device
         self._sumsq = torch.zeros(1, device=dev, dtype=torch.float32)
         self.tp_sharded = dict(tp_sharded or {})
+        self._pending: list = []   # (group name, lo, hi, event) of in-flight async update segments
         self._sumsq_tp = torch.zeros(1, device=dev, dtype=torch.float32)
 
     def grad_norm_sq(self) -> torch.Tensor:
@@ -93,17 +94,59 @@ class FlatAdamW:
             dist.all_reduce(self._sumsq, group=g)
         return self._sumsq
 
-    def step(self, grad_scale: float = 1.0, lr: Optional[float] = None):
-        """grad_scale multiplies raw gradients (e.g. 1/dp for SUM-reduced grads)."""
+    def step(self, grad_scale: float = 1.0, lr: Optional[float] = None, segments=None, stream=None):
+        """grad_scale multiplies raw gradients (e.g. 1/dp for SUM-reduced grads).
+
+        ``stream`` + ``segments`` (a forward-ordered list of ``(group, lo, hi)`` parameter
+        ranges): after the gradient norm is known, the update runs segment by segment on
+        ``stream`` and each segment records an event; :meth:`wait_params` makes the compute
+        stream wait for exactly the segment the next forward is about to read, so the
+        HBM-bound AdamW overlaps the next step's MFMA-bound forward instead of serialising
+        with it."""
         c = self.cfg
         self.step_count += 1
         lr = c.lr if lr is None else lr
         sumsq = self.grad_norm_sq() if c.max_grad_norm > 0 else None
-        for sh in self.shards:
-            ops.adamw_(sh.group.params[sh.lo:sh.hi], sh.master, sh.m, sh.v,
-                       sh.group.grads[sh.lo:sh.hi], (sh.hi - sh.lo) if sh.decay else 0,
+
+        def upd(sh, a, b):
+            ops.adamw_(sh.group.params[a:b], sh.master[a - sh.lo:b - sh.lo], sh.m[a - sh.lo:b - sh.lo],
+                       sh.v[a - sh.lo:b - sh.lo], sh.group.grads[a:b], (b - a) if sh.decay else 0,
                        lr, c.betas[0], c.betas[1], c.eps, c.weight_decay, self.step_count,
                        grad_scale, sumsq, c.max_grad_norm)
+
+        if stream is None or segments is None:
+            for sh in self.shards:
+                upd(sh, sh.lo, sh.hi)
+            return
+        self.wait_all()
+        ready = torch.cuda.Event()
+        ready.record()
+        stream.wait_event(ready)
+        with torch.cuda.stream(stream):
+            for g, lo, hi in segments:
+                for sh in self.shards:
+                    if sh.group is g and sh.hi > lo and sh.lo < hi:
+                        upd(sh, max(lo, sh.lo), min(hi, sh.hi))
+                ev = torch.cuda.Event()
+                ev.record(stream)
+                self._pending.append((g.name, lo, hi, ev))
+
+    def wait_params(self, group: FlatGroup, lo: int, hi: int):
+        """Compute stream waits for the pending update segments overlapping [lo, hi)."""
+        if not self._pending:
+            return
+        keep = []
+        for name, a, b, ev in self._pending:
+            if name == group.name and a < hi and b > lo:
+                torch.cuda.current_stream().wait_event(ev)
+            else:
+                keep.append((name, a, b, ev))
+        self._pending = keep
+
+    def wait_all(self):
+        for _, _, _, ev in self._pending:
+            torch.cuda.current_stream().wait_event(ev)
+        self._pending = []
 
     def state_dict(self):
         return {"step": self.step_count,

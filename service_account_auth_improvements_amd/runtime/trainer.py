@@ -28,6 +28,10 @@ class TrainConfig:
     grad_accum: int = 1
     zero1: bool = False
     overlap_allgather: bool = True   # ZeRO-1: hide the param all-gather behind the next forward
+    # AdamW on a side stream overlapped with the next forward (GPU, no ZeRO).  Measured on MI355X:
+    # 64% of AdamW time overlaps, but both sides slow down (HBM/CU contention) -- no net gain
+    # at 8B (profiles/async_optimizer_overlap.txt), so it is off by default.
+    async_optimizer: bool = False
     bucket_mb: int = 256
     lr: float = 3e-4
     weight_decay: float = 0.1
@@ -72,8 +76,14 @@ class Trainer:
         self._sync()
         self.init_times["optimizer_state_s"] = time.time() - t0
         self.step_idx = 0
+        self._opt_stream = None
+        self._segments = None
         if mode == "reduce_scatter" and tcfg.overlap_allgather:
             self.model.param_wait = self.reducer.wait_params
+        elif mode == "allreduce" and tcfg.async_optimizer and self.st.device.type == "cuda":
+            self._opt_stream = torch.cuda.Stream(device=self.st.device)
+            self._segments = self.model.param_segments()
+            self.model.param_wait = self.opt.wait_params
 
     def _sync(self):
         if self.st.device.type == "cuda":
@@ -87,8 +97,10 @@ class Trainer:
         self.opt.shards = []
 
     def sync_params(self):
-        """Complete any in-flight ZeRO-1 parameter gathers (before checkpoint / eval)."""
+        """Complete in-flight ZeRO-1 parameter gathers / async optimizer segments (before
+        checkpoint, eval or host reads of the parameters)."""
         self.reducer.wait_all_params()
+        self.opt.wait_all()
 
     @property
     def tokens_per_step(self) -> int:
@@ -108,7 +120,7 @@ class Trainer:
         self.model.on_grad_ready = None
         self.reducer.wait_all_params()     # a bucket the forward never read (padding) must land too
         self.reducer.finish()
-        self.opt.step(grad_scale=1.0 / self.st.dp)
+        self.opt.step(grad_scale=1.0 / self.st.dp, segments=self._segments, stream=self._opt_stream)
         self.reducer.all_gather_params(overlap=self.tcfg.overlap_allgather)
         self.step_idx += 1
         return total
