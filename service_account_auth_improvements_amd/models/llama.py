@@ -196,6 +196,12 @@ class Llama:
 
     @staticmethod
     def _mm_into(out, a, b, accumulate):
+        """out (+)= a . b.  Weight gradients (a = dY^T, a transposed view of [T, N]) go to the
+        hand-written gfx950 dW kernel (ops/csrc/gemm.hip, faster than hipBLASLt's TN
+        solutions at every Llama shape) when its tiling constraints hold."""
+        if a.is_cuda and a.stride(0) == 1 and ops.gemm_tn_ok(a.t(), b, out):
+            ops.gemm_tn_(a.t(), b, out, accumulate)
+            return
         if accumulate:
             out.addmm_(a, b)
         else:

@@ -94,6 +94,23 @@ def skinny_gemm(x, w, swiglu: bool = False):
     return y.to(x.dtype)
 
 
+# ---------------------------------------------------------------- weight-gradient GEMM
+def gemm_tn_ok(a, b, c) -> bool:
+    """True when the HIP weight-gradient GEMM handles c = a^T b for these operands."""
+    return a.is_cuda and _k().gemm_tn_ok(a, b, c)
+
+
+def gemm_tn_(a, b, c, accumulate: bool = False):
+    """c[M, N] (+)= a^T . b, a = [K, M], b = [K, N] (K = tokens): the dW = dY^T X product,
+    hand-written MFMA kernel (ops/csrc/gemm.hip) on the GPU."""
+    if a.is_cuda:
+        return _k().gemm_tn_(a, b, c, accumulate)
+    r = torch.mm(a.float().t(), b.float())
+    if accumulate:
+        r += c.float()
+    c.copy_(r)
+
+
 # ---------------------------------------------------------------- SwiGLU (K4)
 def swiglu_fwd(gu):
     return _k().swiglu_fwd(gu) if gu.is_cuda else reference.swiglu_fwd(gu)

@@ -44,6 +44,7 @@ int kf_kv_fill(const void*, long, int, int, int, int, int, void*, void*, int, hi
 int kf_embed_fwd(const long*, const void*, void*, int, int, long, long, hipStream_t);
 int kf_embed_bwd(const long*, const long*, const void*, void*, int, int, long, long, int, hipStream_t);
 int kf_skinny_gemm(const void*, long, int, const void*, int, int, void*, long, int, int, hipStream_t);
+int kf_gemm_tn(const void*, long, const void*, long, void*, long, int, int, int, int, hipStream_t);
 }
 
 namespace {
@@ -367,6 +368,29 @@ at::Tensor skinny_gemm(const at::Tensor& x, const at::Tensor& w, bool swiglu) {
   return y;
 }
 
+// Weight-gradient GEMM: C[M, N] (+)= a^T . b with a = [K, M], b = [K, N] (row stride may
+// exceed the width: views into fused activations); C may be a view into the flat grad buffer.
+bool gemm_tn_ok(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c) {
+  if (!a.is_cuda() || a.scalar_type() != at::kBFloat16 || b.scalar_type() != at::kBFloat16 ||
+      c.scalar_type() != at::kBFloat16)
+    return false;
+  if (a.dim() != 2 || b.dim() != 2 || c.dim() != 2 || a.stride(1) != 1 || b.stride(1) != 1 || c.stride(1) != 1)
+    return false;
+  const int64_t K = a.size(0), M = a.size(1), N = b.size(1);
+  return b.size(0) == K && c.size(0) == M && c.size(1) == N && M % 256 == 0 && N % 256 == 0 && K % 128 == 0 &&
+         a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 && c.stride(0) % 4 == 0 &&
+         (reinterpret_cast<uintptr_t>(a.data_ptr()) & 15) == 0 && (reinterpret_cast<uintptr_t>(b.data_ptr()) & 15) == 0 &&
+         (reinterpret_cast<uintptr_t>(c.data_ptr()) & 7) == 0 && K < (1l << 31) && M < (1l << 31);
+}
+
+void gemm_tn_(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, bool accumulate) {
+  TORCH_CHECK(gemm_tn_ok(a, b, c), "gemm_tn: unsupported shapes/strides (needs M, N % 256, K % 128, bf16)");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(a.device());
+  check_rc(kf_gemm_tn(a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(), c.stride(0), (int)a.size(1),
+                      (int)b.size(1), (int)a.size(0), accumulate ? 1 : 0, cur_stream()),
+           "gemm_tn");
+}
+
 // K7 embedding: tokens int64 [T]; E [vl, H] (this rank's vocab shard starting at vstart).
 at::Tensor embed_fwd(const at::Tensor& tok, const at::Tensor& E, int64_t vstart) {
   check_bf16_cuda(E, "E");
@@ -412,6 +436,8 @@ TORCH_LIBRARY(kfamd, m) {
   m.def("flash_bwd", &flash_bwd);
   m.def("decode_attn", &decode_attn);
   m.def("skinny_gemm", &skinny_gemm);
+  m.def("gemm_tn_ok", &gemm_tn_ok);
+  m.def("gemm_tn_(Tensor a, Tensor b, Tensor(a!) c, bool accumulate) -> ()", &gemm_tn_);
   m.def("embed_fwd", &embed_fwd);
   m.def("embed_bwd_(Tensor tok, Tensor g, Tensor(a!) dE, int vstart, bool accumulate) -> ()", &embed_bwd_);
   m.def("rope_append_(Tensor(a!) qkv, int Hq, Tensor cos, Tensor sin, Tensor slots, Tensor pos, Tensor(b!) kc, "

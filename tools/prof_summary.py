@@ -7,6 +7,7 @@ tot = sum(float(r['TotalDurationNs']) for r in rows)
 cats = {}
 def cat(n):
     if n.startswith('Cijk') or 'Custom_Cijk' in n: return 'GEMM (hipBLASLt)'
+    if 'gemm_tn' in n: return 'GEMM dW (HIP, MFMA 16x16x32)'
     if 'flash_fwd' in n: return 'attention fwd (HIP)'
     if 'flash_bwd' in n: return 'attention bwd (HIP)'
     if 'adamw' in n or 'sumsq' in n or 'sum_final' in n: return 'optimizer (HIP)'
