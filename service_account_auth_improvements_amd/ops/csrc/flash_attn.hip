@@ -20,7 +20,8 @@
 //    kv-head), so its K/V (fwd, dQ) or Q/dO (dK/dV) stay in that XCD's 4 MB L2; causal
 //    work is launched heaviest-first.
 //
-// Forward: 1 workgroup = 4 waves x 32 query rows, 64-key tiles, online softmax (exp2).
+// Forward: 1 workgroup = 8 waves x 32 query rows, 64-key tiles in a 4-deep LDS-DMA ring,
+// online softmax (exp2) with the running max folded into the MFMA chain (see the kernel).
 // Backward, two kernels, no dQ atomics:
 //  * dQ kernel (forward-shaped, per 128 query rows): S^T, dP^T = V.dO^T, P^T, dS^T,
 //    dQ^T += K^T.dS^T; dQ written once as bf16 into the dqkv buffer.
@@ -45,7 +46,7 @@ constexpr int BK = 64;            // keys per tile (forward / dQ)
 constexpr int TILE = BK * D * 2;  // 16 KB
 constexpr int BKV = 128;          // keys per dK/dV workgroup (4 waves x 32)
 constexpr int QT = 32;            // query rows per dK/dV iteration
-constexpr int QCH = 1024;         // query rows per dK/dV work item
+constexpr int QCH = 1024;         // query rows per dK/dV work item (512 / 2048: 6 % / 4 % slower)
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float LN2 = 0.6931471805599453f;
 
@@ -126,97 +127,182 @@ __device__ __forceinline__ QBlock decode_qblock(int S, int Hq, int Hkv, int B, b
 
 using namespace fa;
 
+// xor-32 lane reductions by v_permlane32_swap (no LDS round trip on the softmax path)
+__device__ __forceinline__ float xor32_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xor32_sum(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float bf16_round(float x) { return (float)(__bf16)x; }
+__device__ __forceinline__ u32 lds_addr(const void* p) { return (u32)(uintptr_t)LDS_PTR(const char, p); }
+// one MFMA operand fragment = two transposed 4x16 reads, in inline asm: hipcc treats every
+// compiler-visible LDS read as aliasing an in-flight LDS-DMA and would wait vmcnt(0) first
+__device__ __forceinline__ bf16x8 tr_pair_asm(u32 a0, u32 a1) {
+  u32x2 x, y;
+  asm volatile("ds_read_b64_tr_b16 %0, %2\n\tds_read_b64_tr_b16 %1, %3" : "=&v"(x), "=v"(y) : "v"(a0), "v"(a1) : "memory");
+  return as_bf16x8(u32x4{x[0], x[1], y[0], y[1]});
+}
+// wait until at most N LDS operations are outstanding; ties the fragments that become valid
+template <int N>
+__device__ __forceinline__ void lgkm_wait_tie(bf16x8* f) {
+  asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]) : "i"(N) : "memory");
+}
+__device__ __forceinline__ void barrier() { asm volatile("s_barrier" ::: "memory"); }
+template <int N>
+__device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory"); }
+// Row constant folded into an MFMA chain as one extra k-chunk: A holds a ones column at
+// k = 0, 1 and B the (hi, lo) bf16 split of -c for this lane's row, so the product adds
+// -c (to ~2^-16 relative) to every accumulator element of the row.
+__device__ __forceinline__ bf16x8 fold_ones(int hh) {
+  return hh ? bf16x8{} : bf16x8{(__bf16)1.f, (__bf16)1.f, 0, 0, 0, 0, 0, 0};
+}
+__device__ __forceinline__ bf16x8 fold_const(float c, int hh) {
+  const __bf16 hi = (__bf16)(-c);
+  const __bf16 lo = (__bf16)(-c - (float)hi);
+  return hh ? bf16x8{} : bf16x8{hi, lo, 0, 0, 0, 0, 0, 0};
+}
+
 // ====================================================================================
 // Forward
 // ====================================================================================
+// 1 workgroup = 8 waves x 32 query rows (256 rows), one workgroup per CU (2 waves per SIMD).
+//  * K/V 64-key tiles arrive by LDS-DMA in a 4-deep ring of K+V stages (128 KB): the DMA
+//    runs three tiles ahead and each tile is published by a COUNTED vmcnt + raw s_barrier
+//    (a __syncthreads() would drain every stage in flight).  Each staged tile feeds 8 waves.
+//  * The loop is VALU-issue bound (two waves share a SIMD's vector issue; an MFMA holds it
+//    for 8 of its 32 cycles), so the softmax is put on a diet: Q is pre-scaled by
+//    scale*log2(e) once, and the running row max m (bf16-exact) rides in the S^T MFMA
+//    chain as a folded row constant, so p = exp2(S') costs one v_exp and no FMA.  m only
+//    moves (rescaling O, l and the tile) when a row's tile max exceeds it by > 2^8, which
+//    after the first tiles is rare -- the per-tile rescale of the usual online softmax is
+//    gone.  (Measured: +10 % over the FMA form; an MFMA row sum instead of the 32 VALU adds
+//    and static younger-half priority were both slower or null.)
+//  * V^T fragments for output block t+1 are read while block t's MFMAs run.
+constexpr int BQ8 = 256, NST = 4, STG = 2 * TILE;   // stage = K tile + V tile (32 KB)
+constexpr float FOLD_T = 8.f;                       // tolerated growth of p above 1 (log2)
+
+// wait until stage `next` landed, given that stages up to `last` were issued (4 DMA
+// instructions per wave per stage, retired in order)
+__device__ __forceinline__ void wait_stage(int next, int last) {
+  const int ahead = last - next;
+  if (ahead >= 2) vm_wait<8>();
+  else if (ahead == 1) vm_wait<4>();
+  else vm_wait<0>();
+}
+
 template <bool CAUSAL>
-__global__ __launch_bounds__(256, 2) void flash_fwd_kernel(
+__global__ __launch_bounds__(512, 1) void flash_fwd_kernel(
     const bf16_t* __restrict__ qkv, long ld, bf16_t* __restrict__ out, long ldo,
     float* __restrict__ lse_out, int B, int S, int Hq, int Hkv, float scale_log2) {
-  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];  // K0 K1 V0 V1
-  const QBlock blk = decode_qblock(S, Hq, Hkv, B, CAUSAL);
-  const int b = blk.b, h = blk.h, hkv = blk.hkv, qb = blk.qb;
+  __shared__ __attribute__((aligned(16))) char smem[NST * STG];
+  const int nqb = (S + BQ8 - 1) / BQ8, G = Hq / Hkv;
+  // logical order [b][hkv][q-block][g]: an XCD's contiguous range shares one K/V panel
+  int lid = xcd_remap(blockIdx.x, B * Hq * nqb);
+  const int g = lid % G;
+  lid /= G;
+  int qb = lid % nqb;
+  lid /= nqb;
+  const int hkv = lid % Hkv, b = lid / Hkv, h = hkv * G + g;
+  if (CAUSAL) qb = nqb - 1 - qb;   // heaviest blocks first
+
   const int tid = threadIdx.x, l = tid & 63, lr = l & 31, hh = l >> 5;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int q = qb * BQ + w * 32 + lr;
-  const int qmin_w = qb * BQ + w * 32, qmax_w = qmin_w + 31;
+  const int q = qb * BQ8 + w * 32 + lr;
+  const int qmin_w = qb * BQ8 + w * 32, qmax_w = qmin_w + 31;
+  const bool live = qmin_w < S;   // the last block of S % 256 == 128 has 4 idle waves
 
   bf16x8 qf[8];  // B operand of S^T = K Q^T: Q[q][16ks + 8hh .. +8]
   {
-    const bf16_t* qp = qkv + ((long)b * S + q) * ld + (long)h * D + 8 * hh;
+    const bf16_t* qp = qkv + ((long)b * S + min(q, S - 1)) * ld + (long)h * D + 8 * hh;
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) qf[ks] = as_bf16x8(ld16(qp + 16 * ks));
   }
   const bf16_t* kp = qkv + (long)b * S * ld + (long)(Hq + hkv) * D;
   const bf16_t* vp = qkv + (long)b * S * ld + (long)(Hq + Hkv + hkv) * D;
-  auto stage = [&](int j, int buf) {
-    stage_rows(kp + (long)j * BK * ld, ld, smem + buf * TILE, BK, w, 4, l);
-    stage_rows(vp + (long)j * BK * ld, ld, smem + (2 + buf) * TILE, BK, w, 4, l);
+  auto stage = [&](int j) {
+    char* st = smem + (j % NST) * STG;
+    stage_rows(kp + (long)j * BK * ld, ld, st, BK, w, 8, l);
+    stage_rows(vp + (long)j * BK * ld, ld, st + TILE, BK, w, 8, l);
   };
+  const int ntiles = CAUSAL ? min(S, qb * BQ8 + BQ8) / BK : S / BK;
+  for (int j = 0; j < NST - 1 && j < ntiles; ++j) stage(j);
 
+  // retire the Q loads HERE (the compiler's wait counts only them, the DMA stays in flight):
+  // a first use inside the loop would make hipcc wait vmcnt(0) on every tile
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) asm volatile("" : "+v"(qf[ks]));
+  const bf16x8 ones = fold_ones(hh);
+  bf16x8 mref = bf16x8{};    // folded -m (m bf16-exact: the hi part carries it, lo = 0)
+  bool first = true;
+  const float thresh = FOLD_T / scale_log2;   // m and S' are in raw score units
+  float m = 0.f, lsum = 0.f;
   f32x16 o[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) o[t] = f32x16{};
-  float m = -INFINITY, lsum = 0.f;
-  const int ntiles = CAUSAL ? (qb * BQ + BQ) / BK : S / BK;
   const int vrow = 4 * hh + ((l & 15) >> 2);
   const int vcol = 16 * ((l >> 4) & 1) + 4 * (l & 3);
 
-  stage(0, 0);
-  wait_dma_barrier();
+  wait_stage(0, min(NST - 2, ntiles - 1));
+  barrier();
   for (int j = 0; j < ntiles; ++j) {
-    const int cur = j & 1;
-    if (j + 1 < ntiles) stage(j + 1, cur ^ 1);
+    if (j + NST - 1 < ntiles) stage(j + NST - 1);   // refills the buffer of tile j-1
     const int k0 = j * BK;
-    if (!CAUSAL || k0 <= qmax_w) {
-      const char* Ks = smem + cur * TILE;
-      const char* Vs = smem + (2 + cur) * TILE;
-      f32x16 s[2];
+    if (live && (!CAUSAL || k0 <= qmax_w)) {
+      const char* Ks = smem + (j % NST) * STG;
+      const char* Vs = Ks + TILE;
+      f32x16 sc[2];   // S'^T = K (c Q)^T - m: key on the accumulator rows, query on the lane
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
-        s[kt] = f32x16{};
+        sc[kt] = mfma32(ones, mref, f32x16{});
 #pragma unroll
-        for (int ks = 0; ks < 8; ++ks) s[kt] = mfma32(row_read(Ks, swz(32 * kt + lr, 2 * ks + hh)), qf[ks], s[kt]);
+        for (int ks = 0; ks < 8; ++ks) sc[kt] = mfma32(row_read(Ks, swz(32 * kt + lr, 2 * ks + hh)), qf[ks], sc[kt]);
       }
-      // scores stay unscaled; the running max m lives in the scaled log2 domain so each
-      // p = exp2(s*c - m) is one FMA + one raw v_exp_f32 (argument <= 0: exp2f's
-      // denormal fix-up is dead weight).  Only a wave's diagonal tiles mask (uniform branch).
-      if (CAUSAL && k0 + BK - 1 > qmin_w) {
+      if (CAUSAL && k0 + BK - 1 > qmin_w) {   // a wave's diagonal tiles only (uniform branch)
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int key = k0 + 32 * kt + (r & 3) + 8 * (r >> 2) + 4 * hh;
-            s[kt][r] = key > q ? -INFINITY : s[kt][r];
+            sc[kt][r] = key > q ? -INFINITY : sc[kt][r];
           }
       }
       float mx = -INFINITY;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kt][r]);
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mnew = fmaxf(m, mx * scale_log2);
-      const float msafe = (mnew == -INFINITY) ? 0.f : mnew;
-      const float alpha = __builtin_amdgcn_exp2f(m - msafe);
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sc[kt][r]);
+      mx = xor32_max(mx);
+      if (__ballot(first || mx > thresh)) {
+        // move the reference: m' = bf16(m + max(mx, 0)); rescale O, l and this tile's S'
+        const float mnew = first ? bf16_round(mx) : bf16_round(m + fmaxf(mx, 0.f));
+        const float shift = first ? mnew : mnew - m;
+        const float alpha = first ? 0.f : __builtin_amdgcn_exp2f(-shift * scale_log2);
+        lsum *= alpha;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) sc[kt][r] -= shift;
+        m = mnew;
+        first = false;
+        mref = fold_const(m, hh);
+      }
       float rs = 0.f;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float p = __builtin_amdgcn_exp2f(fmaf(s[kt][r], scale_log2, -msafe));
-          s[kt][r] = p;
+          const float p = __builtin_amdgcn_exp2f(sc[kt][r] * scale_log2);
+          sc[kt][r] = p;
           rs += p;
         }
-      rs += __shfl_xor(rs, 32, 64);
-      lsum = lsum * alpha + rs;
-      m = mnew;
-      if (__ballot(alpha != 1.f)) {   // skip the O rescale when no row's max moved
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
-      }
+      lsum += xor32_sum(rs);
       bf16x8 pf[2][2];
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
@@ -224,21 +310,42 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(
         for (int ss = 0; ss < 2; ++ss) {
           u32x4 u;
 #pragma unroll
-          for (int i = 0; i < 4; ++i) u[i] = pack2(s[kt][8 * ss + 2 * i], s[kt][8 * ss + 2 * i + 1]);
+          for (int i = 0; i < 4; ++i) u[i] = pack2(sc[kt][8 * ss + 2 * i], sc[kt][8 * ss + 2 * i + 1]);
           pf[kt][ss] = as_bf16x8(u);
         }
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
+      // O^T += V^T P^T; the V^T fragments of block t+1 are read while block t's MFMAs run
+      const u32 vbase = lds_addr(Vs);
+      bf16x8 vf[2][4];
+      auto v_read = [&](int t, bf16x8* f) {
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
           for (int ss = 0; ss < 2; ++ss) {
             const int row = 32 * kt + 16 * ss + vrow, col = 32 * t + vcol;
-            o[t] = mfma32(tr_pair(Vs, swz8(row, col), swz8(row + 8, col)), pf[kt][ss], o[t]);
+            f[2 * kt + ss] = tr_pair_asm(vbase + swz8(row, col), vbase + swz8(row + 8, col));
           }
+      };
+      v_read(0, vf[0]);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        if (t < 3) {
+          v_read(t + 1, vf[(t + 1) & 1]);
+          lgkm_wait_tie<8>(vf[t & 1]);
+        } else {
+          lgkm_wait_tie<0>(vf[t & 1]);
+        }
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int ss = 0; ss < 2; ++ss) o[t] = mfma32(vf[t & 1][2 * kt + ss], pf[kt][ss], o[t]);
+      }
     }
-    wait_dma_barrier();
+    if (j + 1 < ntiles) {
+      wait_stage(j + 1, min(j + NST - 1, ntiles - 1));
+      barrier();
+    }
   }
+  if (!live) return;
   const float inv = 1.f / lsum;
   bf16_t* op = out + ((long)b * S + q) * ldo + (long)h * D;
 #pragma unroll
@@ -251,7 +358,7 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(
       v[1] = pack2(o[t][4 * gq + 2] * inv, o[t][4 * gq + 3] * inv);
       *reinterpret_cast<u32x2*>(op + d) = v;
     }
-  if (hh == 0) lse_out[((long)b * Hq + h) * S + q] = (m + log2f(lsum)) * LN2;
+  if (hh == 0) lse_out[((long)b * Hq + h) * S + q] = (m * scale_log2 + log2f(lsum)) * LN2;
 }
 
 // ====================================================================================
@@ -286,72 +393,91 @@ __global__ __launch_bounds__(256) void flash_bwd_pre_kernel(const bf16_t* __rest
 // ====================================================================================
 // Backward: dQ (forward-shaped)
 // ====================================================================================
+// Same skeleton as the forward (8 waves x 32 query rows, 4-deep K+V LDS-DMA ring, counted
+// vmcnt + raw barrier).  Per 64-key tile: S'^T = K Q^T - lse/scale and dP'^T = V dO^T - delta
+// come out of the MFMA chains with both row constants folded in (hi/lo bf16 split, no
+// accumulator-initialising moves), so dS^T = exp2(c S') * dP' per element; dQ^T += K^T dS^T
+// with the K^T fragments read (inline asm, counted waits) one output block ahead.
 template <bool CAUSAL>
-__global__ __launch_bounds__(256, 2) void flash_bwd_dq_kernel(
+__global__ __launch_bounds__(512, 1) void flash_bwd_dq_kernel(
     const bf16_t* __restrict__ qkv, long ld, const bf16_t* __restrict__ dout, long lddo,
     const float* __restrict__ lse, const float* __restrict__ delta, bf16_t* __restrict__ dqkv,
     long lddq, int B, int S, int Hq, int Hkv, float scale_log2, float scale) {
-  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];  // K0 K1 V0 V1
-  const QBlock blk = decode_qblock(S, Hq, Hkv, B, CAUSAL);
-  const int b = blk.b, h = blk.h, hkv = blk.hkv, qb = blk.qb;
+  __shared__ __attribute__((aligned(16))) char smem[NST * STG];
+  const int nqb = (S + BQ8 - 1) / BQ8, G = Hq / Hkv;
+  int lid = xcd_remap(blockIdx.x, B * Hq * nqb);
+  const int g = lid % G;
+  lid /= G;
+  int qb = lid % nqb;
+  lid /= nqb;
+  const int hkv = lid % Hkv, b = lid / Hkv, h = hkv * G + g;
+  if (CAUSAL) qb = nqb - 1 - qb;
+
   const int tid = threadIdx.x, l = tid & 63, lr = l & 31, hh = l >> 5;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int q = qb * BQ + w * 32 + lr;
-  const int qmin_w = qb * BQ + w * 32, qmax_w = qmin_w + 31;
+  const int q = qb * BQ8 + w * 32 + lr, qc = min(q, S - 1);
+  const int qmin_w = qb * BQ8 + w * 32, qmax_w = qmin_w + 31;
+  const bool live = qmin_w < S;
 
   bf16x8 qf[8], df[8];
   {
-    const bf16_t* qp = qkv + ((long)b * S + q) * ld + (long)h * D + 8 * hh;
-    const bf16_t* dp_ = dout + ((long)b * S + q) * lddo + (long)h * D + 8 * hh;
+    const bf16_t* qp = qkv + ((long)b * S + qc) * ld + (long)h * D + 8 * hh;
+    const bf16_t* dp_ = dout + ((long)b * S + qc) * lddo + (long)h * D + 8 * hh;
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) {
       qf[ks] = as_bf16x8(ld16(qp + 16 * ks));
       df[ks] = as_bf16x8(ld16(dp_ + 16 * ks));
     }
   }
-  const float lse2 = lse[((long)b * Hq + h) * S + q] * LOG2E;
-  const float dl = delta[((long)b * Hq + h) * S + q];
+  float lse_s = lse[((long)b * Hq + h) * S + qc] / scale;   // lse in raw score units
+  float dl = delta[((long)b * Hq + h) * S + qc];
   const bf16_t* kp = qkv + (long)b * S * ld + (long)(Hq + hkv) * D;
   const bf16_t* vp = qkv + (long)b * S * ld + (long)(Hq + Hkv + hkv) * D;
-  auto stage = [&](int j, int buf) {
-    stage_rows(kp + (long)j * BK * ld, ld, smem + buf * TILE, BK, w, 4, l);
-    stage_rows(vp + (long)j * BK * ld, ld, smem + (2 + buf) * TILE, BK, w, 4, l);
+  auto stage = [&](int j) {
+    char* st = smem + (j % NST) * STG;
+    stage_rows(kp + (long)j * BK * ld, ld, st, BK, w, 8, l);
+    stage_rows(vp + (long)j * BK * ld, ld, st + TILE, BK, w, 8, l);
   };
+  const int ntiles = CAUSAL ? min(S, qb * BQ8 + BQ8) / BK : S / BK;
+  for (int j = 0; j < NST - 1 && j < ntiles; ++j) stage(j);
+  // retire the register loads before the loop (see the forward)
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) asm volatile("" : "+v"(qf[ks]), "+v"(df[ks]));
+  asm volatile("" : "+v"(lse_s), "+v"(dl));
+  const bf16x8 ones = fold_ones(hh), lse_b = fold_const(lse_s, hh), dl_b = fold_const(dl, hh);
   f32x16 dq[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) dq[t] = f32x16{};
-  const int ntiles = CAUSAL ? (qb * BQ + BQ) / BK : S / BK;
   const int vrow = 4 * hh + ((l & 15) >> 2);
   const int vcol = 16 * ((l >> 4) & 1) + 4 * (l & 3);
 
-  stage(0, 0);
-  wait_dma_barrier();
+  wait_stage(0, min(NST - 2, ntiles - 1));
+  barrier();
   for (int j = 0; j < ntiles; ++j) {
-    const int cur = j & 1;
-    if (j + 1 < ntiles) stage(j + 1, cur ^ 1);
+    if (j + NST - 1 < ntiles) stage(j + NST - 1);
     const int k0 = j * BK;
-    if (!CAUSAL || k0 <= qmax_w) {
-      const char* Ks = smem + cur * TILE;
-      const char* Vs = smem + (2 + cur) * TILE;
+    if (live && (!CAUSAL || k0 <= qmax_w)) {
+      const char* Ks = smem + (j % NST) * STG;
+      const char* Vs = Ks + TILE;
       const bool need_mask = CAUSAL && (k0 + BK - 1 > qmin_w);
       bf16x8 sf[2][2];
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
-        f32x16 s = f32x16{}, dp = f32x16{};
+        f32x16 s = mfma32(ones, lse_b, f32x16{}), dp = mfma32(ones, dl_b, f32x16{});
 #pragma unroll
         for (int ks = 0; ks < 8; ++ks) {
           s = mfma32(row_read(Ks, swz(32 * kt + lr, 2 * ks + hh)), qf[ks], s);
           dp = mfma32(row_read(Vs, swz(32 * kt + lr, 2 * ks + hh)), df[ks], dp);
         }
+        if (need_mask) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          float p = __builtin_amdgcn_exp2f(s[r] * scale_log2 - lse2);
-          if (need_mask) {
+          for (int r = 0; r < 16; ++r) {
             const int key = k0 + 32 * kt + (r & 3) + 8 * (r >> 2) + 4 * hh;
-            if (key > q) p = 0.f;
+            s[r] = key > q ? -INFINITY : s[r];
           }
-          s[r] = p * (dp[r] - dl);   // dS^T (unscaled)
         }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[r] = __builtin_amdgcn_exp2f(s[r] * scale_log2) * dp[r];   // dS^T (unscaled)
 #pragma unroll
         for (int ss = 0; ss < 2; ++ss) {
           u32x4 u;
@@ -360,18 +486,38 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dq_kernel(
           sf[kt][ss] = as_bf16x8(u);
         }
       }
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
+      const u32 kbase = lds_addr(Ks);
+      bf16x8 kf[2][4];
+      auto k_read = [&](int t, bf16x8* f) {
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
           for (int ss = 0; ss < 2; ++ss) {
             const int row = 32 * kt + 16 * ss + vrow, col = 32 * t + vcol;
-            dq[t] = mfma32(tr_pair(Ks, swz8(row, col), swz8(row + 8, col)), sf[kt][ss], dq[t]);
+            f[2 * kt + ss] = tr_pair_asm(kbase + swz8(row, col), kbase + swz8(row + 8, col));
           }
+      };
+      k_read(0, kf[0]);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        if (t < 3) {
+          k_read(t + 1, kf[(t + 1) & 1]);
+          lgkm_wait_tie<8>(kf[t & 1]);
+        } else {
+          lgkm_wait_tie<0>(kf[t & 1]);
+        }
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int ss = 0; ss < 2; ++ss) dq[t] = mfma32(kf[t & 1][2 * kt + ss], sf[kt][ss], dq[t]);
+      }
     }
-    wait_dma_barrier();
+    if (j + 1 < ntiles) {
+      wait_stage(j + 1, min(j + NST - 1, ntiles - 1));
+      barrier();
+    }
   }
+  if (!live) return;
   bf16_t* op = dqkv + ((long)b * S + q) * lddq + (long)h * D;
 #pragma unroll
   for (int t = 0; t < 4; ++t)
@@ -429,8 +575,7 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
   const int tid = threadIdx.x, l = tid & 63, lr = l & 31, hh = l >> 5;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int kw0 = kv0 + 32 * w;
-  const float c = scale * LOG2E;
-  const float inv_scale = 1.f / scale;
+  const float c = scale * LOG2E, inv_scale = 1.f / scale;
   const long rowB = (long)b * S;
   const bf16_t* kp = qkv + rowB * ld + (long)(Hq + hkv) * D;
   const bf16_t* vp = qkv + rowB * ld + (long)(Hq + Hkv + hkv) * D;
@@ -460,6 +605,7 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
 
   if (niter > 0) stage(0, 0);
   wait_dma_barrier();
+  const bf16x8 ones = fold_ones(hh);
   for (int it = 0; it < niter; ++it) {
     const int cur = it & 1;
     const int qt = it % ntq;
@@ -469,25 +615,25 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
     const char* dOs = smem + OFF_DO + cur * 8192;
     const float* Ls = reinterpret_cast<const float*>(smem + OFF_LD + cur * 256);
     if (!CAUSAL || kw0 <= q0 + QT - 1) {
-      // row constants, q(r) = (r&3) + 8(r>>2) + 4hh
-      f32x16 s, dp;
+      // row constants -lse/scale and -delta of query row lr folded into the chains
+      f32x16 s = mfma32(fold_const(Ls[lr] * inv_scale, hh), ones, f32x16{});
+      f32x16 dp = mfma32(fold_const(Ls[32 + lr], hh), ones, f32x16{});
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const f4 L4 = *reinterpret_cast<const f4*>(Ls + 8 * g + 4 * hh);
-        const f4 D4 = *reinterpret_cast<const f4*>(Ls + 32 + 8 * g + 4 * hh);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) { s[4 * g + i] = -L4[i] * inv_scale; dp[4 * g + i] = -D4[i]; }
-      }
-#pragma unroll
-      for (int ks = 0; ks < 8; ++ks)
+      for (int ks = 0; ks < 8; ++ks) {
         s = mfma32(row_read(Qs, swz(lr, 2 * ks + hh)), row_read(smem + OFF_K, swz(32 * w + lr, 2 * ks + hh)), s);
+        dp = mfma32(row_read(dOs, swz(lr, 2 * ks + hh)), vf[ks], dp);
+      }
       const int key = kw0 + lr;
       const bool need_mask = CAUSAL && (kw0 + 31 > q0);
+      if (need_mask) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float p = __builtin_amdgcn_exp2f(s[r] * c);
-        if (need_mask && key > q0 + (r & 3) + 8 * (r >> 2) + 4 * hh) p = 0.f;
-        s[r] = p;
+        for (int r = 0; r < 16; ++r) {
+          const float p = __builtin_amdgcn_exp2f(s[r] * c);
+          s[r] = key > q0 + (r & 3) + 8 * (r >> 2) + 4 * hh ? 0.f : p;
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[r] = __builtin_amdgcn_exp2f(s[r] * c);
       }
       bf16x8 pf[2];
 #pragma unroll
@@ -504,8 +650,6 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
           const int row = 16 * ss + vrow, col = 32 * t + vcol;
           dV[t] = mfma32(tr_pair(dOs, swz8(row, col), swz8(row + 8, col)), pf[ss], dV[t]);
         }
-#pragma unroll
-      for (int ks = 0; ks < 8; ++ks) dp = mfma32(row_read(dOs, swz(lr, 2 * ks + hh)), vf[ks], dp);
       bf16x8 sf[2];
 #pragma unroll
       for (int ss = 0; ss < 2; ++ss) {
@@ -569,13 +713,13 @@ extern "C" {
 int kf_flash_fwd(const void* qkv, long ld, void* out, long ldo, float* lse, int B, int S, int Hq,
                  int Hkv, int D_, float scale, int causal, hipStream_t st) {
   if (D_ != D || S % BQ != 0 || Hq % Hkv != 0 || ld % 8 || ldo % 8) return 1;
-  const int grid = B * Hq * (S / BQ);
+  const int grid = B * Hq * ((S + BQ8 - 1) / BQ8);
   const float sl2 = scale * LOG2E;
   if (causal)
-    flash_fwd_kernel<true><<<grid, 256, 0, st>>>((const bf16_t*)qkv, ld, (bf16_t*)out, ldo, lse, B, S,
+    flash_fwd_kernel<true><<<grid, 512, 0, st>>>((const bf16_t*)qkv, ld, (bf16_t*)out, ldo, lse, B, S,
                                                  Hq, Hkv, sl2);
   else
-    flash_fwd_kernel<false><<<grid, 256, 0, st>>>((const bf16_t*)qkv, ld, (bf16_t*)out, ldo, lse, B,
+    flash_fwd_kernel<false><<<grid, 512, 0, st>>>((const bf16_t*)qkv, ld, (bf16_t*)out, ldo, lse, B,
                                                   S, Hq, Hkv, sl2);
   return 0;
 }
@@ -592,17 +736,17 @@ int kf_flash_bwd(const void* qkv, long ld, const void* o, long ldo, const void* 
                                                            lddo, delta, B, S, Hq);
   int items = 0;
   for (int kb = 0; kb < S / BKV; ++kb) items += (S - (causal ? kb * BKV : 0) + QCH - 1) / QCH;
-  const int g_kv = B * Hkv * items, g_q = B * Hq * (S / BQ);
+  const int g_kv = B * Hkv * items, g_q = B * Hq * ((S + BQ8 - 1) / BQ8);
   const float sl2 = scale * LOG2E;
   if (causal) {
     flash_bwd_dkdv_kernel<true><<<g_kv, 256, 0, st>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo,
                                                       lse, delta, dk_acc, dv_acc, B, S, Hq, Hkv, scale, items);
-    flash_bwd_dq_kernel<true><<<g_q, 256, 0, st>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo, lse,
+    flash_bwd_dq_kernel<true><<<g_q, 512, 0, st>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo, lse,
                                                    delta, (bf16_t*)dqkv, lddqkv, B, S, Hq, Hkv, sl2, scale);
   } else {
     flash_bwd_dkdv_kernel<false><<<g_kv, 256, 0, st>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo,
                                                        lse, delta, dk_acc, dv_acc, B, S, Hq, Hkv, scale, items);
-    flash_bwd_dq_kernel<false><<<g_q, 256, 0, st>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo, lse,
+    flash_bwd_dq_kernel<false><<<g_q, 512, 0, st>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo, lse,
                                                     delta, (bf16_t*)dqkv, lddqkv, B, S, Hq, Hkv, sl2, scale);
   }
   const long chunks = (long)T * Hkv * 32;

@@ -1,0 +1,66 @@
+// Standalone microbench for the dW GEMM (ops/csrc/gemm.hip) at the Llama-3-8B training shapes
+// (K = 16384 tokens): C[M,N] = A^T B with A [K, M], B [K, N].  Prints per-shape time, TFLOP/s
+// and a checksum so build variants (-D flags) can be compared.  Run: gemm_bench [iters].
+#include "../../service_account_auth_improvements_amd/ops/csrc/gemm.hip"
+
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#define CK(x)                                                                                   \
+  do {                                                                                          \
+    hipError_t e_ = (x);                                                                        \
+    if (e_ != hipSuccess) {                                                                     \
+      fprintf(stderr, "%s:%d %s -> %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_));       \
+      exit(1);                                                                                  \
+    }                                                                                           \
+  } while (0)
+
+__global__ void init_bf16(bf16_t* p, long n, u32 seed, float amp) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    u32 x = (u32)i * 2654435761u ^ seed;
+    x ^= x >> 15; x *= 2246822519u; x ^= x >> 13; x *= 3266489917u; x ^= x >> 16;
+    p[i] = f2bf(((float)(x & 0xffffff) / 8388608.f - 1.f) * amp);
+  }
+}
+
+int main(int argc, char** argv) {
+  const int iters = argc > 1 ? atoi(argv[1]) : 20;
+  const int K = 16384;
+  struct Shape { const char* name; int M, N; };
+  const Shape shapes[] = {{"wqkv", 6144, 4096}, {"wo", 4096, 4096}, {"wgu", 28672, 4096},
+                          {"wd", 4096, 14336}, {"lm_head", 128256, 4096}};
+  bf16_t *A, *B, *C;
+  CK(hipMalloc(&A, (size_t)K * 128256 * 2));
+  CK(hipMalloc(&B, (size_t)K * 14336 * 2));
+  CK(hipMalloc(&C, (size_t)128256 * 4096 * 2));
+  init_bf16<<<4096, 256>>>(A, (long)K * 128256, 0x1111u, 1.f);
+  init_bf16<<<4096, 256>>>(B, (long)K * 14336, 0x2222u, 1.f);
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  double tot_ms = 0, tot_fl = 0;
+  for (const Shape& s : shapes) {
+    auto run = [&] { if (kf_gemm_tn(A, s.M, B, s.N, C, s.N, s.M, s.N, K, 0, 0)) { fprintf(stderr, "bad shape\n"); exit(1); } };
+    for (int i = 0; i < 3; ++i) run();
+    CK(hipDeviceSynchronize());
+    CK(hipEventRecord(e0));
+    for (int i = 0; i < iters; ++i) run();
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    ms /= iters;
+    const double fl = 2.0 * s.M * s.N * K;
+    const double mult = strcmp(s.name, "lm_head") ? 32 : 1;
+    tot_ms += mult * ms;
+    tot_fl += mult * fl;
+    std::vector<uint16_t> h(4096);
+    CK(hipMemcpy(h.data(), C, h.size() * 2, hipMemcpyDeviceToHost));
+    double cs = 0;
+    for (size_t i = 0; i < h.size(); ++i) cs += __builtin_bit_cast(float, (u32)h[i] << 16) * (double)(i % 5 + 1);
+    printf("%-8s M=%6d N=%6d  %8.3f ms  %6.0f TF  chk %.6e\n", s.name, s.M, s.N, ms, fl / (ms * 1e-3) / 1e12, cs);
+  }
+  printf("dW per step: %.1f ms  %.0f TF\n", tot_ms, tot_fl / (tot_ms * 1e-3) / 1e12);
+  return 0;
+}
