@@ -25,23 +25,14 @@
 //    output columns -> 8-byte stores (and loads when accumulating).
 //  * XCD-aware bijective block remap + grouped (8 M-tiles) raster: the workgroups of one
 //    XCD share A and B panels in its L2.
+//  * s_setprio(1/0) around each MFMA group measured null (tools/kbench/gemm_bench: 1276 vs
+//    1279 TF over the step's dW shapes), so the schedule is left to the counted waits.
 #include "common.h"
 
 using namespace kf;
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 #define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
-
-#ifndef GM_PRIO
-#define GM_PRIO 0
-#endif
-#if GM_PRIO
-#define GM_PRIO_ON() __builtin_amdgcn_s_setprio(1)
-#define GM_PRIO_OFF() __builtin_amdgcn_s_setprio(0)
-#else
-#define GM_PRIO_ON() ((void)0)
-#define GM_PRIO_OFF() ((void)0)
-#endif
 
 namespace gm {
 constexpr int BM = 256, BN = 256, BK = 32, NBUF = 4;
@@ -201,10 +192,8 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_kernel(const bf16_t* __restric
       constexpr int t = decltype(tc)::value;
       if constexpr (t == 0) lgkm_wait<Cnt<0>::v>(a[0], b);
       else lgkm_wait<Cnt<t>::v>(a[t]);
-      GM_PRIO_ON();
 #pragma unroll
       for (int u = 0; u < 4; ++u) acc[u][t] = mfma16(b[u], a[t], acc[u][t]);
-      GM_PRIO_OFF();
       if constexpr (t == 3) {
         // publish stage s+1 (its DMA was issued two stages ago), then refill the buffer
         // every wave has finished with (stage s-1's) with stage s+3
