@@ -94,6 +94,21 @@ def skinny_gemm(x, w, swiglu: bool = False):
     return y.to(x.dtype)
 
 
+def skinny_gemm_norm_ok(x, K: int) -> bool:
+    """True when the fused residual+RMSNorm decode GEMM handles these rows."""
+    return x.is_cuda and x.shape[0] <= 4 and x.shape[0] * K <= 32768 and K % 256 == 0
+
+
+def skinny_gemm_norm(x, residual, norm_w, eps, w, swiglu: bool = False):
+    """h = x (+ residual); y = (rmsnorm(h) * norm_w) . w^T (SwiGLU epilogue when ``swiglu``).
+    One kernel on the GPU: the norm is the decode GEMM's prologue.  Returns (y, h)."""
+    if x.is_cuda:
+        return _k().skinny_gemm_norm(x.contiguous(), None if residual is None else residual.contiguous(),
+                                     norm_w, float(eps), w, swiglu)
+    a, h, _ = rmsnorm_fwd(x, norm_w, eps, residual=residual)
+    return skinny_gemm(a, w, swiglu), h
+
+
 # ---------------------------------------------------------------- weight-gradient GEMM
 def gemm_tn_ok(a, b, c) -> bool:
     """True when the HIP weight-gradient GEMM handles c = a^T b for these operands."""

@@ -44,6 +44,8 @@ int kf_kv_fill(const void*, long, int, int, int, int, int, void*, void*, int, hi
 int kf_embed_fwd(const long*, const void*, void*, int, int, long, long, hipStream_t);
 int kf_embed_bwd(const long*, const long*, const void*, void*, int, int, long, long, int, hipStream_t);
 int kf_skinny_gemm(const void*, long, int, const void*, int, int, void*, long, int, int, hipStream_t);
+int kf_skinny_gemm_norm(const void*, long, int, const void*, const void*, float, void*, long, const void*, int, int,
+                        void*, long, int, int, hipStream_t);
 int kf_gemm_tn(const void*, long, const void*, long, void*, long, int, int, int, int, hipStream_t);
 }
 
@@ -368,6 +370,38 @@ at::Tensor skinny_gemm(const at::Tensor& x, const at::Tensor& w, bool swiglu) {
   return y;
 }
 
+// Decode GEMM with the residual-add + RMSNorm fused in as a prologue:
+//   h = x (+ res);  y = (rmsnorm(h) * nw) . w^T  [SwiGLU epilogue when swiglu].
+// Returns (y, h); h aliases x when res is None.  Needs M <= 8 and M * K <= 32768.
+std::tuple<at::Tensor, at::Tensor> skinny_gemm_norm(const at::Tensor& x, const std::optional<at::Tensor>& res,
+                                                    const at::Tensor& nw, double eps, const at::Tensor& w,
+                                                    bool swiglu) {
+  check_bf16_cuda(x, "x");
+  check_bf16_cuda(w, "w");
+  check_bf16_cuda(nw, "norm weight");
+  TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && w.dim() == 2 && w.is_contiguous(), "skinny_gemm_norm: 2-D operands");
+  const int64_t M = x.size(0), K = x.size(1), Nw = w.size(0);
+  TORCH_CHECK(w.size(1) == K && nw.numel() == K && nw.is_contiguous(), "skinny_gemm_norm: K mismatch");
+  TORCH_CHECK(M >= 1 && M <= 8 && M * K <= 32768 && K % 256 == 0, "skinny_gemm_norm: needs M <= 8, M*K <= 32768, K % 256 == 0");
+  const int64_t N = swiglu ? Nw / 2 : Nw;
+  TORCH_CHECK(N % 16 == 0 && (!swiglu || Nw % 2 == 0), "skinny_gemm_norm: N % 16 != 0");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  at::Tensor h = x;
+  const void* rp = nullptr;
+  if (res.has_value()) {
+    check_bf16_cuda(*res, "res");
+    TORCH_CHECK(res->sizes() == x.sizes() && res->is_contiguous(), "skinny_gemm_norm: res shape");
+    h = at::empty_like(x);
+    rp = res->data_ptr();
+  }
+  auto y = at::empty({M, N}, x.options());
+  check_rc(kf_skinny_gemm_norm(x.data_ptr(), x.stride(0), (int)M, rp, nw.data_ptr(), (float)eps,
+                               rp ? h.data_ptr() : nullptr, h.stride(0), w.data_ptr(), (int)N, (int)K, y.data_ptr(),
+                               y.stride(0), swiglu ? 1 : 0, (int)N, cur_stream()),
+           "skinny_gemm_norm");
+  return {y, h};
+}
+
 // Weight-gradient GEMM: C[M, N] (+)= a^T . b with a = [K, M], b = [K, N] (row stride may
 // exceed the width: views into fused activations); C may be a view into the flat grad buffer.
 bool gemm_tn_ok(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c) {
@@ -436,6 +470,7 @@ TORCH_LIBRARY(kfamd, m) {
   m.def("flash_bwd", &flash_bwd);
   m.def("decode_attn", &decode_attn);
   m.def("skinny_gemm", &skinny_gemm);
+  m.def("skinny_gemm_norm", &skinny_gemm_norm);
   m.def("gemm_tn_ok", &gemm_tn_ok);
   m.def("gemm_tn_(Tensor a, Tensor b, Tensor(a!) c, bool accumulate) -> ()", &gemm_tn_);
   m.def("embed_fwd", &embed_fwd);

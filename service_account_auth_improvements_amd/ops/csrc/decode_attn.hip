@@ -164,13 +164,16 @@ __global__ __launch_bounds__(D) void decode_combine_kernel(const float* __restri
   const int bh = blockIdx.x, d = threadIdx.x;
   const int b = bh / hq, h = bh % hq;
   const float* ml = part_ml + (long)bh * splits * 2;
+  // branch-free and unrolled: the split partials are independent L2 loads, so they are
+  // issued back to back instead of one dependent round trip per split (latency-bound at B=1)
   float M = -INFINITY;
+#pragma unroll 8
   for (int s = 0; s < splits; ++s) M = fmaxf(M, ml[2 * s]);
   float num = 0.f, den = 0.f;
+#pragma unroll 8
   for (int s = 0; s < splits; ++s) {
     const float m = ml[2 * s];
-    if (m == -INFINITY) continue;
-    const float w = exp2f(m - M);
+    const float w = m == -INFINITY ? 0.f : exp2f(m - M);
     num = fmaf(w, part_o[((long)bh * splits + s) * D + d], num);
     den = fmaf(w, ml[2 * s + 1], den);
   }

@@ -12,6 +12,11 @@
 //  * epilogues: plain bf16 store, or SwiGLU -- the workgroup also computes the matching
 //    "up" rows (W row n + F) and writes silu(gate) * up, so the decode MLP's gate/up GEMM
 //    and the activation are one kernel.
+//  * optional fused residual-add + RMSNorm PROLOGUE (the decode layer's two norms): every
+//    workgroup forms h = bf16(x + res) for its <= 8 rows, reduces sum(h^2) over K, and stages
+//    y = bf16(h * rstd * w_norm) in LDS as the X operand; workgroup 0 also stores h (the new
+//    residual stream).  The first W loads are issued before the prologue, so its latency
+//    hides under the weight stream, and two launches (+ their graph gaps) per layer vanish.
 // MFMA 16x16x32 bf16 layout (guide §3): lane l holds A[row l&15][k 8(l>>4)+j] and
 // B[k 8(l>>4)+j][col l&15]; D: col = l&15, row = 4(l>>4) + reg.
 #include "common.h"
@@ -31,11 +36,25 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
-template <int NT, bool SWIGLU, int UNROLL>
+// residual-add + RMSNorm prologue operands (NORM kernels only)
+struct NormArgs {
+  const bf16_t* res;   // added to x (nullable)
+  const bf16_t* w;     // norm weight [K]
+  bf16_t* h_out;       // h = bf16(x + res), written by workgroup 0 (nullable when res is null)
+  long ldh;
+  float eps;
+};
+constexpr int NORM_MAX_ROWS = 8;
+constexpr int NORM_LDS = 64 * 1024;   // staged normalised X: rows * K * 2 bytes
+
+template <int NT, bool SWIGLU, int UNROLL, bool NORM>
 __global__ __launch_bounds__(64 * WAVES) void skinny_gemm_kernel(const bf16_t* __restrict__ x, long ldx, int M,
                                                                  const bf16_t* __restrict__ w, int K,
-                                                                 bf16_t* __restrict__ y, long ldy, int up_off) {
+                                                                 bf16_t* __restrict__ y, long ldy, int up_off,
+                                                                 NormArgs na) {
   __shared__ float red[WAVES][SWIGLU ? 2 : 1][NT][16 * 16];
+  extern __shared__ __attribute__((aligned(16))) bf16_t xs[];   // NORM: staged X, M * K (dynamic)
+  __shared__ float ssq[NORM ? WAVES * NORM_MAX_ROWS : 1];
   const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63;
   const int r = l & 15, q = l >> 4;
   const int n0 = blockIdx.x * 16;
@@ -49,20 +68,82 @@ __global__ __launch_bounds__(64 * WAVES) void skinny_gemm_kernel(const bf16_t* _
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[e][t] = f32x4{};
 
-  for (int k = 0; k < kw; k += 32 * UNROLL) {
-    u32x4 a[UNROLL], au[UNROLL];
+  u32x4 a[UNROLL], au[UNROLL];
+  auto load_w = [&](int k) {
 #pragma unroll
     for (int i = 0; i < UNROLL; ++i) {
       a[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wp + k + 32 * i));
       if (SWIGLU) au[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wu + k + 32 * i));
     }
+  };
+  load_w(0);   // the weight stream starts before the (NORM) prologue
+  if constexpr (NORM) {
+    // h = bf16(x + res) -> sum of squares per row -> y = bf16(h * rstd * w) into LDS
+    const int nch = K / 8;                   // 16-byte chunks per row
+    float ss[NORM_MAX_ROWS];
+#pragma unroll
+    for (int m = 0; m < NORM_MAX_ROWS; ++m) ss[m] = 0.f;
+    for (int c = tid; c < nch; c += 64 * WAVES) {
+#pragma unroll
+      for (int m = 0; m < NORM_MAX_ROWS; ++m) {
+        if (m >= M) break;
+        float hv[8];
+        unpack8(ld16(x + (long)m * ldx + 8 * c), hv);
+        if (na.res) {
+          float t[8];
+          unpack8(ld16(na.res + (long)m * ldx + 8 * c), t);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) hv[j] += t[j];
+          const u32x4 hb = pack8(hv);        // the residual stream is stored (and normed) as bf16
+          if (blockIdx.x == 0) st16(na.h_out + (long)m * na.ldh + 8 * c, hb);
+          unpack8(hb, hv);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ss[m] += hv[j] * hv[j];
+        st16(xs + (long)m * K + 8 * c, pack8(hv));   // un-normalised h for now
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < NORM_MAX_ROWS; ++m) {
+      if (m >= M) break;
+      const float v = wave_sum(ss[m]);
+      if (l == 0) ssq[wave * NORM_MAX_ROWS + m] = v;
+    }
+    __syncthreads();
+    for (int c = tid; c < nch; c += 64 * WAVES) {
+      float wf[8];
+      unpack8(ld16(na.w + 8 * c), wf);
+#pragma unroll
+      for (int m = 0; m < NORM_MAX_ROWS; ++m) {
+        if (m >= M) break;
+        float tot = 0.f;
+#pragma unroll
+        for (int v = 0; v < WAVES; ++v) tot += ssq[v * NORM_MAX_ROWS + m];
+        const float rs = rsqrtf(tot / (float)K + na.eps);
+        float hv[8];
+        unpack8(*reinterpret_cast<const u32x4*>(xs + (long)m * K + 8 * c), hv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) hv[j] = hv[j] * rs * wf[j];
+        *reinterpret_cast<u32x4*>(xs + (long)m * K + 8 * c) = pack8(hv);
+      }
+    }
+    __syncthreads();
+  }
+
+  for (int k = 0; k < kw; k += 32 * UNROLL) {
+    if (k > 0) load_w(k);
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int row = 16 * t + r;
       u32x4 bx[UNROLL];
 #pragma unroll
-      for (int i = 0; i < UNROLL; ++i)
-        bx[i] = row < M ? ld16(x + (long)row * ldx + kbeg + k + 32 * i + 8 * q) : u32x4{0, 0, 0, 0};
+      for (int i = 0; i < UNROLL; ++i) {
+        if constexpr (NORM)
+          bx[i] = row < M ? *reinterpret_cast<const u32x4*>(xs + (long)row * K + kbeg + k + 32 * i + 8 * q)
+                          : u32x4{0, 0, 0, 0};
+        else
+          bx[i] = row < M ? ld16(x + (long)row * ldx + kbeg + k + 32 * i + 8 * q) : u32x4{0, 0, 0, 0};
+      }
 #pragma unroll
       for (int i = 0; i < UNROLL; ++i) {
         acc[0][t] = mfma16(as_bf(a[i]), as_bf(bx[i]), acc[0][t]);
@@ -95,23 +176,36 @@ __global__ __launch_bounds__(64 * WAVES) void skinny_gemm_kernel(const bf16_t* _
   }
 }
 
-template <int NT, bool SWIGLU>
+template <int NT, bool SWIGLU, bool NORM = false>
 int launch(const bf16_t* x, long ldx, int M, const bf16_t* w, int N, int K, bf16_t* y, long ldy, int up_off,
-           hipStream_t st) {
+           hipStream_t st, NormArgs na = NormArgs{}) {
   dim3 grid(N / 16), block(64 * WAVES);
+  const size_t dyn = NORM ? (size_t)M * K * 2 : 0;   // LDS sized to the rows: B = 1 keeps occupancy
   if (K % (WAVES * 32 * 8) == 0)
-    hipLaunchKernelGGL((skinny_gemm_kernel<NT, SWIGLU, 8>), grid, block, 0, st, x, ldx, M, w, K, y, ldy, up_off);
+    hipLaunchKernelGGL((skinny_gemm_kernel<NT, SWIGLU, 8, NORM>), grid, block, dyn, st, x, ldx, M, w, K, y, ldy, up_off, na);
   else if (K % (WAVES * 32 * 4) == 0)
-    hipLaunchKernelGGL((skinny_gemm_kernel<NT, SWIGLU, 4>), grid, block, 0, st, x, ldx, M, w, K, y, ldy, up_off);
+    hipLaunchKernelGGL((skinny_gemm_kernel<NT, SWIGLU, 4, NORM>), grid, block, dyn, st, x, ldx, M, w, K, y, ldy, up_off, na);
   else if (K % (WAVES * 32 * 2) == 0)
-    hipLaunchKernelGGL((skinny_gemm_kernel<NT, SWIGLU, 2>), grid, block, 0, st, x, ldx, M, w, K, y, ldy, up_off);
+    hipLaunchKernelGGL((skinny_gemm_kernel<NT, SWIGLU, 2, NORM>), grid, block, dyn, st, x, ldx, M, w, K, y, ldy, up_off, na);
   else
-    hipLaunchKernelGGL((skinny_gemm_kernel<NT, SWIGLU, 1>), grid, block, 0, st, x, ldx, M, w, K, y, ldy, up_off);
+    hipLaunchKernelGGL((skinny_gemm_kernel<NT, SWIGLU, 1, NORM>), grid, block, dyn, st, x, ldx, M, w, K, y, ldy, up_off, na);
   KF_CHECK_LAUNCH();
   return 0;
 }
 
 }  // namespace
+
+// y = (rmsnorm(x + res) * w_norm) . W^T  [SwiGLU epilogue when swiglu]; h_out = x + res.
+// Needs M <= NORM_MAX_ROWS and M * K * 2 <= NORM_LDS (the staged X); returns 1 otherwise.
+extern "C" int kf_skinny_gemm_norm(const void* x, long ldx, int M, const void* res, const void* nw, float eps,
+                                   void* h_out, long ldh, const void* w, int N, int K, void* y, long ldy,
+                                   int swiglu, int up_off, hipStream_t st) {
+  if (M <= 0 || M > NORM_MAX_ROWS || (long)M * K * 2 > NORM_LDS || N % 16 != 0 || K % (WAVES * 32) != 0) return 1;
+  if (res && !h_out) return 1;
+  const NormArgs na{(const bf16_t*)res, (const bf16_t*)nw, (bf16_t*)h_out, ldh, eps};
+  if (swiglu) return launch<1, true, true>((const bf16_t*)x, ldx, M, (const bf16_t*)w, N, K, (bf16_t*)y, ldy, up_off, st, na);
+  return launch<1, false, true>((const bf16_t*)x, ldx, M, (const bf16_t*)w, N, K, (bf16_t*)y, ldy, 0, st, na);
+}
 
 // swiglu: W holds [gate (up_off rows); up (up_off rows)], N = up_off, Y = silu(X.Wg^T) * (X.Wu^T)
 extern "C" int kf_skinny_gemm(const void* x, long ldx, int M, const void* w, int N, int K, void* y, long ldy,

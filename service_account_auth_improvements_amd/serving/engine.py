@@ -11,7 +11,9 @@ MI355X-first design:
   RoPE, MFMA flash attention, SwiGLU) and streams K/V into the slot with ``kv_fill_``.
 * Decode appends K/V (``kv_append_``) and runs the split-K GQA decode kernel (K8); for
   batches <= 16 the projections use the weight-streaming skinny GEMM (ops/csrc/skinny_gemm.hip,
-  gate/up GEMM fused with SwiGLU), larger batches hipBLASLt.  Every
+  gate/up GEMM fused with SwiGLU), larger batches hipBLASLt.  For batches <= 8 the two
+  residual-add + RMSNorms of a layer are the QKV and gate/up GEMMs' prologues (no norm
+  launches on the decode path).  Every
   decode step for a batch-size bucket is captured once in a HIP graph (static input
   buffers, padded rows point at a scratch slot), so a token costs one graph launch instead
   of ~350 kernel launches.
@@ -111,8 +113,12 @@ class Engine:
 
     def _decode_mlp(self, i, h1, da):
         m, cfg = self.m, self.cfg
-        mm, h2, _ = ops.rmsnorm_fwd(h1, m.P(f"l{i}.norm2"), cfg.norm_eps, residual=da)
         wgu = m.P(f"l{i}.wgu")
+        if ops.skinny_gemm_norm_ok(h1, wgu.shape[1]):
+            # residual add + RMSNorm + gate/up GEMM + SwiGLU: one kernel
+            s, h2 = ops.skinny_gemm_norm(h1, da, m.P(f"l{i}.norm2"), cfg.norm_eps, wgu, swiglu=True)
+            return h2, tp_all_reduce(self._mm(s, m.P(f"l{i}.wd")), m.st)
+        mm, h2, _ = ops.rmsnorm_fwd(h1, m.P(f"l{i}.norm2"), cfg.norm_eps, residual=da)
         if mm.is_cuda and mm.shape[0] <= SKINNY_MAX_ROWS and wgu.shape[1] % 256 == 0:
             s = ops.skinny_gemm(mm, wgu, swiglu=True)          # gate/up GEMM + SwiGLU in one kernel
         else:
@@ -124,8 +130,12 @@ class Engine:
         r = self._embed(tokens)
         d = None
         for li, i in enumerate(m.layers):
-            a, h1, _ = ops.rmsnorm_fwd(r, m.P(f"l{i}.norm1"), cfg.norm_eps, residual=d)
-            qkv = self._mm(a, m.P(f"l{i}.wqkv"))
+            wqkv = m.P(f"l{i}.wqkv")
+            if ops.skinny_gemm_norm_ok(r, wqkv.shape[1]):
+                qkv, h1 = ops.skinny_gemm_norm(r, d, m.P(f"l{i}.norm1"), cfg.norm_eps, wqkv)
+            else:
+                a, h1, _ = ops.rmsnorm_fwd(r, m.P(f"l{i}.norm1"), cfg.norm_eps, residual=d)
+                qkv = self._mm(a, wqkv)
             rope_append_(qkv, m.hq, m.cos, m.sin, slots, pos, self.kc[li], self.vc[li])
             o = decode_attention(qkv, self.kc[li], self.vc[li], slots, lengths, m.hq)
             da = tp_all_reduce(self._mm(o, m.P(f"l{i}.wo")), m.st)

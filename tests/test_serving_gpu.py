@@ -108,6 +108,24 @@ def test_skinny_gemm(M, N, K, swiglu):
     assert torch.allclose(ops.skinny_gemm(xs, w, swiglu).float(), ops.skinny_gemm(xs.contiguous(), w, swiglu).float())
 
 
+@pytest.mark.parametrize("M,N,K,swiglu,res", [(1, 6144, 4096, False, True), (1, 14336, 4096, True, True),
+                                              (4, 6144, 4096, False, False), (8, 2048, 4096, True, True)])
+def test_skinny_gemm_norm_matches_unfused(M, N, K, swiglu, res):
+    """Residual-add + RMSNorm prologue fused into the decode GEMM == rmsnorm_fwd + skinny_gemm."""
+    from service_account_auth_improvements_amd import ops
+    g = torch.Generator(device="cpu").manual_seed(M * 7 + N)
+    x = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+    r = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16) if res else None
+    nw = (1 + 0.1 * torch.randn(K, generator=g)).to(DEV, torch.bfloat16)
+    w = (torch.randn((2 * N if swiglu else N), K, generator=g) * 0.02).to(DEV, torch.bfloat16)
+    y, h = ops.skinny_gemm_norm(x, r, nw, 1e-5, w, swiglu)
+    a, h_ref, _ = ops.rmsnorm_fwd(x, nw, 1e-5, residual=r)
+    y_ref = ops.skinny_gemm(a, w, swiglu)
+    assert torch.equal(h, h_ref)                       # the residual stream is bit-identical
+    err = ((y.float() - y_ref.float()).abs().max() / y_ref.float().abs().max()).item()
+    assert y.shape == (M, N) and err < 1e-2, err
+
+
 def test_rope_append_matches_reference():
     from service_account_auth_improvements_amd.ops import reference
     from service_account_auth_improvements_amd.ops.attention import rope_append_
