@@ -47,6 +47,13 @@ int kf_skinny_gemm(const void*, long, int, const void*, int, int, void*, long, i
 int kf_skinny_gemm_norm(const void*, long, int, const void*, const void*, float, void*, long, const void*, int, int,
                         void*, long, int, int, hipStream_t);
 int kf_gemm_tn(const void*, long, const void*, long, void*, long, int, int, int, int, hipStream_t);
+long kf_car_header_bytes();
+int kf_car_alloc(long, void**, void*);
+int kf_car_open(const void*, void**);
+int kf_car_close(void*);
+int kf_car_free(void*);
+int kf_car_allreduce(void* const*, int, int, const void*, void*, long, long, int, hipStream_t);
+int kf_car_error(void*, hipStream_t);
 }
 
 namespace {
@@ -402,6 +409,39 @@ std::tuple<at::Tensor, at::Tensor> skinny_gemm_norm(const at::Tensor& x, const s
   return {y, h};
 }
 
+// ---- one-shot IPC all-reduce (ops/csrc/custom_ar.hip). Device pointers travel as int64.
+std::tuple<int64_t, at::Tensor> car_alloc(int64_t slot_bytes) {
+  void* p = nullptr;
+  auto h = at::empty({64}, at::TensorOptions().dtype(at::kByte));
+  TORCH_CHECK(kf_car_alloc(slot_bytes, &p, h.data_ptr()) == 0, "car_alloc: uncached IPC allocation failed");
+  return {reinterpret_cast<int64_t>(p), h};
+}
+
+int64_t car_open(const at::Tensor& handle) {
+  TORCH_CHECK(handle.numel() == 64 && handle.scalar_type() == at::kByte && !handle.is_cuda(), "car_open: 64-byte handle");
+  void* p = nullptr;
+  TORCH_CHECK(kf_car_open(handle.contiguous().data_ptr(), &p) == 0, "car_open: hipIpcOpenMemHandle failed");
+  return reinterpret_cast<int64_t>(p);
+}
+
+void car_close(int64_t p) { kf_car_close(reinterpret_cast<void*>(p)); }
+void car_free(int64_t p) { kf_car_free(reinterpret_cast<void*>(p)); }
+
+// in place, like dist.all_reduce (the engine's TP code relies on all-reduce being in place)
+void car_allreduce_(const std::vector<int64_t>& ptrs, int64_t rank, at::Tensor& x, int64_t slot_bytes, int64_t blocks) {
+  check_bf16_cuda(x, "x");
+  TORCH_CHECK(x.is_contiguous() && x.numel() % 8 == 0 && 2 * x.numel() <= slot_bytes,
+              "car_allreduce: contiguous bf16 with numel % 8 == 0 that fits the slot");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  std::vector<void*> pv;
+  for (auto v : ptrs) pv.push_back(reinterpret_cast<void*>(v));
+  check_rc(kf_car_allreduce(pv.data(), (int)pv.size(), (int)rank, x.data_ptr(), x.data_ptr(), x.numel(), slot_bytes,
+                            (int)blocks, cur_stream()),
+           "car_allreduce");
+}
+
+int64_t car_error(int64_t own) { return kf_car_error(reinterpret_cast<void*>(own), cur_stream()); }
+
 // Weight-gradient GEMM: C[M, N] (+)= a^T . b with a = [K, M], b = [K, N] (row stride may
 // exceed the width: views into fused activations); C may be a view into the flat grad buffer.
 bool gemm_tn_ok(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c) {
@@ -471,6 +511,12 @@ TORCH_LIBRARY(kfamd, m) {
   m.def("decode_attn", &decode_attn);
   m.def("skinny_gemm", &skinny_gemm);
   m.def("skinny_gemm_norm", &skinny_gemm_norm);
+  m.def("car_alloc", &car_alloc);
+  m.def("car_open", &car_open);
+  m.def("car_close", &car_close);
+  m.def("car_free", &car_free);
+  m.def("car_allreduce_(int[] ptrs, int rank, Tensor(a!) x, int slot_bytes, int blocks) -> ()", &car_allreduce_);
+  m.def("car_error", &car_error);
   m.def("gemm_tn_ok", &gemm_tn_ok);
   m.def("gemm_tn_(Tensor a, Tensor b, Tensor(a!) c, bool accumulate) -> ()", &gemm_tn_);
   m.def("embed_fwd", &embed_fwd);

@@ -1,0 +1,158 @@
+// One-shot all-reduce over peer-mapped HIP IPC buffers (C7 in SURVEY.md §2.8: the per-layer,
+// per-token TP all-reduce of InferenceService decode with TP > 1).
+//
+// Decode all-reduces are tiny ([B, hidden] bf16: 16 KB at B = 1 for 70B) and sit on the
+// token-latency critical path twice per layer, where a ring (RCCL) pays 2(N-1) link hops of
+// latency.  On one MI355X node every GPU pair has its own xGMI link, so each rank can read
+// every peer's copy directly and sum locally: ONE hop, one kernel, no host involvement.
+//
+// Buffer of each rank (hipExtMallocWithFlags(..., hipDeviceMallocUncached): the flags are
+// polled by other GPUs and the data is read by them across xGMI, so nothing may sit in a
+// non-coherent cache), exported with hipIpcGetMemHandle and opened by every peer:
+//   [flags: 2 slots x MAXB blocks x MAXW ranks int32][epochs: MAXB int32][err: int32]
+//   [data: 2 slots x slot_bytes]
+// Call protocol, per block b (no grid-wide sync; blocks own disjoint chunks):
+//   e = ++epoch[b] (block-private counter, so HIP-graph replays need no host epoch);
+//   slot = e & 1; copy my chunk of x into data[slot];
+//   release (system scope) -> write e into flags[slot][b][my_rank] of EVERY peer;
+//   spin until flags[slot][b][p] == e for all p in my buffer (bounded: on timeout set err
+//   and give up instead of hanging the GPU) -> acquire;
+//   out[chunk] = sum_p peer_p.data[slot][chunk], accumulated in fp32 in rank order, so every
+//   rank produces bit-identical results.  out may be x (in place, like dist.all_reduce): a
+//   block reads its chunk of x before the flag exchange and writes it after.
+// Two slots suffice: to enter call e a block needs every peer's call-(e-1) flag, i.e. every
+// peer block has finished reading call e-2's data from the slot being overwritten.
+#include <cstring>
+
+#include "common.h"
+
+using namespace kf;
+
+namespace car {
+constexpr int MAXW = 8;        // ranks (one MI355X node)
+constexpr int MAXB = 64;       // blocks (chunks) per call
+constexpr int NT = 512;
+constexpr long FLAG_BYTES = 2L * MAXB * MAXW * 4;
+constexpr long EPOCH_OFF = FLAG_BYTES;
+constexpr long ERR_OFF = EPOCH_OFF + MAXB * 4;
+constexpr long DATA_OFF = 8192;  // header padded to 8 KB
+constexpr unsigned SPIN_LIMIT = 1u << 24;   // x s_sleep(2) ~ seconds: a dead peer errors out, never hangs
+
+struct Peers {
+  char* p[MAXW];
+};
+
+__device__ __forceinline__ int* flags(char* base, int slot, int b, int r) {
+  return reinterpret_cast<int*>(base) + ((slot * MAXB + b) * MAXW + r);
+}
+
+template <int W>
+__global__ __launch_bounds__(NT) void one_shot_ar_kernel(Peers peers, int rank, const bf16_t* x, bf16_t* out,
+                                                         long n, long slot_bytes) {
+  __shared__ int e_sh;
+  const int b = blockIdx.x, tid = threadIdx.x;
+  char* mine = peers.p[rank];
+  int* epoch = reinterpret_cast<int*>(mine + EPOCH_OFF) + b;
+  if (tid == 0) e_sh = __hip_atomic_load(epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  __syncthreads();
+  const int e = e_sh, slot = e & 1;
+  // chunk of 8-element (16 B) vectors owned by this block
+  const long nv = n / 8, per = (nv + gridDim.x - 1) / gridDim.x;
+  const long v0 = b * per, v1 = min(nv, v0 + per);
+  u32x4* dst = reinterpret_cast<u32x4*>(mine + DATA_OFF + slot * slot_bytes);
+  for (long v = v0 + tid; v < v1; v += NT) dst[v] = ld16(x + 8 * v);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid < W) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // system scope: data before flag, for every GPU
+    __hip_atomic_store(flags(peers.p[tid], slot, b, rank), e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    int* f = flags(mine, slot, b, tid);
+    unsigned spins = 0;
+    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != e) {
+      if (++spins > SPIN_LIMIT) {
+        __hip_atomic_store(reinterpret_cast<int*>(mine + ERR_OFF), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  }
+  __syncthreads();
+  for (long v = v0 + tid; v < v1; v += NT) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int p = 0; p < W; ++p) {
+      const u32x4 src = reinterpret_cast<const u32x4*>(peers.p[p] + DATA_OFF + slot * slot_bytes)[v];
+      float f[8];
+      unpack8(src, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += f[j];
+    }
+    st16(out + 8 * v, pack8(acc));
+  }
+  if (tid == 0) __hip_atomic_store(epoch, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+}  // namespace car
+
+using namespace car;
+
+extern "C" {
+
+long kf_car_header_bytes() { return DATA_OFF; }
+
+// Allocate this rank's uncached, IPC-exportable buffer (zeroed); handle: 64-byte hipIpcMemHandle_t.
+int kf_car_alloc(long slot_bytes, void** ptr, void* handle) {
+  const long bytes = DATA_OFF + 2 * slot_bytes;
+  if (hipExtMallocWithFlags(ptr, bytes, hipDeviceMallocUncached) != hipSuccess) return 1;
+  if (hipMemset(*ptr, 0, bytes) != hipSuccess) return 2;
+  if (hipDeviceSynchronize() != hipSuccess) return 3;
+  hipIpcMemHandle_t h;
+  if (hipIpcGetMemHandle(&h, *ptr) != hipSuccess) return 4;
+  std::memcpy(handle, &h, sizeof(h));
+  return 0;
+}
+
+int kf_car_open(const void* handle, void** ptr) {
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, handle, sizeof(h));
+  return hipIpcOpenMemHandle(ptr, h, hipIpcMemLazyEnablePeerAccess) == hipSuccess ? 0 : 1;
+}
+
+int kf_car_close(void* ptr) { return hipIpcCloseMemHandle(ptr) == hipSuccess ? 0 : 1; }
+int kf_car_free(void* ptr) { return hipFree(ptr) == hipSuccess ? 0 : 1; }
+
+// ptrs: world device pointers (own buffer at index rank); x/out: n bf16 (n % 8 == 0,
+// 2 * n <= slot_bytes; out == x allowed).  Returns non-zero on a bad shape (nothing launched).
+int kf_car_allreduce(void* const* ptrs, int world, int rank, const void* x, void* out, long n, long slot_bytes,
+                     int blocks, hipStream_t st) {
+  if (world < 1 || world > MAXW || rank < 0 || rank >= world || n % 8 || 2 * n > slot_bytes) return 1;
+  if (((uintptr_t)x | (uintptr_t)out) & 15) return 2;
+  blocks = std::max(1, std::min(blocks, MAXB));
+  Peers P{};
+  for (int i = 0; i < world; ++i) P.p[i] = static_cast<char*>(ptrs[i]);
+  auto X = static_cast<const bf16_t*>(x);
+  auto O = static_cast<bf16_t*>(out);
+  switch (world) {
+    case 1: hipLaunchKernelGGL(one_shot_ar_kernel<1>, dim3(blocks), dim3(NT), 0, st, P, rank, X, O, n, slot_bytes); break;
+    case 2: hipLaunchKernelGGL(one_shot_ar_kernel<2>, dim3(blocks), dim3(NT), 0, st, P, rank, X, O, n, slot_bytes); break;
+    case 4: hipLaunchKernelGGL(one_shot_ar_kernel<4>, dim3(blocks), dim3(NT), 0, st, P, rank, X, O, n, slot_bytes); break;
+    case 8: hipLaunchKernelGGL(one_shot_ar_kernel<8>, dim3(blocks), dim3(NT), 0, st, P, rank, X, O, n, slot_bytes); break;
+    default: return 3;
+  }
+  KF_CHECK_LAUNCH();
+  return 0;
+}
+
+// error word (1 = a peer never arrived within the spin budget); cleared by the read
+int kf_car_error(void* own, hipStream_t st) {
+  int v = 0;
+  char* p = static_cast<char*>(own) + ERR_OFF;
+  if (hipMemcpyAsync(&v, p, 4, hipMemcpyDeviceToHost, st) != hipSuccess) return -1;
+  if (hipStreamSynchronize(st) != hipSuccess) return -1;
+  if (v) {
+    const int z = 0;
+    hipMemcpy(p, &z, 4, hipMemcpyHostToDevice);
+  }
+  return v;
+}
+}

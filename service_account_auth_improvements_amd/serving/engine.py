@@ -19,8 +19,10 @@ MI355X-first design:
   of ~350 kernel launches.
 * Continuous batching: ``Scheduler`` admits requests into free slots between decode steps
   (prefill one sequence at a time), retires finished sequences immediately.
-* TP > 1 (one process per GPU over RCCL): Megatron split via the model's ``tp_all_reduce``;
-  vocab-parallel logits are all-gathered for sampling.
+* TP > 1 (one process per GPU): Megatron split; prefill all-reduces over RCCL, the decode
+  step's [B, hidden] all-reduces one-shot over peer-mapped IPC buffers (xGMI, one hop,
+  graph-capturable: parallel/custom_ar.py); vocab-parallel logits are all-gathered for
+  sampling.
 """
 from __future__ import annotations
 
@@ -59,6 +61,12 @@ class Engine:
         self.kc = torch.zeros(shape, dtype=torch.bfloat16, device=self.dev)
         self.vc = torch.zeros(shape, dtype=torch.bfloat16, device=self.dev)
         self.use_graphs = (self.dev.type == "cuda") if use_graphs is None else use_graphs
+        # TP > 1 on GPUs: the decode step's small all-reduces go one-shot over peer-mapped
+        # IPC buffers (parallel/custom_ar.py, C7) instead of an RCCL ring
+        self.car = None
+        if model.tp > 1 and self.dev.type == "cuda":
+            from ..parallel.custom_ar import OneShotAllReduce
+            self.car = OneShotAllReduce(model.st.tp_group)
         self._graphs: Dict[int, tuple] = {}
 
     # ------------------------------------------------------------------ helpers
@@ -105,6 +113,11 @@ class Engine:
         return self._logits_full(y)[0]
 
     # ------------------------------------------------------------------ decode
+    def _tp_ar(self, x):
+        if self.car is not None and self.car.supports(x):
+            return self.car(x)
+        return tp_all_reduce(x, self.m.st)
+
     def _mm(self, x, w):
         """Decode GEMM: the skinny weight-streaming kernel for small batches on the GPU."""
         if x.is_cuda and x.shape[0] <= SKINNY_MAX_ROWS and w.shape[0] <= SKINNY_MAX_N and w.shape[1] % 256 == 0:
@@ -117,13 +130,13 @@ class Engine:
         if ops.skinny_gemm_norm_ok(h1, wgu.shape[1]):
             # residual add + RMSNorm + gate/up GEMM + SwiGLU: one kernel
             s, h2 = ops.skinny_gemm_norm(h1, da, m.P(f"l{i}.norm2"), cfg.norm_eps, wgu, swiglu=True)
-            return h2, tp_all_reduce(self._mm(s, m.P(f"l{i}.wd")), m.st)
+            return h2, self._tp_ar(self._mm(s, m.P(f"l{i}.wd")))
         mm, h2, _ = ops.rmsnorm_fwd(h1, m.P(f"l{i}.norm2"), cfg.norm_eps, residual=da)
         if mm.is_cuda and mm.shape[0] <= SKINNY_MAX_ROWS and wgu.shape[1] % 256 == 0:
             s = ops.skinny_gemm(mm, wgu, swiglu=True)          # gate/up GEMM + SwiGLU in one kernel
         else:
             s = ops.swiglu_fwd(torch.mm(mm, wgu.t()))
-        return h2, tp_all_reduce(self._mm(s, m.P(f"l{i}.wd")), m.st)
+        return h2, self._tp_ar(self._mm(s, m.P(f"l{i}.wd")))
 
     def _decode_body(self, tokens, slots, pos, lengths):
         m, cfg = self.m, self.cfg
@@ -138,7 +151,7 @@ class Engine:
                 qkv = self._mm(a, wqkv)
             rope_append_(qkv, m.hq, m.cos, m.sin, slots, pos, self.kc[li], self.vc[li])
             o = decode_attention(qkv, self.kc[li], self.vc[li], slots, lengths, m.hq)
-            da = tp_all_reduce(self._mm(o, m.P(f"l{i}.wo")), m.st)
+            da = self._tp_ar(self._mm(o, m.P(f"l{i}.wo")))
             r, d = self._decode_mlp(i, h1, da)
         y, _, _ = ops.rmsnorm_fwd(r, m.P("final_norm"), cfg.norm_eps, residual=d)
         return self._logits_full(y)
