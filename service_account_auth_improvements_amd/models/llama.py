@@ -207,6 +207,17 @@ class Llama:
         else:
             torch.mm(a, b, out=out)
 
+    def _mm_into2(self, p0, p1, accumulate):
+        """Two dW products ``(out, a, b)`` of one layer half: one grouped launch of the dW
+        kernel when both fit it (fills each other's partial last wave), else two calls."""
+        (o0, a0, b0), (o1, a1, b1) = p0, p1
+        if (a0.is_cuda and a0.stride(0) == 1 and a1.stride(0) == 1 and a0.shape[1] == a1.shape[1]
+                and ops.gemm_tn_ok(a0.t(), b0, o0) and ops.gemm_tn_ok(a1.t(), b1, o1)):
+            ops.gemm_tn2_(a0.t(), b0, o0, a1.t(), b1, o1, accumulate)
+            return
+        self._mm_into(o0, a0, b0, accumulate)
+        self._mm_into(o1, a1, b1, accumulate)
+
     # ------------------------------------------------------------------ embedding
     def embed_fwd(self, tokens: torch.Tensor) -> torch.Tensor:
         """K7 gather (vocab-parallel: rows outside this rank's shard are zero, then summed)."""
@@ -239,27 +250,28 @@ class Llama:
     def layer_bwd(self, i: int, c: _LayerCtx, g: torch.Tensor, B: int, S: int, accumulate: bool):
         cfg = self.cfg
         Wd, Wgu, Wo, Wqkv = (self.P(f"l{i}.{n}") for n in ("wd", "wgu", "wo", "wqkv"))
+        # The four weight gradients run as two grouped dW launches whose tile counts fill whole
+        # waves of the 256 CUs: {wgu, wo} (7 + 1 waves at Llama-3-8B) as soon as dh2 exists,
+        # {wd, wqkv} (3.5 + 1.5) at the end -- separately, wd and wqkv each end on a half wave.
         # MLP
         gs = torch.mm(g, Wd)
-        self._mm_into(self.G(f"l{i}.wd"), g.t(), c.s, accumulate)
-        c.s = None
         dgu = ops.swiglu_bwd(c.gu, gs)
         del gs
         c.gu = None
         dmm = tp_all_reduce(torch.mm(dgu, Wgu), self.st)
-        self._mm_into(self.G(f"l{i}.wgu"), dgu.t(), c.m, accumulate)
-        del dgu
         dh2 = ops.rmsnorm_bwd(dmm, c.h2, c.rstd2, self.P(f"l{i}.norm2"), self.G(f"l{i}.norm2"),
                               accumulate, dres=g)
         del dmm
+        self._mm_into2((self.G(f"l{i}.wgu"), dgu.t(), c.m), (self.G(f"l{i}.wo"), dh2.t(), c.o), accumulate)
+        del dgu
         # attention
         do = torch.mm(dh2, Wo)
-        self._mm_into(self.G(f"l{i}.wo"), dh2.t(), c.o, accumulate)
         dqkv = attention_bwd(c.qkv, c.o, c.lse, do, B, S, self.hq, self.hkv, cfg.head_dim)
         del do
         ops.rope_(dqkv, self.hq + self.hkv, cfg.head_dim, self.cos, self.sin, seq_len=S, inverse=True)
         da = tp_all_reduce(torch.mm(dqkv, Wqkv), self.st)
-        self._mm_into(self.G(f"l{i}.wqkv"), dqkv.t(), c.a, accumulate)
+        self._mm_into2((self.G(f"l{i}.wd"), g.t(), c.s), (self.G(f"l{i}.wqkv"), dqkv.t(), c.a), accumulate)
+        c.s = None
         del dqkv
         dh1 = ops.rmsnorm_bwd(da, c.h1, c.rstd1, self.P(f"l{i}.norm1"), self.G(f"l{i}.norm1"),
                               accumulate, dres=dh2)

@@ -126,6 +126,13 @@ def gemm_tn_(a, b, c, accumulate: bool = False):
     c.copy_(r)
 
 
+def gemm_tn2_(a0, b0, c0, a1, b1, c1, accumulate: bool = False):
+    """Two weight-gradient products c_i (+)= a_i^T b_i over the same K in ONE launch (the
+    tiles of both share the grid, so one product's partial last wave is filled by the
+    other's tiles).  GPU only; both pairs must satisfy :func:`gemm_tn_ok`."""
+    _k().gemm_tn2_(a0, b0, c0, a1, b1, c1, accumulate)
+
+
 # ---------------------------------------------------------------- SwiGLU (K4)
 def swiglu_fwd(gu):
     return _k().swiglu_fwd(gu) if gu.is_cuda else reference.swiglu_fwd(gu)

@@ -47,6 +47,8 @@ int kf_skinny_gemm(const void*, long, int, const void*, int, int, void*, long, i
 int kf_skinny_gemm_norm(const void*, long, int, const void*, const void*, float, void*, long, const void*, int, int,
                         void*, long, int, int, hipStream_t);
 int kf_gemm_tn(const void*, long, const void*, long, void*, long, int, int, int, int, hipStream_t);
+int kf_gemm_tn2(const void*, long, const void*, long, void*, long, int, int, const void*, long, const void*, long, void*,
+                long, int, int, int, int, hipStream_t);
 long kf_car_header_bytes();
 int kf_car_alloc(long, void**, void*);
 int kf_car_open(const void*, void**);
@@ -465,6 +467,19 @@ void gemm_tn_(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, bool accu
            "gemm_tn");
 }
 
+// Two weight-gradient products over the same K in one launch (their tiles share one grid).
+void gemm_tn2_(const at::Tensor& a0, const at::Tensor& b0, at::Tensor& c0, const at::Tensor& a1, const at::Tensor& b1,
+               at::Tensor& c1, bool accumulate) {
+  TORCH_CHECK(gemm_tn_ok(a0, b0, c0) && gemm_tn_ok(a1, b1, c1) && a0.size(0) == a1.size(0),
+              "gemm_tn2: unsupported shapes/strides");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(a0.device());
+  check_rc(kf_gemm_tn2(a0.data_ptr(), a0.stride(0), b0.data_ptr(), b0.stride(0), c0.data_ptr(), c0.stride(0),
+                       (int)a0.size(1), (int)b0.size(1), a1.data_ptr(), a1.stride(0), b1.data_ptr(), b1.stride(0),
+                       c1.data_ptr(), c1.stride(0), (int)a1.size(1), (int)b1.size(1), (int)a0.size(0),
+                       accumulate ? 1 : 0, cur_stream()),
+           "gemm_tn2");
+}
+
 // K7 embedding: tokens int64 [T]; E [vl, H] (this rank's vocab shard starting at vstart).
 at::Tensor embed_fwd(const at::Tensor& tok, const at::Tensor& E, int64_t vstart) {
   check_bf16_cuda(E, "E");
@@ -519,6 +534,8 @@ TORCH_LIBRARY(kfamd, m) {
   m.def("car_error", &car_error);
   m.def("gemm_tn_ok", &gemm_tn_ok);
   m.def("gemm_tn_(Tensor a, Tensor b, Tensor(a!) c, bool accumulate) -> ()", &gemm_tn_);
+  m.def("gemm_tn2_(Tensor a0, Tensor b0, Tensor(a!) c0, Tensor a1, Tensor b1, Tensor(b!) c1, bool accumulate) -> ()",
+        &gemm_tn2_);
   m.def("embed_fwd", &embed_fwd);
   m.def("embed_bwd_(Tensor tok, Tensor g, Tensor(a!) dE, int vstart, bool accumulate) -> ()", &embed_bwd_);
   m.def("rope_append_(Tensor(a!) qkv, int Hq, Tensor cos, Tensor sin, Tensor slots, Tensor pos, Tensor(b!) kc, "

@@ -126,14 +126,36 @@ template <> struct Cnt<5> { static constexpr int v = 8; };
 template <> struct Cnt<6> { static constexpr int v = 10; };
 template <> struct Cnt<7> { static constexpr int v = 12; };
 
-template <bool ACC>
-__global__ __launch_bounds__(512, 1) void gemm_tn_kernel(const bf16_t* __restrict__ A, long lda,
-                                                         const bf16_t* __restrict__ Bm, long ldb,
-                                                         bf16_t* __restrict__ C, long ldc, int M, int N, int K) {
+// Up to two independent products with the same K (the two weight gradients of one half of a
+// decoder layer) share one launch: their tiles form one grid, so the partial last wave of
+// one product is filled by tiles of the other (e.g. wo 256 + wqkv 384 tiles = 2.5 waves of
+// 256 CUs instead of 1 + 1.5 rounded up to 3).
+struct TnProblem {
+  const bf16_t* A;
+  const bf16_t* B;
+  bf16_t* C;
+  long lda, ldb, ldc;
+  int M, N, acc, tiles;
+};
+struct TnGroup {
+  TnProblem p[2];
+  int n, total;
+};
+
+__global__ __launch_bounds__(512, 1) void gemm_tn_kernel(TnGroup grp, int K) {
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int lid = xcd_remap(blockIdx.x, grp.total);
+  const int pi = (grp.n > 1 && lid >= grp.p[0].tiles) ? 1 : 0;
+  if (pi) lid -= grp.p[0].tiles;
+  const TnProblem& P = grp.p[pi];
+  const bf16_t* __restrict__ A = P.A;
+  const bf16_t* __restrict__ Bm = P.B;
+  bf16_t* __restrict__ C = P.C;
+  const long lda = P.lda, ldb = P.ldb, ldc = P.ldc;
+  const int M = P.M, N = P.N;
+  const bool ACC = P.acc != 0;
   const int mt_n = M / BM, nt_n = N / BN;
-  const int lid = xcd_remap(blockIdx.x, mt_n * nt_n);
   const int per_group = GROUP_M * nt_n;
   const int gid = lid / per_group, first_m = gid * GROUP_M;
   const int gsize = min(mt_n - first_m, GROUP_M);
@@ -247,18 +269,40 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_kernel(const bf16_t* __restric
   }
 }
 
+static bool tn_shape_ok(const void* A, long lda, const void* B, long ldb, const void* C, long ldc, int M, int N,
+                        int K) {
+  if (M % BM || N % BN || K % (BK * NBUF) || lda % 8 || ldb % 8 || ldc % 4) return false;
+  return !(((uintptr_t)A | (uintptr_t)B) & 15) && !((uintptr_t)C & 7);
+}
+
 extern "C" int kf_gemm_tn(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K,
                           int accumulate, hipStream_t s) {
-  if (M % BM || N % BN || K % (BK * NBUF) || lda % 8 || ldb % 8 || ldc % 4) return 1;
-  if (((uintptr_t)A | (uintptr_t)B) & 15 || ((uintptr_t)C & 7)) return 2;
+  if (!tn_shape_ok(A, lda, B, ldb, C, ldc, M, N, K)) return 1;
   if (M == 0 || N == 0) return 0;
-  const int grid = (M / BM) * (N / BN);
-  if (accumulate)
-    hipLaunchKernelGGL(gemm_tn_kernel<true>, dim3(grid), dim3(512), 0, s, (const bf16_t*)A, lda, (const bf16_t*)B, ldb,
-                       (bf16_t*)C, ldc, M, N, K);
-  else
-    hipLaunchKernelGGL(gemm_tn_kernel<false>, dim3(grid), dim3(512), 0, s, (const bf16_t*)A, lda, (const bf16_t*)B,
-                       ldb, (bf16_t*)C, ldc, M, N, K);
+  TnGroup g{};
+  g.p[0] = TnProblem{(const bf16_t*)A, (const bf16_t*)B, (bf16_t*)C, lda, ldb, ldc, M, N, accumulate, (M / BM) * (N / BN)};
+  g.n = 1;
+  g.total = g.p[0].tiles;
+  hipLaunchKernelGGL(gemm_tn_kernel, dim3(g.total), dim3(512), 0, s, g, K);
+  KF_CHECK_LAUNCH();
+  return 0;
+}
+
+// two products C_i (+)= A_i^T B_i over the same K in one launch (see TnGroup)
+extern "C" int kf_gemm_tn2(const void* A0, long lda0, const void* B0, long ldb0, void* C0, long ldc0, int M0, int N0,
+                           const void* A1, long lda1, const void* B1, long ldb1, void* C1, long ldc1, int M1, int N1,
+                           int K, int accumulate, hipStream_t s) {
+  if (!tn_shape_ok(A0, lda0, B0, ldb0, C0, ldc0, M0, N0, K) || !tn_shape_ok(A1, lda1, B1, ldb1, C1, ldc1, M1, N1, K))
+    return 1;
+  TnGroup g{};
+  g.p[0] = TnProblem{(const bf16_t*)A0, (const bf16_t*)B0, (bf16_t*)C0, lda0, ldb0, ldc0, M0, N0, accumulate,
+                     (M0 / BM) * (N0 / BN)};
+  g.p[1] = TnProblem{(const bf16_t*)A1, (const bf16_t*)B1, (bf16_t*)C1, lda1, ldb1, ldc1, M1, N1, accumulate,
+                     (M1 / BM) * (N1 / BN)};
+  g.n = 2;
+  g.total = g.p[0].tiles + g.p[1].tiles;
+  if (g.total == 0) return 0;
+  hipLaunchKernelGGL(gemm_tn_kernel, dim3(g.total), dim3(512), 0, s, g, K);
   KF_CHECK_LAUNCH();
   return 0;
 }

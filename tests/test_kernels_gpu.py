@@ -187,6 +187,23 @@ def test_gemm_tn(M, N, K, accumulate):
     assert torch.equal(c, c2)
 
 
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_gemm_tn2_grouped_matches_single(accumulate):
+    """Two dW products in one grouped launch == two single launches, bit for bit."""
+    torch.manual_seed(1)
+    K = 512
+    shapes = ((768, 512), (256, 1280))
+    a = [torch.randn(K, M + 32, device=DEV, dtype=torch.bfloat16)[:, :M] for M, _ in shapes]
+    b = [torch.randn(K, N, device=DEV, dtype=torch.bfloat16) for _, N in shapes]
+    c0 = [torch.randn(M, N, device=DEV, dtype=torch.bfloat16) for M, N in shapes]
+    c = [x.clone() for x in c0]
+    ops.gemm_tn2_(a[0], b[0], c[0], a[1], b[1], c[1], accumulate)
+    for i in range(2):
+        ref = c0[i].clone()
+        ops.gemm_tn_(a[i], b[i], ref, accumulate)
+        assert torch.equal(c[i], ref), i
+
+
 def test_gemm_tn_rejects_unaligned():
     a = torch.randn(64, 200, device=DEV, dtype=torch.bfloat16)
     b = torch.randn(64, 256, device=DEV, dtype=torch.bfloat16)
