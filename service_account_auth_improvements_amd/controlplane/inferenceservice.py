@@ -13,7 +13,8 @@ For ``spec.predictor`` it reconciles:
   container ``kserve-container`` running this repo's predictor
   (``python -m service_account_auth_improvements_amd.serving.server``) on :8080 with the
   model's ``resources`` (``amd.com/gpu``, which the device plugin turns into
-  ``HIP_VISIBLE_DEVICES``); ``storageUri`` ``pvc://<claim>/<path>`` mounts the claim
+  ``HIP_VISIBLE_DEVICES``; more than one GPU runs the predictor tensor-parallel, one process
+  per GPU under ``kfamd-launch``, see serving/tp.py); ``storageUri`` ``pvc://<claim>/<path>`` mounts the claim
   read-only at ``/mnt/models`` and passes ``--checkpoint``.  ``predictor.containers``
   (custom predictor) is used verbatim.
 * Service ``<name>-predictor`` (80 -> 8080) and, with ``ISTIO_GATEWAY``/``ISTIO_HOST`` set, a
@@ -65,9 +66,18 @@ def predictor_container(isvc: dict) -> tuple:
         mounts.append({"name": "kserve-pvc-source", "mountPath": "/mnt/pvc", "readOnly": True})
         args += ["--checkpoint", os.path.join("/mnt/pvc", sub) if sub else "/mnt/pvc"]
     args += [str(a) for a in model.get("args") or []]
+    command = ["python"]
+    resources = model.get("resources") or {}
+    gpus = int((resources.get("limits") or {}).get("amd.com/gpu", 0) or 0)
+    if gpus > 1:
+        # one process per GPU (Megatron TP over the pod's GPUs); rank 0 serves HTTP (serving/tp.py)
+        from .training import launcher_path
+        command = [launcher_path(), "--nnodes", "1", "--node-rank", "0", "--nproc-per-node", str(gpus),
+                   "--master-addr", "127.0.0.1", "--master-port", "29590", "--isolate-devices", "--", "python"]
+        args += ["--tp", str(gpus)]
     ctr = {"name": "kserve-container", "image": model.get("image") or os.environ.get(
                "KFAMD_PREDICTOR_IMAGE", "kfamd/predictor-rocm:latest"),
-           "command": ["python"], "args": args,
+           "command": command, "args": args,
            "env": [{"name": "MODEL_NAME", "value": name}, {"name": "PORT", "value": "8080"}]
            + copy.deepcopy(model.get("env") or []),
            "ports": [{"containerPort": 8080, "name": "http1", "protocol": "TCP"}],

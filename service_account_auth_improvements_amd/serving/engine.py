@@ -331,14 +331,15 @@ class Scheduler:
 
 def build_engine(model_name: str = "llama3-8b", device=None, n_slots: int = 64, max_len: int = 4096,
                  checkpoint: Optional[str] = None, n_layers: Optional[int] = None, seed: int = 1234,
-                 st: Optional[ParallelState] = None, use_graphs: Optional[bool] = None) -> Engine:
+                 st: Optional[ParallelState] = None, use_graphs: Optional[bool] = None,
+                 full_init: bool = False) -> Engine:
     cfg = LlamaConfig.preset(model_name)
     if n_layers:
         cfg = cfg.with_(n_layers=n_layers)
     if device is None:
         device = "cuda" if torch.cuda.is_available() else "cpu"
     st = st or ParallelState(device=torch.device(device))
-    model = Llama(cfg, st=st, device=device, seed=seed).allocate(grads=False)
+    model = Llama(cfg, st=st, device=device, seed=seed, full_init=full_init).allocate(grads=False)
     if checkpoint:
         from ..runtime.checkpoint import load_params
         load_params(model, checkpoint)

@@ -199,9 +199,26 @@ def main(argv=None):
     p.add_argument("--slots", type=int, default=64)
     p.add_argument("--max-len", type=int, default=4096)
     p.add_argument("--layers", type=int, default=None)
+    p.add_argument("--tp", type=int, default=int(os.environ.get("WORLD_SIZE", "1")),
+                   help="tensor-parallel degree (one process per GPU under kfamd-launch; rank 0 serves HTTP)")
     a = p.parse_args(argv)
     logging.basicConfig(level=logging.INFO)
-    eng = build_engine(a.model, n_slots=a.slots, max_len=a.max_len, checkpoint=a.checkpoint, n_layers=a.layers)
+    st = None
+    if a.tp > 1:
+        import torch.distributed as dist
+
+        from ..parallel.state import init_distributed
+        from .tp import TPLeaderEngine, follower_loop
+        st = init_distributed(tp=a.tp)
+        ctrl = dist.new_group(backend="gloo")      # command channel (host objects)
+    eng = build_engine(a.model, n_slots=a.slots, max_len=a.max_len, checkpoint=a.checkpoint, n_layers=a.layers,
+                       st=st, device=None if st is None else str(st.device))
+    if st is not None:
+        if st.rank != 0:
+            n = follower_loop(eng, ctrl)
+            log.info("TP follower rank %d done after %d commands", st.rank, n)
+            return
+        eng = TPLeaderEngine(eng, ctrl)
     sched = Scheduler(eng, max_batch=a.slots).start()
     tok = HFTokenizer(a.tokenizer) if a.tokenizer else None
     app = create_app(sched, a.model_name, tok)

@@ -155,3 +155,59 @@ def test_isvc_end_to_end_cpu(tmp_path):
     finally:
         mgr.stop()
         kub.shutdown()
+
+
+def test_isvc_multi_gpu_predictor_runs_tensor_parallel():
+    srv = APIServer()
+    c = InMemoryClient(srv)
+    c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "team"}})
+    mgr = Manager(c).add(isvcmod.InferenceServiceReconciler(c))
+    c.create(_isvc(resources={"limits": {"amd.com/gpu": "4"}}))
+    mgr.run_until_idle()
+    ctr = c.get("apps/v1", "Deployment", "llama-predictor", "team")["spec"]["template"]["spec"]["containers"][0]
+    cmd = ctr["command"]
+    assert cmd[0].endswith("kfamd_launch") and cmd[cmd.index("--nproc-per-node") + 1] == "4"
+    assert "--isolate-devices" in cmd and cmd[-2:] == ["--", "python"]
+    assert ctr["args"][ctr["args"].index("--tp") + 1] == "4"
+
+
+def _tp_predictor_body(rank, world):
+    import torch.distributed as dist
+
+    from service_account_auth_improvements_amd.parallel.state import init_distributed
+    from service_account_auth_improvements_amd.serving.engine import Request, Scheduler, build_engine
+    from service_account_auth_improvements_amd.serving.tp import TPLeaderEngine, follower_loop
+
+    st = init_distributed(tp=world, pp=1, device="cpu")
+    ctrl = dist.new_group(backend="gloo")
+    e = build_engine("tiny", device="cpu", n_slots=4, max_len=128, st=st, full_init=True)
+    if rank != 0:
+        return follower_loop(e, ctrl)
+    lead = TPLeaderEngine(e, ctrl)
+    logits = [lead.prefill(0, list(range(3, 40)))]
+    for j, t in enumerate((5, 6)):
+        logits.append(lead.decode([t], [0], [37 + j])[0])
+    s = Scheduler(lead, max_batch=2)
+    reqs = [s.submit(Request(prompt=list(range(k, k + 9)), max_new_tokens=4)) for k in (1, 20)]
+    s.run_until_idle()
+    lead.stop()
+    return torch.stack([x.float() for x in logits]), [r.output for r in reqs]
+
+
+def test_tp_predictor_leader_drives_followers():
+    """Rank 0 (HTTP + scheduler) broadcasts every engine call; rank 1 replays it: the TP=2
+    logits match a TP=1 engine and the scheduler completes requests through the leader."""
+    from dist_util import run_ranks
+    from service_account_auth_improvements_amd.serving.engine import build_engine
+
+    res = run_ranks(_tp_predictor_body, world=2, timeout=300)
+    logits, outs = res[0]
+    # follower replayed: 1 prefill + 2 decodes, then the scheduler's 2 prefills (first tokens)
+    # and 3 joint decode steps (tokens 2..4 of both requests)
+    assert res[1] == 3 + 2 + 3
+    ref = build_engine("tiny", device="cpu", n_slots=4, max_len=128, full_init=True)
+    exp = [ref.prefill(0, list(range(3, 40)))]
+    for j, t in enumerate((5, 6)):
+        exp.append(ref.decode([t], [0], [37 + j])[0])
+    assert (logits - torch.stack([x.float() for x in exp])).abs().max().item() < 5e-2
+    assert all(len(o) == 4 for o in outs)
