@@ -24,6 +24,7 @@ Design (MI355X-first):
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, replace
 from typing import Callable, List, Optional
 
@@ -34,6 +35,9 @@ import torch.nn.functional as F
 from .. import ops
 from ..ops.attention import attention_bwd, attention_fwd
 from ..parallel.state import ParallelState, get_state, tp_all_reduce
+
+# KFAMD_DX_T=0 runs the activation-gradient GEMMs on the untransposed weights (A/B switch)
+_DX_T = os.environ.get("KFAMD_DX_T", "1") != "0"
 from ..runtime.flat import FlatGroup
 
 
@@ -207,6 +211,16 @@ class Llama:
         else:
             torch.mm(a, b, out=out)
 
+    @staticmethod
+    def _mm_dx(dy, w):
+        """Activation gradient dy . w for w [N, K] row-major.  On the GPU w is first
+        transposed into scratch (ops/csrc/transpose.hip) so hipBLASLt sees the forward's
+        operand layout (dy . (w^T)^T), whose solutions run 10-30 % faster at the Llama shapes
+        than the plain "dy . w" ones; the copy costs one streaming pass over w."""
+        if _DX_T and dy.is_cuda and ops.transpose_ok(w):
+            return torch.mm(dy, ops.transpose(w).t())
+        return torch.mm(dy, w)
+
     def _mm_into2(self, p0, p1, accumulate):
         """Two dW products ``(out, a, b)`` of one layer half: one grouped launch of the dW
         kernel when both fit it (fills each other's partial last wave), else two calls."""
@@ -254,22 +268,22 @@ class Llama:
         # waves of the 256 CUs: {wgu, wo} (7 + 1 waves at Llama-3-8B) as soon as dh2 exists,
         # {wd, wqkv} (3.5 + 1.5) at the end -- separately, wd and wqkv each end on a half wave.
         # MLP
-        gs = torch.mm(g, Wd)
+        gs = self._mm_dx(g, Wd)
         dgu = ops.swiglu_bwd(c.gu, gs)
         del gs
         c.gu = None
-        dmm = tp_all_reduce(torch.mm(dgu, Wgu), self.st)
+        dmm = tp_all_reduce(self._mm_dx(dgu, Wgu), self.st)
         dh2 = ops.rmsnorm_bwd(dmm, c.h2, c.rstd2, self.P(f"l{i}.norm2"), self.G(f"l{i}.norm2"),
                               accumulate, dres=g)
         del dmm
         self._mm_into2((self.G(f"l{i}.wgu"), dgu.t(), c.m), (self.G(f"l{i}.wo"), dh2.t(), c.o), accumulate)
         del dgu
         # attention
-        do = torch.mm(dh2, Wo)
+        do = self._mm_dx(dh2, Wo)
         dqkv = attention_bwd(c.qkv, c.o, c.lse, do, B, S, self.hq, self.hkv, cfg.head_dim)
         del do
         ops.rope_(dqkv, self.hq + self.hkv, cfg.head_dim, self.cos, self.sin, seq_len=S, inverse=True)
-        da = tp_all_reduce(torch.mm(dqkv, Wqkv), self.st)
+        da = tp_all_reduce(self._mm_dx(dqkv, Wqkv), self.st)
         self._mm_into2((self.G(f"l{i}.wd"), g.t(), c.s), (self.G(f"l{i}.wqkv"), dqkv.t(), c.a), accumulate)
         c.s = None
         del dqkv
@@ -301,7 +315,7 @@ class Llama:
 
     def head_bwd(self, ctx, accumulate: bool):
         h, rstd, y, dlogits = ctx
-        dy = tp_all_reduce(torch.mm(dlogits, self.P("lm_head")), self.st)
+        dy = tp_all_reduce(self._mm_dx(dlogits, self.P("lm_head")), self.st)
         self._mm_into(self.G("lm_head"), dlogits.t(), y, accumulate)
         self._ready(self.mats, "lm_head")
         dh = ops.rmsnorm_bwd(dy, h, rstd, self.P("final_norm"), self.G("final_norm"), accumulate)

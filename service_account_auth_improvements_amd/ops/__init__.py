@@ -109,6 +109,17 @@ def skinny_gemm_norm(x, residual, norm_w, eps, w, swiglu: bool = False):
     return skinny_gemm(a, w, swiglu), h
 
 
+def transpose_ok(w) -> bool:
+    return w.is_cuda and w.dim() == 2 and w.stride(1) == 1 and w.shape[0] % 64 == 0 and w.shape[1] % 64 == 0
+
+
+def transpose(w):
+    """Row-major copy of w^T (LDS-tiled HIP kernel on the GPU)."""
+    if w.is_cuda:
+        return _k().transpose_bf16(w)
+    return w.t().contiguous()
+
+
 # ---------------------------------------------------------------- weight-gradient GEMM
 def gemm_tn_ok(a, b, c) -> bool:
     """True when the HIP weight-gradient GEMM handles c = a^T b for these operands."""

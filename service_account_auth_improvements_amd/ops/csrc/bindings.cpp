@@ -49,6 +49,7 @@ int kf_skinny_gemm_norm(const void*, long, int, const void*, const void*, float,
 int kf_gemm_tn(const void*, long, const void*, long, void*, long, int, int, int, int, hipStream_t);
 int kf_gemm_tn2(const void*, long, const void*, long, void*, long, int, int, const void*, long, const void*, long, void*,
                 long, int, int, int, int, hipStream_t);
+int kf_transpose_bf16(const void*, long, void*, long, int, int, hipStream_t);
 long kf_car_header_bytes();
 int kf_car_alloc(long, void**, void*);
 int kf_car_open(const void*, void**);
@@ -411,6 +412,19 @@ std::tuple<at::Tensor, at::Tensor> skinny_gemm_norm(const at::Tensor& x, const s
   return {y, h};
 }
 
+// out = in^T for a bf16 [R, C] matrix (R, C % 64 == 0; unit inner stride)
+at::Tensor transpose_bf16(const at::Tensor& x) {
+  check_bf16_cuda(x, "x");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.size(0) % 64 == 0 && x.size(1) % 64 == 0,
+              "transpose_bf16: 2-D, unit inner stride, dims % 64 == 0");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  auto out = at::empty({x.size(1), x.size(0)}, x.options());
+  check_rc(kf_transpose_bf16(x.data_ptr(), x.stride(0), out.data_ptr(), out.stride(0), (int)x.size(0), (int)x.size(1),
+                             cur_stream()),
+           "transpose_bf16");
+  return out;
+}
+
 // ---- one-shot IPC all-reduce (ops/csrc/custom_ar.hip). Device pointers travel as int64.
 std::tuple<int64_t, at::Tensor> car_alloc(int64_t slot_bytes) {
   void* p = nullptr;
@@ -526,6 +540,7 @@ TORCH_LIBRARY(kfamd, m) {
   m.def("decode_attn", &decode_attn);
   m.def("skinny_gemm", &skinny_gemm);
   m.def("skinny_gemm_norm", &skinny_gemm_norm);
+  m.def("transpose_bf16", &transpose_bf16);
   m.def("car_alloc", &car_alloc);
   m.def("car_open", &car_open);
   m.def("car_close", &car_close);

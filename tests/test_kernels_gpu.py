@@ -209,3 +209,17 @@ def test_gemm_tn_rejects_unaligned():
     b = torch.randn(64, 256, device=DEV, dtype=torch.bfloat16)
     c = torch.empty(200, 256, device=DEV, dtype=torch.bfloat16)
     assert not ops.gemm_tn_ok(a, b, c)
+
+
+@pytest.mark.parametrize("shape", [(64, 64), (4096, 6144), (14336, 4096), (192, 128)])
+def test_transpose_bf16_exact(shape):
+    from service_account_auth_improvements_amd import ops
+
+    w = torch.randn(*shape, device="cuda", dtype=torch.bfloat16)
+    t = ops.transpose(w)
+    assert t.shape == (shape[1], shape[0]) and t.is_contiguous()
+    assert torch.equal(t, w.t().contiguous())
+    # strided input rows (a column slice of a wider matrix)
+    big = torch.randn(shape[0], shape[1] + 128, device="cuda", dtype=torch.bfloat16)
+    v = big[:, 64:64 + shape[1]]
+    assert torch.equal(ops.transpose(v), v.t().contiguous())
