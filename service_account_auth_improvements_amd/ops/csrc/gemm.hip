@@ -27,6 +27,9 @@
 //    XCD share A and B panels in its L2.
 //  * s_setprio(1/0) around each MFMA group measured null (tools/kbench/gemm_bench: 1276 vs
 //    1279 TF over the step's dW shapes), so the schedule is left to the counted waits.
+//  * A 4-wave variant (2 x 2 waves of 128 x 128, 256 accumulators pinned to AGPRs with
+//    inline-asm MFMAs, two-group-ahead operand reads) halves the LDS read rate but ran at
+//    1210 TF vs 1275: at one wave per SIMD every wait/barrier bubble reaches the MFMA pipe.
 #include "common.h"
 
 using namespace kf;

@@ -24,6 +24,15 @@ __global__ void init_bf16(bf16_t* p, long n, u32 seed, float amp) {
   }
 }
 
+// full-matrix checksum: sum_i C[i] * (i % 7 + 1) in double (per-thread partials, one atomic per block)
+__global__ void checksum(const bf16_t* c, long n, double* out) {
+  double acc = 0;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    acc += (double)bf2f(c[i]) * (double)(i % 7 + 1);
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  if ((threadIdx.x & 63) == 0) atomicAdd(out, acc);
+}
+
 int main(int argc, char** argv) {
   const int iters = argc > 1 ? atoi(argv[1]) : 20;
   const int K = 16384;
@@ -55,10 +64,13 @@ int main(int argc, char** argv) {
     const double mult = strcmp(s.name, "lm_head") ? 32 : 1;
     tot_ms += mult * ms;
     tot_fl += mult * fl;
-    std::vector<uint16_t> h(4096);
-    CK(hipMemcpy(h.data(), C, h.size() * 2, hipMemcpyDeviceToHost));
+    double* dcs;
+    CK(hipMalloc(&dcs, 8));
+    CK(hipMemset(dcs, 0, 8));
+    checksum<<<1024, 256>>>(C, (long)s.M * s.N, dcs);
     double cs = 0;
-    for (size_t i = 0; i < h.size(); ++i) cs += __builtin_bit_cast(float, (u32)h[i] << 16) * (double)(i % 5 + 1);
+    CK(hipMemcpy(&cs, dcs, 8, hipMemcpyDeviceToHost));
+    CK(hipFree(dcs));
     printf("%-8s M=%6d N=%6d  %8.3f ms  %6.0f TF  chk %.6e\n", s.name, s.M, s.N, ms, fl / (ms * 1e-3) / 1e12, cs);
   }
   printf("dW per step: %.1f ms  %.0f TF\n", tot_ms, tot_fl / (tot_ms * 1e-3) / 1e12);
