@@ -110,7 +110,9 @@ def skinny_gemm_norm(x, residual, norm_w, eps, w, swiglu: bool = False):
 
 
 def transpose_ok(w) -> bool:
-    return w.is_cuda and w.dim() == 2 and w.stride(1) == 1 and w.shape[0] % 64 == 0 and w.shape[1] % 64 == 0
+    return (w.is_cuda and w.dtype == torch.bfloat16 and w.dim() == 2 and w.stride(1) == 1
+            and w.shape[0] % 64 == 0 and w.shape[1] % 64 == 0 and w.stride(0) % 8 == 0
+            and w.data_ptr() % 16 == 0)
 
 
 def transpose(w):
