@@ -1,0 +1,72 @@
+"""Data-parallel training on the GPU with two ranks sharing the test box's one MI355X.
+
+RCCL refuses two ranks on one device, so the collectives run over gloo (CUDA tensors staged
+through the host); everything else -- the HIP kernels, the transposed-weight activation
+gradients, the ZeRO-1 flat buffers and their overlapped all-gather -- is the code that runs
+one rank per GPU over RCCL on an 8-GPU node (bench.py under torchrun)."""
+import pytest
+import torch
+
+from dist_util import run_ranks
+
+pytestmark = pytest.mark.gpu
+
+
+def _batches(vocab, n, B=2, S=256, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return [(torch.randint(0, vocab, (B, S), generator=g), torch.randint(0, vocab, (B, S), generator=g))
+            for _ in range(n)]
+
+
+def _dp_body(rank, world, zero1):
+    import os
+
+    os.environ["KFAMD_DIST_BACKEND"] = "gloo"
+    from service_account_auth_improvements_amd.parallel.state import init_distributed
+    from service_account_auth_improvements_amd.runtime.trainer import TrainConfig, Trainer
+
+    st = init_distributed(tp=1, pp=1, device="cuda")
+    tr = Trainer(TrainConfig(model="small", seq_len=256, micro_batch=2, n_layers=2, zero1=zero1, bucket_mb=4,
+                             lr=1e-3), st)
+    b = _batches(tr.mcfg.vocab_size, world)[rank]
+    mine = [(b[0].to(st.device), b[1].to(st.device))]
+    tr.opt.cfg.lr = 0.0
+    tr.train_step(mine)                      # lr 0: exposes the reduced gradients
+    grads = tr.model.mats.grads.float().clone() / world
+    if zero1:   # after the reduce-scatter only this rank's shard of each bucket is reduced
+        mask = torch.zeros_like(grads, dtype=torch.bool)
+        for lo, hi in tr.reducer.shard_ranges(tr.model.mats, st.dp_rank):
+            mask[lo:hi] = True
+        grads = torch.where(mask, grads, torch.full_like(grads, float("nan")))
+    tr.opt.cfg.lr = 1e-3
+    losses = [float(tr.train_step(mine)) for _ in range(3)]
+    tr.sync_params()
+    torch.cuda.synchronize()
+    return losses, tr.model.mats.params.float().cpu(), grads.cpu()
+
+
+def _single_grads(world):
+    from service_account_auth_improvements_amd.parallel.state import ParallelState
+    from service_account_auth_improvements_amd.runtime.trainer import TrainConfig, Trainer
+
+    st = ParallelState(device=torch.device("cuda", 0))
+    tr = Trainer(TrainConfig(model="small", seq_len=256, micro_batch=2, n_layers=2, lr=0.0), st)
+    batches = [(x.to(st.device), y.to(st.device)) for x, y in _batches(tr.mcfg.vocab_size, world)]
+    tr.train_step(batches)                   # both ranks' batches as 2 accumulated micro-batches
+    return tr.model.mats.grads.float().cpu()
+
+
+@pytest.mark.parametrize("zero1", [False, True])
+def test_ddp_two_ranks_one_gpu_matches_single_process(zero1):
+    res = run_ranks(_dp_body, world=2, args=(zero1,), timeout=300)
+    (l0, p0, g0), (l1, p1, g1) = res
+    assert torch.equal(p0, p1), "replicas diverged"
+    assert l0[-1] < l0[0], l0
+    ref = _single_grads(2)
+    for g in (g0, g1):
+        own = ~torch.isnan(g)
+        assert own.any()
+        rel = ((g[own] - ref[own]).abs().max() / ref.abs().max()).item()
+        assert rel < 2e-2, rel
+    if zero1:   # the two shards tile the buffer
+        assert bool((~torch.isnan(g0) | ~torch.isnan(g1)).all())
