@@ -44,6 +44,8 @@ int kf_kv_fill(const void*, long, int, int, int, int, int, void*, void*, int, hi
 int kf_embed_fwd(const long*, const void*, void*, int, int, long, long, hipStream_t);
 int kf_embed_bwd(const long*, const long*, const void*, void*, int, int, long, long, int, hipStream_t);
 int kf_skinny_gemm(const void*, long, int, const void*, int, int, void*, long, int, int, hipStream_t);
+int kf_gemv(const void*, long, int, const void*, const void*, float, void*, long, const void*, int, int, void*, long,
+            int, int, hipStream_t);
 int kf_skinny_gemm_norm(const void*, long, int, const void*, const void*, float, void*, long, const void*, int, int,
                         void*, long, int, int, hipStream_t);
 int kf_gemm_tn(const void*, long, const void*, long, void*, long, int, int, int, int, hipStream_t);
@@ -361,6 +363,15 @@ void kv_fill_(const at::Tensor& qkv, int64_t S, int64_t Hq, int64_t slot, at::Te
            "kv_fill");
 }
 
+// 1-2 decode rows (and 3-4 rows on the large matrices) stream W faster through the VALU GEMV
+// (ops/csrc/gemv.hip, 1 KB contiguous per row and instruction) than through the MFMA skinny
+// kernel: tools/kbench/gemv_bench.hip, e.g. gate/up 59 -> 41 us, LM head 199 -> 154 us at M = 1.
+static bool use_gemv(int64_t M, int64_t Nw, int64_t K) {
+  if (M > 4) return false;
+  const bool mfma_fits = K % 256 == 0 && Nw % 16 == 0;   // else the GEMV is the only kernel for it
+  return M <= 2 || !mfma_fits || Nw * K > (int64_t)20 * 1024 * 1024;
+}
+
 // Decode GEMM: x [M<=64, K] (unit inner stride) . w[N, K]^T -> [M, N]; swiglu: w = [gate; up]
 // (2F rows) -> silu(x.gate^T) * (x.up^T), [M, F].
 at::Tensor skinny_gemm(const at::Tensor& x, const at::Tensor& w, bool swiglu) {
@@ -369,11 +380,16 @@ at::Tensor skinny_gemm(const at::Tensor& x, const at::Tensor& w, bool swiglu) {
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && w.dim() == 2 && w.is_contiguous(), "skinny_gemm: 2-D operands");
   const int64_t M = x.size(0), K = x.size(1), Nw = w.size(0);
   TORCH_CHECK(w.size(1) == K, "skinny_gemm: K mismatch");
-  TORCH_CHECK(M >= 1 && M <= 64 && K % 256 == 0, "skinny_gemm: needs 1 <= M <= 64, K % 256 == 0");
+  TORCH_CHECK(!swiglu || Nw % 2 == 0, "skinny_gemm: swiglu needs an even number of rows");
   const int64_t N = swiglu ? Nw / 2 : Nw;
-  TORCH_CHECK(N % 16 == 0 && (!swiglu || Nw % 2 == 0), "skinny_gemm: N % 16 != 0");
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   auto y = at::empty({M, N}, x.options());
+  if (M >= 1 && use_gemv(M, Nw, K) &&
+      kf_gemv(x.data_ptr(), x.stride(0), (int)M, nullptr, nullptr, 0.f, nullptr, 0, w.data_ptr(), (int)N, (int)K,
+              y.data_ptr(), y.stride(0), swiglu ? 1 : 0, (int)N, cur_stream()) == 0)
+    return y;
+  TORCH_CHECK(M >= 1 && M <= 64 && K % 256 == 0, "skinny_gemm: needs 1 <= M <= 64, K % 256 == 0");
+  TORCH_CHECK(N % 16 == 0, "skinny_gemm: N % 16 != 0");
   check_rc(kf_skinny_gemm(x.data_ptr(), x.stride(0), (int)M, w.data_ptr(), (int)N, (int)K, y.data_ptr(), y.stride(0),
                           swiglu ? 1 : 0, (int)N, cur_stream()),
            "skinny_gemm");
@@ -393,8 +409,8 @@ std::tuple<at::Tensor, at::Tensor> skinny_gemm_norm(const at::Tensor& x, const s
   const int64_t M = x.size(0), K = x.size(1), Nw = w.size(0);
   TORCH_CHECK(w.size(1) == K && nw.numel() == K && nw.is_contiguous(), "skinny_gemm_norm: K mismatch");
   TORCH_CHECK(M >= 1 && M <= 8 && M * K <= 32768 && K % 256 == 0, "skinny_gemm_norm: needs M <= 8, M*K <= 32768, K % 256 == 0");
+  TORCH_CHECK(!swiglu || Nw % 2 == 0, "skinny_gemm_norm: swiglu needs an even number of rows");
   const int64_t N = swiglu ? Nw / 2 : Nw;
-  TORCH_CHECK(N % 16 == 0 && (!swiglu || Nw % 2 == 0), "skinny_gemm_norm: N % 16 != 0");
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   at::Tensor h = x;
   const void* rp = nullptr;
@@ -405,6 +421,12 @@ std::tuple<at::Tensor, at::Tensor> skinny_gemm_norm(const at::Tensor& x, const s
     rp = res->data_ptr();
   }
   auto y = at::empty({M, N}, x.options());
+  if (use_gemv(M, Nw, K) &&
+      kf_gemv(x.data_ptr(), x.stride(0), (int)M, rp, nw.data_ptr(), (float)eps, rp ? h.data_ptr() : nullptr,
+              h.stride(0), w.data_ptr(), (int)N, (int)K, y.data_ptr(), y.stride(0), swiglu ? 1 : 0, (int)N,
+              cur_stream()) == 0)
+    return {y, h};
+  TORCH_CHECK(N % 16 == 0, "skinny_gemm_norm: N % 16 != 0");
   check_rc(kf_skinny_gemm_norm(x.data_ptr(), x.stride(0), (int)M, rp, nw.data_ptr(), (float)eps,
                                rp ? h.data_ptr() : nullptr, h.stride(0), w.data_ptr(), (int)N, (int)K, y.data_ptr(),
                                y.stride(0), swiglu ? 1 : 0, (int)N, cur_stream()),

@@ -156,28 +156,57 @@ __global__ __launch_bounds__(NT) void decode_split_kernel(
   }
 }
 
-// one block per (b, q head): merge the split partials, normalise, write bf16
-__global__ __launch_bounds__(D) void decode_combine_kernel(const float* __restrict__ part_o,
-                                                           const float* __restrict__ part_ml,
-                                                           int splits, bf16_t* __restrict__ out,
-                                                           long out_ld, int hq) {
-  const int bh = blockIdx.x, d = threadIdx.x;
+// one block per (b, q head), 256 threads: merge the split partials, normalise, write bf16.
+// At B = 1 the merge is latency-bound (up to ~128 splits of a few keys each), so the work
+// is spread over the block instead of one dependent loop per output element:
+//   1. the split maxima / weights w_s = exp2(m_s - M) and den = sum w_s l_s are computed
+//      once per block (one split per thread) and w_s is kept in LDS;
+//   2. the two 128-thread halves each sum w_s o_s[d] over every other split (independent,
+//      coalesced L2 loads, 8 in flight per thread), then add their halves through LDS.
+constexpr int CB_NT = 256, CB_MAXS = 1024;
+__global__ __launch_bounds__(CB_NT) void decode_combine_kernel(const float* __restrict__ part_o,
+                                                               const float* __restrict__ part_ml,
+                                                               int splits, bf16_t* __restrict__ out,
+                                                               long out_ld, int hq) {
+  __shared__ float ws[CB_MAXS];
+  __shared__ float red[CB_NT / 64];
+  __shared__ float half_num[D];
+  const int bh = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b = bh / hq, h = bh % hq;
   const float* ml = part_ml + (long)bh * splits * 2;
-  // branch-free and unrolled: the split partials are independent L2 loads, so they are
-  // issued back to back instead of one dependent round trip per split (latency-bound at B=1)
-  float M = -INFINITY;
-#pragma unroll 8
-  for (int s = 0; s < splits; ++s) M = fmaxf(M, ml[2 * s]);
-  float num = 0.f, den = 0.f;
-#pragma unroll 8
-  for (int s = 0; s < splits; ++s) {
+  float mloc = -INFINITY;
+  for (int s = tid; s < splits; s += CB_NT) mloc = fmaxf(mloc, ml[2 * s]);
+  mloc = wave_max(mloc);
+  if (lane == 0) red[wave] = mloc;
+  __syncthreads();
+  float M = red[0];
+#pragma unroll
+  for (int w = 1; w < CB_NT / 64; ++w) M = fmaxf(M, red[w]);
+  __syncthreads();
+  float dl = 0.f;
+  for (int s = tid; s < splits; s += CB_NT) {
     const float m = ml[2 * s];
     const float w = m == -INFINITY ? 0.f : exp2f(m - M);
-    num = fmaf(w, part_o[((long)bh * splits + s) * D + d], num);
-    den = fmaf(w, ml[2 * s + 1], den);
+    ws[s] = w;
+    dl = fmaf(w, ml[2 * s + 1], dl);
   }
-  out[(long)b * out_ld + (long)h * D + d] = f2bf(den > 0.f ? num / den : 0.f);
+  dl = wave_sum(dl);
+  if (lane == 0) red[wave] = dl;
+  __syncthreads();
+  float den = 0.f;
+#pragma unroll
+  for (int w = 0; w < CB_NT / 64; ++w) den += red[w];
+  const int d = tid & (D - 1), half = tid / D;
+  const float* po = part_o + (long)bh * splits * D + d;
+  float num = 0.f;
+#pragma unroll 8
+  for (int s = half; s < splits; s += 2) num = fmaf(ws[s], po[(long)s * D], num);
+  if (half == 1) half_num[d] = num;
+  __syncthreads();
+  if (half == 0) {
+    num += half_num[d];
+    out[(long)b * out_ld + (long)h * D + d] = f2bf(den > 0.f ? num / den : 0.f);
+  }
 }
 
 template <int G>
@@ -208,7 +237,7 @@ extern "C" int kf_decode_attn(const void* q, long q_ld, const void* kc, const vo
                               hipStream_t st) {
   if (Dh != D || Hkv <= 0 || Hq % Hkv != 0) return 1;
   const int G = Hq / Hkv;
-  if (G > MAXG || splits <= 0) return 2;
+  if (G > MAXG || splits <= 0 || splits > CB_MAXS) return 2;
   if ((Lmax + splits - 1) / splits > MAXCHUNK - 16) return 3;
   if (B == 0) return 0;
   const long head_stride = (long)Lmax * D, slot_stride = (long)Hkv * head_stride;
@@ -224,7 +253,7 @@ extern "C" int kf_decode_attn(const void* q, long q_ld, const void* kc, const vo
     case 8: launch_split<8>(grid, st, q16, q_ld, Hq, k16, v16, slots, lengths, slot_stride, head_stride, splits, sl2, part_o, part_ml); break;
     default: return 4;
   }
-  hipLaunchKernelGGL(decode_combine_kernel, dim3(B * Hq), dim3(D), 0, st, part_o, part_ml, splits,
+  hipLaunchKernelGGL(decode_combine_kernel, dim3(B * Hq), dim3(CB_NT), 0, st, part_o, part_ml, splits,
                      (bf16_t*)out, out_ld, Hq);
   KF_CHECK_LAUNCH();
   return 0;

@@ -1,0 +1,226 @@
+// Decode GEMV for 1 <= M <= 4 rows: Y[M, N] = X[M, K] . W[N, K]^T (bf16 in/out, fp32 sum).
+//
+// At batch 1-4 the decode step is a pure weight stream (2-8 flops per weight byte), so the
+// kernel is laid out for HBM, not for the matrix cores: one wave owns R whole rows of W and
+// its 64 lanes read 64 consecutive 16-byte chunks of a row per instruction (1 KB contiguous
+// per row and instruction, full 128-byte lines), U chunks per row in flight per lane.  The
+// MFMA skinny kernel (skinny_gemm.hip) has to give each lane (row l%16, k-chunk l/16) and so
+// touches 16 rows x 64 B per instruction; it stays the path for 5 <= M <= 64.
+//
+//  * VALU dot products: 8 bf16 of W unpacked by shift/mask, fp32 FMAs with X, R x M
+//    partial sums per lane, one wave reduction per (row, x-row) at the end.  X chunks are
+//    shared by the R rows of the wave (read once per chunk from L1/L2, or from LDS when
+//    the norm prologue staged them).
+//  * SWIGLU: the wave's R gate rows n.. and the matching up rows n + up_off.. are streamed
+//    together and the wave writes silu(gate) * up.
+//  * NORM prologue (decode layer norms fused in, as in skinny_gemm.hip): each workgroup
+//    forms h = bf16(x + res) and its sum of squares, stages y = bf16(h * rstd * w_norm) in
+//    LDS; workgroup 0 stores h.  The first W chunks are requested before the prologue.
+#include "common.h"
+
+using namespace kf;
+
+namespace {
+
+constexpr int GV_WAVES = 4;       // 256-thread workgroups
+constexpr int GV_U = 4;           // chunks per row in flight per lane
+
+struct GvNorm {
+  const bf16_t* res;   // nullable
+  const bf16_t* w;
+  bf16_t* h_out;
+  long ldh;
+  float eps;
+};
+
+__device__ __forceinline__ void unpack_bf8(const u32x4& v, float* f) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(v[i] << 16);
+    f[2 * i + 1] = __uint_as_float(v[i] & 0xffff0000u);
+  }
+}
+
+template <int M, int R, bool SWIGLU, bool NORM>
+__global__ __launch_bounds__(64 * GV_WAVES) void gemv_kernel(const bf16_t* __restrict__ x, long ldx,
+                                                            const bf16_t* __restrict__ w, int N, int K,
+                                                            bf16_t* __restrict__ y, long ldy, int up_off,
+                                                            GvNorm na) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t xs[];   // NORM: M x K normalised rows
+  __shared__ float ssq[GV_WAVES][M];
+  constexpr int NR = SWIGLU ? 2 * R : R;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r0 = (blockIdx.x * GV_WAVES + wave) * R;
+  const int nch = K >> 3;                       // 16-byte chunks per row
+  const int J = (nch + 63) >> 6;                // chunk slots per lane
+
+  auto row_ptr = [&](int i) -> const bf16_t* {
+    const int rr = i < R ? r0 + i : r0 + (i - R) + up_off;
+    return w + (long)rr * K + 8 * lane;
+  };
+  auto row_ok = [&](int i) { return r0 + (i < R ? i : i - R) < N; };
+
+  u32x4 wv[NR][GV_U];
+  auto load_w = [&](int j0) {
+#pragma unroll
+    for (int i = 0; i < NR; ++i)
+#pragma unroll
+      for (int u = 0; u < GV_U; ++u) {
+        const int c = lane + 64 * (j0 + u);
+        wv[i][u] = (row_ok(i) && j0 + u < J && c < nch)
+                       ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(row_ptr(i) + 512 * (j0 + u)))
+                       : u32x4{0, 0, 0, 0};
+      }
+  };
+  load_w(0);
+
+  if constexpr (NORM) {
+    float ss[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) ss[m] = 0.f;
+    for (int c = tid; c < nch; c += 64 * GV_WAVES) {
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        float hv[8];
+        unpack8(ld16(x + (long)m * ldx + 8 * c), hv);
+        if (na.res) {
+          float t[8];
+          unpack8(ld16(na.res + (long)m * ldx + 8 * c), t);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) hv[e] += t[e];
+          const u32x4 hb = pack8(hv);     // residual stream kept (and normed) in bf16
+          if (blockIdx.x == 0) st16(na.h_out + (long)m * na.ldh + 8 * c, hb);
+          unpack8(hb, hv);
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) ss[m] += hv[e] * hv[e];
+        *reinterpret_cast<u32x4*>(xs + (long)m * K + 8 * c) = pack8(hv);
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const float v = wave_sum(ss[m]);
+      if (lane == 0) ssq[wave][m] = v;
+    }
+    __syncthreads();
+    float rs[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      float tot = 0.f;
+#pragma unroll
+      for (int v = 0; v < GV_WAVES; ++v) tot += ssq[v][m];
+      rs[m] = rsqrtf(tot / (float)K + na.eps);
+    }
+    for (int c = tid; c < nch; c += 64 * GV_WAVES) {
+      float wf[8];
+      unpack8(ld16(na.w + 8 * c), wf);
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        float hv[8];
+        unpack8(*reinterpret_cast<const u32x4*>(xs + (long)m * K + 8 * c), hv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) hv[e] = hv[e] * rs[m] * wf[e];
+        *reinterpret_cast<u32x4*>(xs + (long)m * K + 8 * c) = pack8(hv);
+      }
+    }
+    __syncthreads();
+  }
+
+  float acc[NR][M];
+#pragma unroll
+  for (int i = 0; i < NR; ++i)
+#pragma unroll
+    for (int m = 0; m < M; ++m) acc[i][m] = 0.f;
+
+  for (int j0 = 0; j0 < J; j0 += GV_U) {
+    if (j0 > 0) load_w(j0);
+#pragma unroll
+    for (int u = 0; u < GV_U; ++u) {
+      const int c = lane + 64 * (j0 + u);
+      if (j0 + u >= J || c >= nch) continue;
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        float xf[8];
+        if constexpr (NORM) unpack_bf8(*reinterpret_cast<const u32x4*>(xs + (long)m * K + 8 * c), xf);
+        else unpack_bf8(ld16(x + (long)m * ldx + 8 * c), xf);
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+          float wf[8];
+          unpack_bf8(wv[i][u], wf);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) acc[i][m] = fmaf(wf[e], xf[e], acc[i][m]);
+        }
+      }
+    }
+  }
+
+#pragma unroll
+  for (int i = 0; i < NR; ++i)
+#pragma unroll
+    for (int m = 0; m < M; ++m) acc[i][m] = wave_sum(acc[i][m]);
+  if (lane < R * M) {
+    const int i = lane / M, m = lane % M;
+    float g = 0.f, u = 0.f;
+#pragma unroll
+    for (int a = 0; a < R; ++a)
+#pragma unroll
+      for (int b = 0; b < M; ++b)
+        if (a == i && b == m) {
+          g = acc[a][b];
+          if constexpr (SWIGLU) u = acc[R + a][b];
+        }
+    if (r0 + i < N) {
+      if constexpr (SWIGLU) g = g * sigmoidf_(g) * u;
+      y[(long)m * ldy + r0 + i] = f2bf(g);
+    }
+  }
+}
+
+template <int M, bool SWIGLU, bool NORM>
+int gv_launch(const bf16_t* x, long ldx, const bf16_t* w, int N, int K, bf16_t* y, long ldy, int up_off,
+              GvNorm na, hipStream_t st) {
+  constexpr int R = SWIGLU ? 2 : 4;
+  const int blocks = (N + R * GV_WAVES - 1) / (R * GV_WAVES);
+  const size_t dyn = NORM ? (size_t)M * K * 2 : 0;
+  hipLaunchKernelGGL((gemv_kernel<M, R, SWIGLU, NORM>), dim3(blocks), dim3(64 * GV_WAVES), dyn, st, x, ldx, w, N,
+                     K, y, ldy, up_off, na);
+  KF_CHECK_LAUNCH();
+  return 0;
+}
+
+template <bool SWIGLU, bool NORM>
+int gv_dispatch(int M, const bf16_t* x, long ldx, const bf16_t* w, int N, int K, bf16_t* y, long ldy, int up_off,
+                GvNorm na, hipStream_t st) {
+  switch (M) {
+    case 1: return gv_launch<1, SWIGLU, NORM>(x, ldx, w, N, K, y, ldy, up_off, na, st);
+    case 2: return gv_launch<2, SWIGLU, NORM>(x, ldx, w, N, K, y, ldy, up_off, na, st);
+    case 3: return gv_launch<3, SWIGLU, NORM>(x, ldx, w, N, K, y, ldy, up_off, na, st);
+    case 4: return gv_launch<4, SWIGLU, NORM>(x, ldx, w, N, K, y, ldy, up_off, na, st);
+    default: return 1;
+  }
+}
+
+}  // namespace
+
+constexpr int GV_MAX_M = 4;
+constexpr long GV_NORM_LDS = 64 * 1024;
+
+// y[M, N] = x . W^T (swiglu: W = [gate; up] with up rows at +up_off, y = silu(gate) * up).
+// Optional norm prologue when nw != nullptr: x := rmsnorm(x + res) * nw, h_out = x + res.
+// Returns 1 (nothing launched) when the shape is outside the kernel's range.
+extern "C" int kf_gemv(const void* x, long ldx, int M, const void* res, const void* nw, float eps, void* h_out,
+                       long ldh, const void* w, int N, int K, void* y, long ldy, int swiglu, int up_off,
+                       hipStream_t st) {
+  if (M < 1 || M > GV_MAX_M || K % 8 != 0 || ldx % 8 != 0 || N <= 0) return 1;
+  if ((((uintptr_t)x) | ((uintptr_t)w)) & 15) return 1;
+  const bool norm = nw != nullptr;
+  if (norm && ((long)M * K * 2 > GV_NORM_LDS || (res && !h_out) || (res && (((uintptr_t)res) & 15)))) return 1;
+  const GvNorm na{(const bf16_t*)res, (const bf16_t*)nw, (bf16_t*)h_out, ldh, eps};
+  auto X = (const bf16_t*)x;
+  auto W = (const bf16_t*)w;
+  auto Y = (bf16_t*)y;
+  if (swiglu) return norm ? gv_dispatch<true, true>(M, X, ldx, W, N, K, Y, ldy, up_off, na, st)
+                          : gv_dispatch<true, false>(M, X, ldx, W, N, K, Y, ldy, up_off, na, st);
+  return norm ? gv_dispatch<false, true>(M, X, ldx, W, N, K, Y, ldy, 0, na, st)
+              : gv_dispatch<false, false>(M, X, ldx, W, N, K, Y, ldy, 0, na, st);
+}

@@ -43,7 +43,8 @@ from ..parallel.state import ParallelState, tp_all_reduce
 
 BUCKETS = (1, 2, 4, 8, 16, 32, 64, 128, 256)
 SKINNY_MAX_ROWS = 16          # decode batches up to this use the weight-streaming skinny GEMM
-SKINNY_MAX_N = 32768          # beyond this (LM head) hipBLASLt already streams at ~HBM rate
+SKINNY_MAX_N = 32768          # beyond this (LM head) hipBLASLt streams faster than the MFMA skinny kernel
+GEMV_MAX_ROWS = 4             # ... but not than the VALU GEMV (ops/csrc/gemv.hip) the 1-4 row case takes
 
 
 class Engine:
@@ -72,7 +73,11 @@ class Engine:
     # ------------------------------------------------------------------ helpers
     def _logits_full(self, y):
         m = self.m
-        logits = torch.mm(y, m.P("lm_head").t())
+        w = m.P("lm_head")
+        if y.is_cuda and y.shape[0] <= GEMV_MAX_ROWS:
+            logits = ops.skinny_gemm(y, w)      # VALU GEMV: streams the LM head faster than hipBLASLt
+        else:
+            logits = torch.mm(y, w.t())
         if m.tp > 1:
             parts = [torch.empty_like(logits) for _ in range(m.tp)]
             dist.all_gather(parts, logits, group=m.st.tp_group)
@@ -120,7 +125,8 @@ class Engine:
 
     def _mm(self, x, w):
         """Decode GEMM: the skinny weight-streaming kernel for small batches on the GPU."""
-        if x.is_cuda and x.shape[0] <= SKINNY_MAX_ROWS and w.shape[0] <= SKINNY_MAX_N and w.shape[1] % 256 == 0:
+        if x.is_cuda and (x.shape[0] <= GEMV_MAX_ROWS or (
+                x.shape[0] <= SKINNY_MAX_ROWS and w.shape[0] <= SKINNY_MAX_N and w.shape[1] % 256 == 0)):
             return ops.skinny_gemm(x, w)
         return torch.mm(x, w.t())
 
@@ -132,7 +138,7 @@ class Engine:
             s, h2 = ops.skinny_gemm_norm(h1, da, m.P(f"l{i}.norm2"), cfg.norm_eps, wgu, swiglu=True)
             return h2, self._tp_ar(self._mm(s, m.P(f"l{i}.wd")))
         mm, h2, _ = ops.rmsnorm_fwd(h1, m.P(f"l{i}.norm2"), cfg.norm_eps, residual=da)
-        if mm.is_cuda and mm.shape[0] <= SKINNY_MAX_ROWS and wgu.shape[1] % 256 == 0:
+        if mm.is_cuda and (mm.shape[0] <= GEMV_MAX_ROWS or (mm.shape[0] <= SKINNY_MAX_ROWS and wgu.shape[1] % 256 == 0)):
             s = ops.skinny_gemm(mm, wgu, swiglu=True)          # gate/up GEMM + SwiGLU in one kernel
         else:
             s = ops.swiglu_fwd(torch.mm(mm, wgu.t()))

@@ -108,6 +108,22 @@ def test_skinny_gemm(M, N, K, swiglu):
     assert torch.allclose(ops.skinny_gemm(xs, w, swiglu).float(), ops.skinny_gemm(xs.contiguous(), w, swiglu).float())
 
 
+@pytest.mark.parametrize("M,N,K,swiglu", [(1, 1000, 1792, False), (2, 4104, 520, True), (3, 16032, 4096, False),
+                                         (4, 4096, 14336, False), (1, 128256, 4096, False)])
+def test_gemv_odd_shapes(M, N, K, swiglu):
+    """The VALU decode GEMV (M <= 4): TP-shard widths (K = 1792), ragged N, LM-head size."""
+    from service_account_auth_improvements_amd import ops
+    g = torch.Generator(device="cpu").manual_seed(M * 13 + N + K)
+    x = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+    w = (torch.randn((2 * N if swiglu else N), K, generator=g) * 0.02).to(DEV, torch.bfloat16)
+    y = ops.skinny_gemm(x, w, swiglu)
+    ref = torch.mm(x.double(), w.double().t())
+    if swiglu:
+        ref = torch.nn.functional.silu(ref[:, :N]) * ref[:, N:]
+    err = ((y.double() - ref).abs().max() / ref.abs().max()).item()
+    assert y.shape == (M, N) and err < 1e-2, err
+
+
 @pytest.mark.parametrize("M,N,K,swiglu,res", [(1, 6144, 4096, False, True), (1, 14336, 4096, True, True),
                                               (4, 6144, 4096, False, False), (8, 2048, 4096, True, True)])
 def test_skinny_gemm_norm_matches_unfused(M, N, K, swiglu, res):
