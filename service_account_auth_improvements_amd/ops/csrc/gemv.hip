@@ -23,7 +23,13 @@ using namespace kf;
 namespace {
 
 constexpr int GV_WAVES = 4;       // 256-thread workgroups
-constexpr int GV_U = 4;           // chunks per row in flight per lane
+#ifndef GV_U_CFG
+#define GV_U_CFG 4
+#endif
+#ifndef GV_R_CFG
+#define GV_R_CFG 4
+#endif
+constexpr int GV_U = GV_U_CFG;    // chunks per row in flight per lane
 
 struct GvNorm {
   const bf16_t* res;   // nullable
@@ -179,7 +185,7 @@ __global__ __launch_bounds__(64 * GV_WAVES) void gemv_kernel(const bf16_t* __res
 template <int M, bool SWIGLU, bool NORM>
 int gv_launch(const bf16_t* x, long ldx, const bf16_t* w, int N, int K, bf16_t* y, long ldy, int up_off,
               GvNorm na, hipStream_t st) {
-  constexpr int R = SWIGLU ? 2 : 4;
+  constexpr int R = SWIGLU ? (GV_R_CFG > 1 ? GV_R_CFG / 2 : 1) : GV_R_CFG;
   const int blocks = (N + R * GV_WAVES - 1) / (R * GV_WAVES);
   const size_t dyn = NORM ? (size_t)M * K * 2 : 0;
   hipLaunchKernelGGL((gemv_kernel<M, R, SWIGLU, NORM>), dim3(blocks), dim3(64 * GV_WAVES), dyn, st, x, ldx, w, N,

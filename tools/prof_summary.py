@@ -14,6 +14,7 @@ def cat(n):
     if 'rmsnorm' in n or 'colsum' in n: return 'rmsnorm (HIP)'
     if 'swiglu' in n: return 'swiglu (HIP)'
     if 'rope' in n: return 'rope (HIP)'
+    if 'transpose_bf16' in n: return 'weight transpose for dX (HIP)'
     if 'embed_' in n: return 'embedding (HIP)'
     if 'ce_kernel' in n: return 'cross-entropy (HIP)'
     if 'attn_fwd' in n or 'bwd_kernel' in n or 'bwd_preprocess' in n: return 'attention (SDPA/AOTriton)'
