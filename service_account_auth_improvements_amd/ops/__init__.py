@@ -109,6 +109,25 @@ def skinny_gemm_norm(x, residual, norm_w, eps, w, swiglu: bool = False):
     return skinny_gemm(a, w, swiglu), h
 
 
+def gemv_norm_rope_ok(x, K: int, head_dim: int) -> bool:
+    """True when the fully fused decode qkv projection (norm + GEMV + RoPE + KV append) applies."""
+    return x.is_cuda and 1 <= x.shape[0] <= 4 and x.shape[0] * K * 2 <= 65536 and K % 8 == 0 and head_dim == 128
+
+
+def gemv_norm_rope(x, residual, norm_w, eps, w, Hq, cos_t, sin_t, slots, pos, k_cache, v_cache):
+    """Decode qkv projection with its neighbours fused (one GPU kernel): h = x (+ residual);
+    qkv = (rmsnorm(h) * norm_w) . w^T; RoPE at pos on the q/k heads; the rotated k and v
+    appended to the KV cache at (slots, pos).  Returns (qkv, h); equals skinny_gemm_norm +
+    attention.rope_append_ bit for bit."""
+    if x.is_cuda:
+        return _k().gemv_norm_rope(x.contiguous(), None if residual is None else residual.contiguous(), norm_w,
+                                   float(eps), w, int(Hq), cos_t, sin_t, slots, pos, k_cache, v_cache)
+    from .attention import rope_append_
+    qkv, h = skinny_gemm_norm(x, residual, norm_w, eps, w)
+    rope_append_(qkv, Hq, cos_t, sin_t, slots, pos, k_cache, v_cache)
+    return qkv, h
+
+
 def transpose_ok(w) -> bool:
     return (w.is_cuda and w.dtype == torch.bfloat16 and w.dim() == 2 and w.stride(1) == 1
             and w.shape[0] % 64 == 0 and w.shape[1] % 64 == 0 and w.stride(0) % 8 == 0

@@ -46,6 +46,9 @@ int kf_embed_bwd(const long*, const long*, const void*, void*, int, int, long, l
 int kf_skinny_gemm(const void*, long, int, const void*, int, int, void*, long, int, int, hipStream_t);
 int kf_gemv(const void*, long, int, const void*, const void*, float, void*, long, const void*, int, int, void*, long,
             int, int, hipStream_t);
+int kf_gemv_norm_rope(const void*, long, int, const void*, const void*, float, void*, long, const void*, int, int,
+                      void*, long, const float*, const float*, const int*, const int*, void*, void*, int, int, int,
+                      hipStream_t);
 int kf_skinny_gemm_norm(const void*, long, int, const void*, const void*, float, void*, long, const void*, int, int,
                         void*, long, int, int, hipStream_t);
 int kf_gemm_tn(const void*, long, const void*, long, void*, long, int, int, int, int, hipStream_t);
@@ -349,6 +352,47 @@ void rope_append_(at::Tensor& qkv, int64_t Hq, const at::Tensor& cos_t, const at
            "rope_append");
 }
 
+// Decode qkv projection, fused: h = x (+ res); qkv = (rmsnorm(h) * nw) . w^T; RoPE at pos[b] on
+// the q/k heads; rotated k and v appended to the cache at (slots[b], pos[b]).  Returns (qkv, h);
+// == skinny_gemm_norm + rope_append_ bit for bit.  1 <= B <= 4 rows, head dim 128.
+std::tuple<at::Tensor, at::Tensor> gemv_norm_rope(const at::Tensor& x, const std::optional<at::Tensor>& res,
+                                                  const at::Tensor& nw, double eps, const at::Tensor& w, int64_t Hq,
+                                                  const at::Tensor& cos_t, const at::Tensor& sin_t,
+                                                  const at::Tensor& slots, const at::Tensor& pos, at::Tensor& kc,
+                                                  at::Tensor& vc) {
+  check_bf16_cuda(x, "x");
+  check_bf16_cuda(w, "w");
+  check_bf16_cuda(nw, "norm weight");
+  const int64_t B = x.size(0), K = x.size(1), N = w.size(0), Hkv = kc.size(1), D = kc.size(3);
+  check_cache(kc, vc, Hkv, D);
+  TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && w.dim() == 2 && w.is_contiguous() && w.size(1) == K &&
+                  nw.numel() == K && nw.is_contiguous(), "gemv_norm_rope: operands");
+  TORCH_CHECK(D == 128 && N == (Hq + 2 * Hkv) * D, "gemv_norm_rope: w must be the fused [q; k; v] projection, D = 128");
+  TORCH_CHECK(B >= 1 && B <= 4 && B * K * 2 <= 64 * 1024 && K % 8 == 0, "gemv_norm_rope: 1 <= B <= 4, B*K*2 <= 64 KB");
+  TORCH_CHECK(cos_t.scalar_type() == at::kFloat && sin_t.scalar_type() == at::kFloat && cos_t.is_contiguous() &&
+                  sin_t.is_contiguous() && cos_t.size(-1) == D / 2 && cos_t.size(0) >= kc.size(2),
+              "gemv_norm_rope: cos/sin tables must be fp32 [>=Lmax, D/2]");
+  check_rows_i32(slots, B, "slots");
+  check_rows_i32(pos, B, "pos");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  at::Tensor h = x;
+  const void* rp = nullptr;
+  if (res.has_value()) {
+    check_bf16_cuda(*res, "res");
+    TORCH_CHECK(res->sizes() == x.sizes() && res->is_contiguous(), "gemv_norm_rope: res shape");
+    h = at::empty_like(x);
+    rp = res->data_ptr();
+  }
+  auto y = at::empty({B, N}, x.options());
+  check_rc(kf_gemv_norm_rope(x.data_ptr(), x.stride(0), (int)B, rp, nw.data_ptr(), (float)eps,
+                             rp ? h.data_ptr() : nullptr, h.stride(0), w.data_ptr(), (int)N, (int)K, y.data_ptr(),
+                             y.stride(0), cos_t.data_ptr<float>(), sin_t.data_ptr<float>(), slots.data_ptr<int>(),
+                             pos.data_ptr<int>(), kc.data_ptr(), vc.data_ptr(), (int)Hq, (int)Hkv, (int)kc.size(2),
+                             cur_stream()),
+           "gemv_norm_rope");
+  return {y, h};
+}
+
 // Prefill: rows [0, S) of one sequence's fused qkv -> positions [0, S) of `slot`.
 void kv_fill_(const at::Tensor& qkv, int64_t S, int64_t Hq, int64_t slot, at::Tensor& kc, at::Tensor& vc) {
   check_bf16_cuda(qkv, "qkv");
@@ -577,6 +621,8 @@ TORCH_LIBRARY(kfamd, m) {
   m.def("embed_bwd_(Tensor tok, Tensor g, Tensor(a!) dE, int vstart, bool accumulate) -> ()", &embed_bwd_);
   m.def("rope_append_(Tensor(a!) qkv, int Hq, Tensor cos, Tensor sin, Tensor slots, Tensor pos, Tensor(b!) kc, "
         "Tensor(c!) vc) -> ()", &rope_append_);
+  m.def("gemv_norm_rope(Tensor x, Tensor? res, Tensor nw, float eps, Tensor w, int Hq, Tensor cos, Tensor sin, "
+        "Tensor slots, Tensor pos, Tensor(a!) kc, Tensor(b!) vc) -> (Tensor, Tensor)", &gemv_norm_rope);
   m.def("kv_append_(Tensor qkv, int Hq, Tensor slots, Tensor pos, Tensor(a!) kc, Tensor(b!) vc) -> ()", &kv_append_);
   m.def("kv_fill_(Tensor qkv, int S, int Hq, int slot, Tensor(a!) kc, Tensor(b!) vc) -> ()", &kv_fill_);
 }

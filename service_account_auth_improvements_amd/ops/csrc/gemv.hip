@@ -39,6 +39,18 @@ struct GvNorm {
   float eps;
 };
 
+// ROPE epilogue (decode qkv projection): RoPE at pos[m] on the q/k heads and the rotated k
+// plus v written into the KV cache at (slot[m], pos[m]) -- rope_append_kernel folded in.
+struct GvRope {
+  const float* cos_t;   // [max_seq, 64]
+  const float* sin_t;
+  const int* slots;
+  const int* pos;
+  bf16_t* kc;           // [n_slots, Hkv, Lmax, 128]
+  bf16_t* vc;
+  int hq, hkv, lmax;
+};
+
 __device__ __forceinline__ void unpack_bf8(const u32x4& v, float* f) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -47,24 +59,31 @@ __device__ __forceinline__ void unpack_bf8(const u32x4& v, float* f) {
   }
 }
 
-template <int M, int R, bool SWIGLU, bool NORM>
+template <int M, int R, bool SWIGLU, bool NORM, bool ROPE = false>
 __global__ __launch_bounds__(64 * GV_WAVES) void gemv_kernel(const bf16_t* __restrict__ x, long ldx,
                                                             const bf16_t* __restrict__ w, int N, int K,
                                                             bf16_t* __restrict__ y, long ldy, int up_off,
-                                                            GvNorm na) {
+                                                            GvNorm na, GvRope ra) {
+  static_assert(!ROPE || (R == 4 && !SWIGLU), "rope epilogue: 4 rows = two rotation pairs per wave");
   extern __shared__ __attribute__((aligned(16))) bf16_t xs[];   // NORM: M x K normalised rows
   __shared__ float ssq[GV_WAVES][M];
   constexpr int NR = SWIGLU ? 2 * R : R;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int r0 = (blockIdx.x * GV_WAVES + wave) * R;
+  const int gw = blockIdx.x * GV_WAVES + wave;
+  // ROPE: wave gw owns rotation pairs (p, p + 64) and (p + 1, p + 65) of head gw / 32
+  const int r0 = ROPE ? (gw >> 5) * 128 + (gw & 31) * 2 : gw * R;
   const int nch = K >> 3;                       // 16-byte chunks per row
   const int J = (nch + 63) >> 6;                // chunk slots per lane
 
+  auto row_of = [&](int i) -> int {
+    if constexpr (ROPE) return r0 + (i & 1) + (i >> 1) * 64;
+    return i < R ? r0 + i : r0 + (i - R);
+  };
   auto row_ptr = [&](int i) -> const bf16_t* {
-    const int rr = i < R ? r0 + i : r0 + (i - R) + up_off;
+    const int rr = (SWIGLU && i >= R) ? r0 + (i - R) + up_off : row_of(i);
     return w + (long)rr * K + 8 * lane;
   };
-  auto row_ok = [&](int i) { return r0 + (i < R ? i : i - R) < N; };
+  auto row_ok = [&](int i) { return row_of(i) < N; };
 
   u32x4 wv[NR][GV_U];
   auto load_w = [&](int j0) {
@@ -174,10 +193,29 @@ __global__ __launch_bounds__(64 * GV_WAVES) void gemv_kernel(const bf16_t* __res
         if (a == i && b == m) {
           g = acc[a][b];
           if constexpr (SWIGLU) u = acc[R + a][b];
+          if constexpr (ROPE) u = acc[a ^ 2][b];   // the other half of the rotation pair
         }
-    if (r0 + i < N) {
+    const int row = row_of(i);
+    if (row < N) {
       if constexpr (SWIGLU) g = g * sigmoidf_(g) * u;
-      y[(long)m * ldy + r0 + i] = f2bf(g);
+      if constexpr (ROPE) {
+        // same arithmetic as rope_append_kernel on the bf16 GEMM output
+        const int head = row >> 7, d = row & 127, pr = d & 63, ps = ra.pos[m];
+        float v = bf2f(f2bf(g));
+        if (head < ra.hq + ra.hkv) {
+          const float o = bf2f(f2bf(u)), c = ra.cos_t[(long)ps * 64 + pr], sn = ra.sin_t[(long)ps * 64 + pr];
+          v = d < 64 ? v * c - o * sn : v * c + o * sn;
+        }
+        const bf16_t vb = f2bf(v);
+        y[(long)m * ldy + row] = vb;
+        if (head >= ra.hq) {
+          const bool is_v = head >= ra.hq + ra.hkv;
+          const int kh = is_v ? head - ra.hq - ra.hkv : head - ra.hq;
+          (is_v ? ra.vc : ra.kc)[(((long)ra.slots[m] * ra.hkv + kh) * ra.lmax + ps) * 128 + d] = vb;
+        }
+      } else {
+        y[(long)m * ldy + row] = f2bf(g);
+      }
     }
   }
 }
@@ -189,7 +227,7 @@ int gv_launch(const bf16_t* x, long ldx, const bf16_t* w, int N, int K, bf16_t* 
   const int blocks = (N + R * GV_WAVES - 1) / (R * GV_WAVES);
   const size_t dyn = NORM ? (size_t)M * K * 2 : 0;
   hipLaunchKernelGGL((gemv_kernel<M, R, SWIGLU, NORM>), dim3(blocks), dim3(64 * GV_WAVES), dyn, st, x, ldx, w, N,
-                     K, y, ldy, up_off, na);
+                     K, y, ldy, up_off, na, GvRope{});
   KF_CHECK_LAUNCH();
   return 0;
 }
@@ -204,6 +242,16 @@ int gv_dispatch(int M, const bf16_t* x, long ldx, const bf16_t* w, int N, int K,
     case 4: return gv_launch<4, SWIGLU, NORM>(x, ldx, w, N, K, y, ldy, up_off, na, st);
     default: return 1;
   }
+}
+
+template <int M>
+int gv_rope_launch(const bf16_t* x, long ldx, const bf16_t* w, int N, int K, bf16_t* y, long ldy, GvNorm na,
+                   GvRope ra, hipStream_t st) {
+  const int blocks = N / (4 * GV_WAVES);
+  hipLaunchKernelGGL((gemv_kernel<M, 4, false, true, true>), dim3(blocks), dim3(64 * GV_WAVES), (size_t)M * K * 2,
+                     st, x, ldx, w, N, K, y, ldy, 0, na, ra);
+  KF_CHECK_LAUNCH();
+  return 0;
 }
 
 }  // namespace
@@ -229,4 +277,27 @@ extern "C" int kf_gemv(const void* x, long ldx, int M, const void* res, const vo
                           : gv_dispatch<true, false>(M, X, ldx, W, N, K, Y, ldy, up_off, na, st);
   return norm ? gv_dispatch<false, true>(M, X, ldx, W, N, K, Y, ldy, 0, na, st)
               : gv_dispatch<false, false>(M, X, ldx, W, N, K, Y, ldy, 0, na, st);
+}
+
+// Decode qkv projection with everything around it fused: h = x + res, rmsnorm(h) * nw as the
+// X operand, Y = X . Wqkv^T, RoPE at pos[m] on the q/k heads (fp32 cos/sin [max_seq, 64]),
+// and the rotated k plus v stored into the KV cache at (slots[m], pos[m]).  Head dim 128.
+extern "C" int kf_gemv_norm_rope(const void* x, long ldx, int M, const void* res, const void* nw, float eps,
+                                 void* h_out, long ldh, const void* w, int N, int K, void* y, long ldy,
+                                 const float* cos_t, const float* sin_t, const int* slots, const int* pos, void* kc,
+                                 void* vc, int hq, int hkv, int lmax, hipStream_t st) {
+  if (M < 1 || M > GV_MAX_M || K % 8 != 0 || ldx % 8 != 0 || (long)M * K * 2 > GV_NORM_LDS) return 1;
+  if (N != (hq + 2 * hkv) * 128 || (res && !h_out)) return 1;
+  if ((((uintptr_t)x) | ((uintptr_t)w) | ((uintptr_t)res)) & 15) return 1;
+  const GvNorm na{(const bf16_t*)res, (const bf16_t*)nw, (bf16_t*)h_out, ldh, eps};
+  const GvRope ra{cos_t, sin_t, slots, pos, (bf16_t*)kc, (bf16_t*)vc, hq, hkv, lmax};
+  auto X = (const bf16_t*)x;
+  auto W = (const bf16_t*)w;
+  auto Y = (bf16_t*)y;
+  switch (M) {
+    case 1: return gv_rope_launch<1>(X, ldx, W, N, K, Y, ldy, na, ra, st);
+    case 2: return gv_rope_launch<2>(X, ldx, W, N, K, Y, ldy, na, ra, st);
+    case 3: return gv_rope_launch<3>(X, ldx, W, N, K, Y, ldy, na, ra, st);
+    default: return gv_rope_launch<4>(X, ldx, W, N, K, Y, ldy, na, ra, st);
+  }
 }

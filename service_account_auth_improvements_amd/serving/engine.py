@@ -150,12 +150,17 @@ class Engine:
         d = None
         for li, i in enumerate(m.layers):
             wqkv = m.P(f"l{i}.wqkv")
-            if ops.skinny_gemm_norm_ok(r, wqkv.shape[1]):
-                qkv, h1 = ops.skinny_gemm_norm(r, d, m.P(f"l{i}.norm1"), cfg.norm_eps, wqkv)
+            if ops.gemv_norm_rope_ok(r, wqkv.shape[1], cfg.head_dim):
+                # residual add + RMSNorm + qkv GEMV + RoPE + KV-cache append: one kernel
+                qkv, h1 = ops.gemv_norm_rope(r, d, m.P(f"l{i}.norm1"), cfg.norm_eps, wqkv, m.hq, m.cos, m.sin,
+                                             slots, pos, self.kc[li], self.vc[li])
             else:
-                a, h1, _ = ops.rmsnorm_fwd(r, m.P(f"l{i}.norm1"), cfg.norm_eps, residual=d)
-                qkv = self._mm(a, wqkv)
-            rope_append_(qkv, m.hq, m.cos, m.sin, slots, pos, self.kc[li], self.vc[li])
+                if ops.skinny_gemm_norm_ok(r, wqkv.shape[1]):
+                    qkv, h1 = ops.skinny_gemm_norm(r, d, m.P(f"l{i}.norm1"), cfg.norm_eps, wqkv)
+                else:
+                    a, h1, _ = ops.rmsnorm_fwd(r, m.P(f"l{i}.norm1"), cfg.norm_eps, residual=d)
+                    qkv = self._mm(a, wqkv)
+                rope_append_(qkv, m.hq, m.cos, m.sin, slots, pos, self.kc[li], self.vc[li])
             o = decode_attention(qkv, self.kc[li], self.vc[li], slots, lengths, m.hq)
             da = self._tp_ar(self._mm(o, m.P(f"l{i}.wo")))
             r, d = self._decode_mlp(i, h1, da)

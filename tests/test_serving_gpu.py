@@ -142,6 +142,34 @@ def test_skinny_gemm_norm_matches_unfused(M, N, K, swiglu, res):
     assert y.shape == (M, N) and err < 1e-2, err
 
 
+@pytest.mark.parametrize("B,res", [(1, True), (2, False), (4, True)])
+def test_gemv_norm_rope_matches_unfused(B, res):
+    """Fused decode qkv projection (norm + GEMV + RoPE + KV append) == skinny_gemm_norm +
+    rope_append_, bit for bit (qkv rows, residual stream and both caches)."""
+    from service_account_auth_improvements_amd import ops
+    from service_account_auth_improvements_amd.ops import reference
+    from service_account_auth_improvements_amd.ops.attention import rope_append_
+    Hq, Hkv, K, Lmax = 32, 8, 4096, 256
+    g = torch.Generator(device="cpu").manual_seed(B * 5 + res)
+    x = torch.randn(B, K, generator=g).to(DEV, torch.bfloat16)
+    r = torch.randn(B, K, generator=g).to(DEV, torch.bfloat16) if res else None
+    nw = (1 + 0.1 * torch.randn(K, generator=g)).to(DEV, torch.bfloat16)
+    w = (torch.randn((Hq + 2 * Hkv) * 128, K, generator=g) * 0.02).to(DEV, torch.bfloat16)
+    cos, sin = (t.to(DEV) for t in reference.rope_tables(Lmax, 128))
+    slots = torch.tensor([3, 0, 5, 1][:B], dtype=torch.int32, device=DEV)
+    pos = torch.tensor([17, 255, 0, 100][:B], dtype=torch.int32, device=DEV)
+    kc = torch.zeros(6, Hkv, Lmax, 128, dtype=torch.bfloat16, device=DEV)
+    vc = torch.zeros_like(kc)
+    kc2, vc2 = kc.clone(), vc.clone()
+    qkv, h = ops.gemv_norm_rope(x, r, nw, 1e-5, w, Hq, cos, sin, slots, pos, kc, vc)
+    q_ref, h_ref = ops.skinny_gemm_norm(x, r, nw, 1e-5, w)
+    rope_append_(q_ref, Hq, cos, sin, slots, pos, kc2, vc2)
+    assert torch.equal(h, h_ref)
+    assert torch.equal(qkv, q_ref)
+    assert torch.equal(kc, kc2) and torch.equal(vc, vc2)
+    assert kc.abs().sum() > 0 and vc.abs().sum() > 0
+
+
 def test_rope_append_matches_reference():
     from service_account_auth_improvements_amd.ops import reference
     from service_account_auth_improvements_amd.ops.attention import rope_append_
