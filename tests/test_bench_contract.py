@@ -1,0 +1,55 @@
+"""bench.py driver contract on the CPU (tiny model): one JSON line from rank 0 with the
+required keys, 1 process and 2 processes under torch.distributed.run (gloo, 127.0.0.1)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config"}
+ARGS = ["--model", "tiny", "--seq-len", "64", "--micro-batch", "1", "--steps", "2", "--warmup", "1"]
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _json_lines(out):
+    return [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+
+
+def _check(rec, n):
+    assert KEYS <= set(rec), KEYS - set(rec)
+    assert rec["n_gpus"] == n and rec["steps"] == 2 and rec["warmup"] == 1
+    assert rec["value"] > 0 and rec["ms_per_step"] > 0 and rec["higher_is_better"] is True
+    assert rec["scaling"] == "weak" and rec["dtype"] == "bf16"
+    assert rec["config"]["global_batch"] == n and rec["config"]["parallelism"] == f"dp{n}"
+    assert rec["metric"].startswith("tokens/sec PyTorchJob Llama-3-8B DDP")
+
+
+def test_bench_single_process_json():
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *ARGS], capture_output=True, text=True,
+                       timeout=300, env=env, cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-2000:]
+    recs = _json_lines(r.stdout)
+    assert len(recs) == 1
+    _check(recs[0], 1)
+
+
+def test_bench_two_ranks_torchrun_json():
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2", *ARGS]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-2000:]
+    recs = _json_lines(r.stdout)
+    assert len(recs) == 1, r.stdout          # rank 0 only
+    _check(recs[0], 2)
+    assert recs[0]["config"]["optimizer_sharding"] == "zero1"
