@@ -38,14 +38,32 @@ def stage_layers(n_layers: int, pp: int, rank: int) -> range:
 class P2P:
     def __init__(self, st: ParallelState, shape, dtype, device):
         self.st, self.shape, self.dtype, self.device = st, shape, dtype, device
+        # gloo (the one-GPU rehearsal backend) moves send/recv payloads without ordering them
+        # against the HIP stream, so GPU tensors are staged through host memory there; RCCL
+        # orders its own stream against the compute stream.
+        self._host = torch.device(device).type == "cuda" and dist.get_backend() == "gloo"
 
     def _buf(self):
         return torch.empty(self.shape, dtype=self.dtype, device=self.device)
 
     def _run(self, ops):
-        if ops:
-            for r in dist.batch_isend_irecv(ops):
-                r.wait()
+        if not ops:
+            return
+        copies = []
+        if self._host:
+            staged = []
+            for op in ops:
+                if op.op is dist.isend:
+                    staged.append(dist.P2POp(dist.isend, op.tensor.cpu(), op.peer))
+                else:
+                    h = torch.empty(op.tensor.shape, dtype=op.tensor.dtype)
+                    copies.append((op.tensor, h))
+                    staged.append(dist.P2POp(dist.irecv, h, op.peer))
+            ops = staged
+        for r in dist.batch_isend_irecv(ops):
+            r.wait()
+        for dev_t, h in copies:
+            dev_t.copy_(h)
 
     def recv_forward(self):
         if self.st.pp_prev is None:

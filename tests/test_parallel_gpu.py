@@ -70,3 +70,77 @@ def test_ddp_two_ranks_one_gpu_matches_single_process(zero1):
         assert rel < 2e-2, rel
     if zero1:   # the two shards tile the buffer
         assert bool((~torch.isnan(g0) | ~torch.isnan(g1)).all())
+
+
+def _tp_body(rank, world, clip):
+    import os
+
+    os.environ["KFAMD_DIST_BACKEND"] = "gloo"
+    from service_account_auth_improvements_amd.parallel.state import init_distributed
+    from service_account_auth_improvements_amd.runtime.trainer import TrainConfig, Trainer
+
+    st = init_distributed(tp=world, pp=1, device="cuda")
+    tr = Trainer(TrainConfig(model="small", seq_len=256, micro_batch=2, n_layers=2, lr=1e-3, max_grad_norm=clip), st,
+                 full_init=True)
+    losses = [float(tr.train_step([(x.to(st.device), y.to(st.device))]))
+              for x, y in _batches(tr.mcfg.vocab_size, 2, seed=11)]
+    torch.cuda.synchronize()
+    return losses, tr.model.norms.params.float().cpu()
+
+
+def test_tensor_parallel_two_ranks_one_gpu_matches_tp1():
+    """Megatron TP=2 on the GPU kernels (sharded GEMMs and transposes, vocab-parallel CE,
+    TP-aware clipping) == TP=1, two full AdamW steps with clipping active."""
+    from service_account_auth_improvements_amd.parallel.state import ParallelState
+    from service_account_auth_improvements_amd.runtime.trainer import TrainConfig, Trainer
+
+    clip = 0.05
+    res = run_ranks(_tp_body, world=2, args=(clip,), timeout=300)
+    st = ParallelState(device=torch.device("cuda", 0))
+    tr = Trainer(TrainConfig(model="small", seq_len=256, micro_batch=2, n_layers=2, lr=1e-3, max_grad_norm=clip), st,
+                 full_init=True)
+    ref = [float(tr.train_step([(x.to(st.device), y.to(st.device))]))
+           for x, y in _batches(tr.mcfg.vocab_size, 2, seed=11)]
+    for losses, _ in res:
+        assert abs(losses[0] - ref[0]) < 1e-2 * ref[0] and abs(losses[1] - ref[1]) < 2e-2 * ref[1], (losses, ref)
+    assert torch.equal(res[0][1], res[1][1])
+    norms = tr.model.norms.params.float().cpu()
+    assert ((res[0][1] - norms).abs().max() / norms.abs().max()).item() < 1e-2
+
+
+def _pp_body(rank, world, n_micro):
+    import os
+
+    os.environ["KFAMD_DIST_BACKEND"] = "gloo"
+    from service_account_auth_improvements_amd.parallel.pipeline import PipelineTrainer
+    from service_account_auth_improvements_amd.parallel.state import init_distributed
+    from service_account_auth_improvements_amd.runtime.trainer import TrainConfig
+
+    st = init_distributed(tp=1, pp=world, device="cuda")
+    tr = PipelineTrainer(TrainConfig(model="small", seq_len=256, lr=0.0, micro_batch=2, n_layers=4), st)
+    mbs = [(x.to(st.device), y.to(st.device)) for x, y in _batches(tr.mcfg.vocab_size, n_micro, seed=5)]
+    loss = tr.train_step(mbs)
+    torch.cuda.synchronize()
+    grads = {s.name: tr.model.G(s.name).float().cpu() for g in tr.model.groups for s in g.specs}
+    return (float(loss) if loss is not None else None), grads
+
+
+def test_pipeline_two_stages_one_gpu_matches_single_stage():
+    """1F1B over 2 stages (activations / gradients sent between the ranks) == one stage."""
+    from service_account_auth_improvements_amd.parallel.state import ParallelState
+    from service_account_auth_improvements_amd.runtime.trainer import TrainConfig, Trainer
+
+    n_micro = 3
+    st = ParallelState(device=torch.device("cuda", 0))
+    ref = Trainer(TrainConfig(model="small", seq_len=256, lr=0.0, micro_batch=2, n_layers=4), st)
+    mbs = [(x.to(st.device), y.to(st.device)) for x, y in _batches(ref.mcfg.vocab_size, n_micro, seed=5)]
+    ref_loss = float(ref.train_step(mbs))
+    res = run_ranks(_pp_body, world=2, args=(n_micro,), timeout=300)
+    assert res[0][0] is None and abs(res[1][0] - ref_loss) < 5e-3 * ref_loss
+    seen = set()
+    for _, grads in res:
+        for name, g in grads.items():
+            r = ref.model.G(name).float().cpu()
+            assert ((g - r).abs().max() / r.abs().max().clamp_min(1e-12)).item() < 3e-2, name
+            seen.add(name)
+    assert seen == {s.name for g in ref.model.groups for s in g.specs}
