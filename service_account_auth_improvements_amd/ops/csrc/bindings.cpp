@@ -5,6 +5,7 @@
 // HIP stream, allocates scratch through the caching allocator (capturable in hipGraphs)
 // and validates shapes/dtypes on the host BEFORE any kernel is launched: a kernel is
 // never started on operands whose shape it does not support.
+#include <cstdlib>
 #include <torch/library.h>
 #include <ATen/ATen.h>
 #include <c10/hip/HIPStream.h>
@@ -305,7 +306,11 @@ at::Tensor decode_attn(const at::Tensor& q2d, const at::Tensor& kc, const at::Te
   check_rows_i32(slots, B, "slots");
   check_rows_i32(lengths, B, "lengths");
   c10::hip::HIPGuardMasqueradingAsCUDA g(q2d.device());
-  const int splits = kf_decode_splits((int)B, (int)Hkv, (int)Lmax);
+  static const int splits_env = [] {
+    const char* v = std::getenv("KFAMD_DECODE_SPLITS");   // tuning override (tools/bench_decode_splits.py)
+    return v ? std::atoi(v) : 0;
+  }();
+  const int splits = splits_env > 0 ? splits_env : kf_decode_splits((int)B, (int)Hkv, (int)Lmax);
   auto f32 = q2d.options().dtype(at::kFloat);
   auto po = at::empty({B * Hq * splits * D}, f32);
   auto pml = at::empty({B * Hq * splits * 2}, f32);
