@@ -7,8 +7,9 @@
 // MFMA skinny kernel (skinny_gemm.hip) has to give each lane (row l%16, k-chunk l/16) and so
 // touches 16 rows x 64 B per instruction; it stays the path for 5 <= M <= 64.
 //
-//  * VALU dot products: 8 bf16 of W unpacked by shift/mask, fp32 FMAs with X, R x M
-//    partial sums per lane, one wave reduction per (row, x-row) at the end.  X chunks are
+//  * VALU dot products on the packed bf16 pairs (v_dot2c_f32_bf16, fp32 accumulate): no
+//    unpacking of W or X (vs unpack + fp32 FMAs: equal at M = 1, 10-20 % faster at M = 4).
+//    R x M partial sums per lane, one wave reduction per (row, x-row) at the end.  X chunks are
 //    shared by the R rows of the wave (read once per chunk from L1/L2, or from LDS when
 //    the norm prologue staged them).
 //  * SWIGLU: the wave's R gate rows n.. and the matching up rows n + up_off.. are streamed
@@ -30,6 +31,11 @@ constexpr int GV_WAVES = 4;       // 256-thread workgroups
 #define GV_R_CFG 4
 #endif
 constexpr int GV_U = GV_U_CFG;    // chunks per row in flight per lane
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+// acc + a.lo * b.lo + a.hi * b.hi for packed bf16 pairs (v_dot2c_f32_bf16)
+__device__ __forceinline__ float dot2_bf16(uint32_t a, uint32_t b, float acc) {
+  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, a), __builtin_bit_cast(bf16x2_t, b), acc, false);
+}
 
 struct GvNorm {
   const bf16_t* res;   // nullable
@@ -50,14 +56,6 @@ struct GvRope {
   bf16_t* vc;
   int hq, hkv, lmax;
 };
-
-__device__ __forceinline__ void unpack_bf8(const u32x4& v, float* f) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    f[2 * i] = __uint_as_float(v[i] << 16);
-    f[2 * i + 1] = __uint_as_float(v[i] & 0xffff0000u);
-  }
-}
 
 template <int M, int R, bool SWIGLU, bool NORM, bool ROPE = false>
 __global__ __launch_bounds__(64 * GV_WAVES) void gemv_kernel(const bf16_t* __restrict__ x, long ldx,
@@ -165,15 +163,16 @@ __global__ __launch_bounds__(64 * GV_WAVES) void gemv_kernel(const bf16_t* __res
       if (j0 + u >= J || c >= nch) continue;
 #pragma unroll
       for (int m = 0; m < M; ++m) {
-        float xf[8];
-        if constexpr (NORM) unpack_bf8(*reinterpret_cast<const u32x4*>(xs + (long)m * K + 8 * c), xf);
-        else unpack_bf8(ld16(x + (long)m * ldx + 8 * c), xf);
+        const u32x4 xv = NORM ? *reinterpret_cast<const u32x4*>(xs + (long)m * K + 8 * c)
+                              : ld16(x + (long)m * ldx + 8 * c);
+        // packed bf16 pairs straight into v_dot2c_f32_bf16: no unpacking of W or X
 #pragma unroll
         for (int i = 0; i < NR; ++i) {
-          float wf[8];
-          unpack_bf8(wv[i][u], wf);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) acc[i][m] = fmaf(wf[e], xf[e], acc[i][m]);
+          const u32x4 wq = wv[i][u];
+          acc[i][m] = dot2_bf16(wq.x, xv.x, acc[i][m]);
+          acc[i][m] = dot2_bf16(wq.y, xv.y, acc[i][m]);
+          acc[i][m] = dot2_bf16(wq.z, xv.z, acc[i][m]);
+          acc[i][m] = dot2_bf16(wq.w, xv.w, acc[i][m]);
         }
       }
     }
