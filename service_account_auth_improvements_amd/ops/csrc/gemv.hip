@@ -9,7 +9,8 @@
 //
 //  * VALU dot products on the packed bf16 pairs (v_dot2c_f32_bf16, fp32 accumulate): no
 //    unpacking of W or X (vs unpack + fp32 FMAs: equal at M = 1, 10-20 % faster at M = 4).
-//    R x M partial sums per lane, one wave reduction per (row, x-row) at the end.  X chunks are
+//    R x M partial sums per lane, one wave reduction per (row, x-row) at the end.  At M = 8
+//    the MFMA skinny kernel wins again (gate/up 52 vs 56 us, wd 30 vs 38 us), hence M <= 4.  X chunks are
 //    shared by the R rows of the wave (read once per chunk from L1/L2, or from LDS when
 //    the norm prologue staged them).
 //  * SWIGLU: the wave's R gate rows n.. and the matching up rows n + up_off.. are streamed
