@@ -54,6 +54,8 @@ def main():
     ap.add_argument("--attn", default="hip", choices=["hip", "sdpa"])
     ap.add_argument("--tp", type=int, default=1, help="tensor parallel degree (configs[4]: 70B TP=8)")
     ap.add_argument("--pp", type=int, default=1, help="pipeline parallel degree (1F1B)")
+    ap.add_argument("--recompute", action="store_true",
+                    help="per-layer activation recomputation (memory plans that need it, e.g. 70B at long S)")
     ap.add_argument("--layers", type=int, default=None, help="DEBUG ONLY: invalid for reporting")
     ap.add_argument("--json-out", default=None)
     a = ap.parse_args()
@@ -67,7 +69,7 @@ def main():
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     tcfg = TrainConfig(model=a.model, seq_len=a.seq_len, micro_batch=a.micro_batch,
                        grad_accum=a.grad_accum, zero1=a.zero1, bucket_mb=a.bucket_mb,
-                       n_layers=a.layers)
+                       n_layers=a.layers, recompute=a.recompute)
     t0 = time.time()
     if a.pp > 1:
         from service_account_auth_improvements_amd.parallel.pipeline import PipelineTrainer
@@ -136,6 +138,7 @@ def main():
                 "grad_accum": a.grad_accum,
                 "n_layers": tr.mcfg.n_layers,
                 "attention": a.attn,
+                "activation_recompute": a.recompute,
             },
             "tokens_per_s_per_gpu": round(value / world, 1),
             "model_tflops_per_gpu": round(value / world * flops_tok / 1e12, 1),

@@ -139,6 +139,10 @@ class Llama:
         # ZeRO-1 overlap: called with (group, lo, hi) before a parameter range is first
         # read in forward, so the async all-gather of that range can be waited on lazily
         self.param_wait: Optional[Callable[[FlatGroup, int, int], None]] = None
+        # activation recomputation: keep only each layer's input (r, d) from the forward and
+        # re-run the layer's forward right before its backward (memory plans where the saved
+        # activations do not fit: 70B at long sequence / larger micro-batch)
+        self.recompute = False
         cos, sin = ops.rope_tables(cfg.max_seq, D, cfg.rope_theta)
         self.cos = cos.to(self.device)
         self.sin = sin.to(self.device)
@@ -363,8 +367,13 @@ class Llama:
             r, d = inp, None
         for i in self.layers:
             self._wait_layer(i)
-            r, d, c = self.layer_fwd(i, r, d, B, S)
-            ctx["layers"].append(c)
+            if self.recompute:
+                inp = (r, d)
+                r, d, _ = self.layer_fwd(i, r, d, B, S)
+                ctx["layers"].append(inp)
+            else:
+                r, d, c = self.layer_fwd(i, r, d, B, S)
+                ctx["layers"].append(c)
         if self.last:
             self._wait("lm_head", "lm_head")
             self._wait("final_norm", "final_norm", self.norms)
@@ -384,6 +393,10 @@ class Llama:
         layers = ctx["layers"]
         for i in reversed(self.layers):
             c = layers.pop()
+            if self.recompute:
+                r, d = c
+                _, _, c = self.layer_fwd(i, r, d, B, S)   # same kernels, same inputs: same values
+                del r, d
             g = self.layer_bwd(i, c, g, B, S, accumulate)
             del c
         if self.first:

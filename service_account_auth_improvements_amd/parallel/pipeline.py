@@ -173,6 +173,7 @@ class PipelineTrainer:
         self.mcfg = mcfg
         lr = stage_layers(mcfg.n_layers, st.pp, st.pp_rank)
         self.model = Llama(mcfg, st, layer_range=lr, seed=tcfg.seed, full_init=full_init)
+        self.model.recompute = tcfg.recompute
         self.model.allocate()
         self.reducer = GradReducer(self.model.groups, st.dp_group, st.dp,
                                    bucket_bytes=tcfg.bucket_mb << 20)

@@ -38,6 +38,7 @@ class TrainConfig:
     max_grad_norm: float = 1.0
     seed: int = 1234
     n_layers: Optional[int] = None   # override (tests only; benches must use the full model)
+    recompute: bool = False          # per-layer activation recomputation (memory for compute)
 
 
 class Trainer:
@@ -54,6 +55,7 @@ class Trainer:
         assert self.st.pp == 1, "use parallel.pipeline.PipelineTrainer for pp > 1"
         t0 = time.time()
         self.model = Llama(mcfg, self.st, seed=tcfg.seed, full_init=full_init)
+        self.model.recompute = tcfg.recompute
         self.model.allocate(pad_to=self.st.dp * 64 if tcfg.zero1 else 1)
         self._sync()
         self.init_times = {"params_alloc_init_s": time.time() - t0}

@@ -47,3 +47,21 @@ def test_param_count_llama3_8b():
     assert abs(cfg.num_params() - 8.03e9) / 8.03e9 < 0.01
     cfg70 = LlamaConfig.preset("llama3-70b")
     assert abs(cfg70.num_params() - 70.6e9) / 70.6e9 < 0.01
+
+
+def test_activation_recompute_matches_saved_activations():
+    """recompute=True (only layer inputs kept, layer forward re-run before its backward)
+    gives bit-identical losses, gradients and updated parameters."""
+    from service_account_auth_improvements_amd.parallel.state import ParallelState
+    from service_account_auth_improvements_amd.runtime.trainer import TrainConfig, Trainer
+    out = []
+    for rc in (False, True):
+        tr = Trainer(TrainConfig(model="tiny", seq_len=32, micro_batch=2, lr=1e-3, recompute=rc), ParallelState())
+        assert tr.model.recompute == rc
+        g = torch.Generator().manual_seed(3)
+        mbs = [(torch.randint(0, tr.mcfg.vocab_size, (2, 32), generator=g),
+                torch.randint(0, tr.mcfg.vocab_size, (2, 32), generator=g)) for _ in range(2)]
+        losses = [float(tr.train_step(mbs)) for _ in range(2)]
+        out.append((losses, tr.model.mats.params.clone(), tr.model.mats.grads.clone()))
+    assert out[0][0] == out[1][0]
+    assert torch.equal(out[0][1], out[1][1]) and torch.equal(out[0][2], out[1][2])

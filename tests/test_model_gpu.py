@@ -53,3 +53,16 @@ def test_async_optimizer_is_bit_identical():
         out.append((losses, tr.model.mats.params.clone(), tr.model.norms.params.clone()))
     assert out[0][0] == out[1][0]
     assert torch.equal(out[0][1], out[1][1]) and torch.equal(out[0][2], out[1][2])
+
+
+def test_activation_recompute_bit_identical_gpu():
+    """Per-layer recomputation on the GPU kernels: same loss, gradients and parameters."""
+    out = []
+    for rc in (False, True):
+        st = ParallelState(device=torch.device("cuda", 0))
+        tr = Trainer(TrainConfig(model="small", seq_len=256, micro_batch=2, n_layers=2, recompute=rc), st)
+        data = SyntheticData(tr.mcfg.vocab_size, 2, 256, "cuda:0", seed=4)
+        losses = [float(tr.train_step([data.next()])) for _ in range(2)]
+        out.append((losses, tr.model.mats.params.clone(), tr.model.mats.grads.clone()))
+    assert out[0][0] == out[1][0]
+    assert torch.equal(out[0][1], out[1][1]) and torch.equal(out[0][2], out[1][2])
