@@ -30,12 +30,13 @@ from ..runtime.flat import FlatGroup
 
 
 class Bucket:
-    __slots__ = ("group", "lo", "hi", "work", "launched")
+    __slots__ = ("group", "lo", "hi", "work", "launched", "staged")
 
     def __init__(self, group: FlatGroup, lo: int, hi: int):
         self.group, self.lo, self.hi = group, lo, hi
         self.work = None
         self.launched = False
+        self.staged = None      # (shard view, separate output) when the backend must not alias
 
 
 class GradReducer:
@@ -89,6 +90,11 @@ class GradReducer:
             n = (b.hi - b.lo) // self.dp
             r = dist.get_rank(self.dp_group) if self.dp_group is not None else dist.get_rank()
             out = x[r * n:(r + 1) * n]
+            if x.is_cuda and dist.get_backend(self.dp_group) == "gloo":
+                # in-place reduce-scatter (output = input + rank * n) is an RCCL/NCCL contract;
+                # the gloo rehearsal backend gets a separate output, copied back in finish()
+                b.staged = (out, torch.empty_like(out))
+                out = b.staged[1]
             b.work = dist.reduce_scatter_tensor(out, x, group=self.dp_group, async_op=True)
         self._pending.append(b)
 
@@ -110,6 +116,9 @@ class GradReducer:
         for b in self._pending:
             if b.work is not None:
                 b.work.wait()
+            if b.staged is not None:
+                b.staged[0].copy_(b.staged[1])
+                b.staged = None
         self._pending = []
 
     def all_gather_params(self, overlap: bool = False):
