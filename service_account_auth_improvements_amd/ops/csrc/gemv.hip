@@ -9,10 +9,12 @@
 //
 //  * VALU dot products on the packed bf16 pairs (v_dot2c_f32_bf16, fp32 accumulate): no
 //    unpacking of W or X (vs unpack + fp32 FMAs: equal at M = 1, 10-20 % faster at M = 4).
-//    R x M partial sums per lane, one wave reduction per (row, x-row) at the end.  At M = 8
-//    the MFMA skinny kernel wins again (gate/up 52 vs 56 us, wd 30 vs 38 us), hence M <= 4.  X chunks are
-//    shared by the R rows of the wave (read once per chunk from L1/L2, or from LDS when
-//    the norm prologue staged them).
+//    R x M partial sums per lane, one wave reduction per (row, x-row) at the end.  X chunks
+//    are shared by the R rows of the wave (read once per chunk from L1/L2, or from LDS when
+//    the norm prologue staged them).  At M = 8 the MFMA skinny kernel wins again (gate/up
+//    52 vs 56 us, wd 30 vs 38 us: X re-reads and VALU work grow with M), hence M <= 4.
+//  * Tuning knobs GV_U_CFG / GV_R_CFG (chunks in flight, rows per wave): a sweep of
+//    R in {1, 2, 4, 8} x U in {2, 4, 8} (tools/kbench/gemv_bench.hip) kept R = 4, U = 4.
 //  * SWIGLU: the wave's R gate rows n.. and the matching up rows n + up_off.. are streamed
 //    together and the wave writes silu(gate) * up.
 //  * NORM prologue (decode layer norms fused in, as in skinny_gemm.hip): each workgroup
