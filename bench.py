@@ -154,6 +154,10 @@ def main():
         if a.json_out:
             with open(a.json_out, "w") as f:
                 f.write(line + "\n")
+    # the last step's ZeRO-1 parameter all-gathers were launched but never waited on (they
+    # overlap the next forward); complete them before the process group goes away
+    if hasattr(tr, "sync_params"):
+        tr.sync_params()
     if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
