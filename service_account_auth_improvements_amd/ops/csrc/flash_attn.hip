@@ -32,6 +32,8 @@
 //    sums are transposed through LDS and added row-contiguously in fp32.
 #include "common.h"
 
+#include <cstdlib>
+
 using namespace kf;
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
@@ -724,6 +726,39 @@ int kf_flash_fwd(const void* qkv, long ld, void* out, long ldo, float* lse, int 
   return 0;
 }
 
+// dQ || dK/dV fork: the two backward kernels only share read-only inputs, so the dQ kernel
+// runs on a side stream (event fork/join, legal under hipGraph capture) and its blocks fill
+// CUs as dK/dV blocks retire instead of waiting for the dK/dV grid's tail.  One side stream
+// and a fork/join event pair per device (one process per GPU).  KFAMD_FA_BWD_FORK=0 serialises.
+namespace {
+struct BwdFork {
+  hipStream_t side = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+bool bwd_fork_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("KFAMD_FA_BWD_FORK");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+BwdFork* bwd_fork() {
+  static BwdFork per_dev[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  BwdFork& f = per_dev[dev];
+  if (!f.side) {
+    if (hipStreamCreateWithFlags(&f.side, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&f.fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&f.join, hipEventDisableTiming) != hipSuccess) {
+      f.side = nullptr;
+      return nullptr;
+    }
+  }
+  return &f;
+}
+}  // namespace
+
 // dk_acc/dv_acc: zeroed fp32 [B*S, Hkv*128]; delta: fp32 [B, Hq, S] scratch.
 int kf_flash_bwd(const void* qkv, long ld, const void* o, long ldo, const void* dout, long lddo,
                  const float* lse, float* delta, float* dk_acc, float* dv_acc, void* dqkv,
@@ -738,16 +773,27 @@ int kf_flash_bwd(const void* qkv, long ld, const void* o, long ldo, const void* 
   for (int kb = 0; kb < S / BKV; ++kb) items += (S - (causal ? kb * BKV : 0) + QCH - 1) / QCH;
   const int g_kv = B * Hkv * items, g_q = B * Hq * ((S + BQ8 - 1) / BQ8);
   const float sl2 = scale * LOG2E;
+  BwdFork* fk = bwd_fork_enabled() ? bwd_fork() : nullptr;
+  hipStream_t sq = st;
+  if (fk && hipEventRecord(fk->fork, st) == hipSuccess &&
+      hipStreamWaitEvent(fk->side, fk->fork, 0) == hipSuccess)
+    sq = fk->side;
+  // dQ first on the side stream: its grid is forward-shaped (heaviest query blocks first) and
+  // starts while the dK/dV grid is being dispatched on `st`
   if (causal) {
+    flash_bwd_dq_kernel<true><<<g_q, 512, 0, sq>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo, lse,
+                                                   delta, (bf16_t*)dqkv, lddqkv, B, S, Hq, Hkv, sl2, scale);
     flash_bwd_dkdv_kernel<true><<<g_kv, 256, 0, st>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo,
                                                       lse, delta, dk_acc, dv_acc, B, S, Hq, Hkv, scale, items);
-    flash_bwd_dq_kernel<true><<<g_q, 512, 0, st>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo, lse,
-                                                   delta, (bf16_t*)dqkv, lddqkv, B, S, Hq, Hkv, sl2, scale);
   } else {
+    flash_bwd_dq_kernel<false><<<g_q, 512, 0, sq>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo, lse,
+                                                    delta, (bf16_t*)dqkv, lddqkv, B, S, Hq, Hkv, sl2, scale);
     flash_bwd_dkdv_kernel<false><<<g_kv, 256, 0, st>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo,
                                                        lse, delta, dk_acc, dv_acc, B, S, Hq, Hkv, scale, items);
-    flash_bwd_dq_kernel<false><<<g_q, 512, 0, st>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo, lse,
-                                                    delta, (bf16_t*)dqkv, lddqkv, B, S, Hq, Hkv, sl2, scale);
+  }
+  if (sq != st) {
+    if (hipEventRecord(fk->join, sq) != hipSuccess || hipStreamWaitEvent(st, fk->join, 0) != hipSuccess)
+      return 2;
   }
   const long chunks = (long)T * Hkv * 32;
   const int pg = (int)std::min<long>((chunks + 255) / 256, 16384);
