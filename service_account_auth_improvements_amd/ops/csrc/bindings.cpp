@@ -270,7 +270,7 @@ at::Tensor flash_bwd(const at::Tensor& qkv, const at::Tensor& o, const at::Tenso
   c10::hip::HIPGuardMasqueradingAsCUDA g(qkv.device());
   auto f32 = qkv.options().dtype(at::kFloat);
   auto delta = at::empty({B, Hq, S}, f32);
-  auto acc = at::zeros({2 * B * S * Hkv * D}, f32);
+  auto acc = at::empty({2 * B * S * Hkv * D}, f32);   // zeroed by kf_flash_bwd on its dK/dV stream
   float* dk = acc.data_ptr<float>();
   float* dv = dk + B * S * Hkv * D;
   auto dqkv = at::empty({B * S, (Hq + 2 * Hkv) * D}, qkv.options());

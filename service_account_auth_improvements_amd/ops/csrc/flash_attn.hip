@@ -726,14 +726,15 @@ int kf_flash_fwd(const void* qkv, long ld, void* out, long ldo, float* lse, int 
   return 0;
 }
 
-// dQ || dK/dV fork: the two backward kernels only share read-only inputs, so the dQ kernel
-// runs on a side stream (event fork/join, legal under hipGraph capture) and its blocks fill
-// CUs as dK/dV blocks retire instead of waiting for the dK/dV grid's tail.  One side stream
-// and a fork/join event pair per device (one process per GPU).  KFAMD_FA_BWD_FORK=0 serialises.
+// dQ || dK/dV fork: the two backward kernels only share read-only inputs, so the dK/dV
+// chain (zero its fp32 accumulators -> dK/dV kernel) runs on a side stream (event fork/join,
+// legal under hipGraph capture): the accumulator memset overlaps the delta pre-pass and the
+// dQ blocks fill CUs as dK/dV blocks retire instead of waiting for that grid's tail.  One
+// side stream and its events per device (one process per GPU).  KFAMD_FA_BWD_FORK=0 serialises.
 namespace {
 struct BwdFork {
   hipStream_t side = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
+  hipEvent_t fork = nullptr, pre = nullptr, join = nullptr;
 };
 bool bwd_fork_enabled() {
   static const bool on = [] {
@@ -750,6 +751,7 @@ BwdFork* bwd_fork() {
   if (!f.side) {
     if (hipStreamCreateWithFlags(&f.side, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&f.fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&f.pre, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&f.join, hipEventDisableTiming) != hipSuccess) {
       f.side = nullptr;
       return nullptr;
@@ -759,7 +761,7 @@ BwdFork* bwd_fork() {
 }
 }  // namespace
 
-// dk_acc/dv_acc: zeroed fp32 [B*S, Hkv*128]; delta: fp32 [B, Hq, S] scratch.
+// dk_acc/dv_acc: fp32 [B*S, Hkv*128] scratch (zeroed here); delta: fp32 [B, Hq, S] scratch.
 int kf_flash_bwd(const void* qkv, long ld, const void* o, long ldo, const void* dout, long lddo,
                  const float* lse, float* delta, float* dk_acc, float* dv_acc, void* dqkv,
                  long lddqkv, int B, int S, int Hq, int Hkv, int D_, float scale, int causal,
@@ -767,34 +769,38 @@ int kf_flash_bwd(const void* qkv, long ld, const void* o, long ldo, const void* 
   using namespace fb;
   if (D_ != D || S % BKV != 0 || S % BQ != 0 || Hq % Hkv != 0) return 1;
   const int T = B * S;
+  const size_t acc_bytes = (size_t)T * Hkv * D * sizeof(float);
+  BwdFork* fk = bwd_fork_enabled() ? bwd_fork() : nullptr;
+  hipStream_t skv = st;
+  if (fk && hipEventRecord(fk->fork, st) == hipSuccess &&
+      hipStreamWaitEvent(fk->side, fk->fork, 0) == hipSuccess)
+    skv = fk->side;
+  if (hipMemsetAsync(dk_acc, 0, acc_bytes, skv) != hipSuccess ||
+      hipMemsetAsync(dv_acc, 0, acc_bytes, skv) != hipSuccess)
+    return 2;
   flash_bwd_pre_kernel<<<(T * Hq + 15) / 16, 256, 0, st>>>((const bf16_t*)o, ldo, (const bf16_t*)dout,
                                                            lddo, delta, B, S, Hq);
+  if (skv != st &&
+      (hipEventRecord(fk->pre, st) != hipSuccess || hipStreamWaitEvent(skv, fk->pre, 0) != hipSuccess))
+    return 2;
   int items = 0;
   for (int kb = 0; kb < S / BKV; ++kb) items += (S - (causal ? kb * BKV : 0) + QCH - 1) / QCH;
   const int g_kv = B * Hkv * items, g_q = B * Hq * ((S + BQ8 - 1) / BQ8);
   const float sl2 = scale * LOG2E;
-  BwdFork* fk = bwd_fork_enabled() ? bwd_fork() : nullptr;
-  hipStream_t sq = st;
-  if (fk && hipEventRecord(fk->fork, st) == hipSuccess &&
-      hipStreamWaitEvent(fk->side, fk->fork, 0) == hipSuccess)
-    sq = fk->side;
-  // dQ first on the side stream: its grid is forward-shaped (heaviest query blocks first) and
-  // starts while the dK/dV grid is being dispatched on `st`
   if (causal) {
-    flash_bwd_dq_kernel<true><<<g_q, 512, 0, sq>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo, lse,
-                                                   delta, (bf16_t*)dqkv, lddqkv, B, S, Hq, Hkv, sl2, scale);
-    flash_bwd_dkdv_kernel<true><<<g_kv, 256, 0, st>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo,
-                                                      lse, delta, dk_acc, dv_acc, B, S, Hq, Hkv, scale, items);
-  } else {
-    flash_bwd_dq_kernel<false><<<g_q, 512, 0, sq>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo, lse,
-                                                    delta, (bf16_t*)dqkv, lddqkv, B, S, Hq, Hkv, sl2, scale);
-    flash_bwd_dkdv_kernel<false><<<g_kv, 256, 0, st>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo,
+    flash_bwd_dkdv_kernel<true><<<g_kv, 256, 0, skv>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo,
                                                        lse, delta, dk_acc, dv_acc, B, S, Hq, Hkv, scale, items);
+    flash_bwd_dq_kernel<true><<<g_q, 512, 0, st>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo, lse,
+                                                   delta, (bf16_t*)dqkv, lddqkv, B, S, Hq, Hkv, sl2, scale);
+  } else {
+    flash_bwd_dkdv_kernel<false><<<g_kv, 256, 0, skv>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo,
+                                                        lse, delta, dk_acc, dv_acc, B, S, Hq, Hkv, scale, items);
+    flash_bwd_dq_kernel<false><<<g_q, 512, 0, st>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo, lse,
+                                                    delta, (bf16_t*)dqkv, lddqkv, B, S, Hq, Hkv, sl2, scale);
   }
-  if (sq != st) {
-    if (hipEventRecord(fk->join, sq) != hipSuccess || hipStreamWaitEvent(st, fk->join, 0) != hipSuccess)
-      return 2;
-  }
+  if (skv != st &&
+      (hipEventRecord(fk->join, skv) != hipSuccess || hipStreamWaitEvent(st, fk->join, 0) != hipSuccess))
+    return 2;
   const long chunks = (long)T * Hkv * 32;
   const int pg = (int)std::min<long>((chunks + 255) / 256, 16384);
   flash_bwd_post_kernel<<<pg, 256, 0, st>>>(dk_acc, dv_acc, (bf16_t*)dqkv, lddqkv, T, Hq, Hkv);
