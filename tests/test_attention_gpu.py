@@ -64,3 +64,29 @@ def test_flash_bwd(B, S, Hq, Hkv, causal):
         a, r = dqkv[:, lo:hi].float(), ref[:, lo:hi]
         rel = ((a - r).abs().max() / r.abs().max()).item()
         assert rel < 3e-2, (name, rel)
+
+
+def test_flash_bwd_stream_fork_ordering():
+    """The backward forks its dK/dV chain (accumulator memset -> dK/dV) onto a side stream and
+    joins before the fp32->bf16 post-pass.  Back-to-back calls on a NON-default stream, with the
+    caching allocator recycling the accumulator between them, must agree with a call after a
+    full device sync: a missing fork/join edge shows up as stale or unzeroed dK/dV."""
+    B, S, Hq, Hkv = 2, 1024, 8, 2
+    sc = 1 / math.sqrt(128)
+    qkv = _qkv(B, S, Hq, Hkv, seed=21)
+    o, lse = torch.ops.kfamd.flash_fwd(qkv, B, S, Hq, Hkv, 128, sc, True)
+    do = torch.randn(o.shape, generator=torch.Generator(device="cpu").manual_seed(5)).to(DEV, torch.bfloat16)
+    base = torch.ops.kfamd.flash_bwd(qkv, o, lse, do, B, S, Hq, Hkv, 128, sc, True)
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream(device=DEV)
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        outs = [torch.ops.kfamd.flash_bwd(qkv, o, lse, do, B, S, Hq, Hkv, 128, sc, True) for _ in range(4)]
+        outs = [x.float().clone() for x in outs]
+    torch.cuda.synchronize()
+    ref = base.float()
+    for x in outs:
+        # dQ is written once (bitwise); dK/dV are fp32 atomic sums (order-dependent last bits)
+        assert torch.equal(x[:, :Hq * 128], ref[:, :Hq * 128])
+        err = ((x - ref).abs().max() / ref.abs().max()).item()
+        assert err < 1e-2, err
