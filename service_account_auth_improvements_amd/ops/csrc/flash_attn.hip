@@ -30,6 +30,8 @@
 //    -lse/scale and -delta, the "row constants"), dV^T += dO^T.P, dK^T += Q^T.dS; each
 //    wave keeps its 32 keys' dK^T/dV^T (128 registers) across the chunk; chunk partial
 //    sums are transposed through LDS and added row-contiguously in fp32.
+//  * The two kernels run concurrently: dQ on the caller's stream, the accumulator memset and
+//    dK/dV on a per-device side stream (event fork/join, see kf_flash_bwd).
 #include "common.h"
 
 #include <cstdlib>
