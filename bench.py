@@ -1,8 +1,11 @@
 #!/usr/bin/env python
 """Headline benchmark: training tokens/s of a PyTorchJob-style Llama-3-8B DDP job.
 
-Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 it is
-launched by torchrun (one rank per GPU, RCCL over xGMI).  W untimed warmup steps, then
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 it runs one
+rank per GPU over RCCL (xGMI).  Under torchrun (``WORLD_SIZE`` set) it is one of the ranks
+and refuses to run when ``WORLD_SIZE != --gpus``; launched bare with ``--gpus N > 1`` it
+starts ``torch.distributed.run`` with N ranks as a CHILD process before anything touches
+the GPU, and exits with the child's status (never an exec of the current process).  W untimed warmup steps, then
 exactly K timed steps bracketed by barrier + device synchronize on both sides; the MAX
 elapsed time over ranks is used; rank 0 prints ONE JSON line.
 
@@ -21,6 +24,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -29,12 +34,29 @@ import torch.distributed as dist
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
-from service_account_auth_improvements_amd.ops import set_attention_backend  # noqa: E402
 from service_account_auth_improvements_amd.parallel.state import init_distributed  # noqa: E402
 from service_account_auth_improvements_amd.runtime.trainer import (SyntheticData, TrainConfig,  # noqa: E402
                                                                    Trainer)
 
 BASELINE_METRIC = "tokens/sec PyTorchJob Llama-3-8B DDP at 1/2/4/8 MI355X; CRD-to-first-step p50"
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _launch_ranks(n: int) -> int:
+    """Run this script as N ranks under torch.distributed.run (a child process; this process
+    has not initialised the GPU and never does)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__), *sys.argv[1:]]
+    print(f"bench: launching {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.call(cmd)
 
 
 def main():
@@ -51,7 +73,9 @@ def main():
                          "behind the next forward (default when N > 1)")
     ap.add_argument("--no-zero1", dest="zero1", action="store_false", help="classic all-reduce DDP")
     ap.add_argument("--bucket-mb", type=int, default=256)
-    ap.add_argument("--attn", default="hip", choices=["hip", "sdpa"])
+    ap.add_argument("--grad-reduce", default="fp32", choices=["fp32", "bf16"],
+                    help="DP gradient reduction precision: fp32 (bf16 shards all-to-all + fp32 sum; "
+                         "fp32 micro-batch accumulation) or bf16 (RCCL bf16 reduce-scatter / all-reduce)")
     ap.add_argument("--tp", type=int, default=1, help="tensor parallel degree (configs[4]: 70B TP=8)")
     ap.add_argument("--pp", type=int, default=1, help="pipeline parallel degree (1F1B)")
     ap.add_argument("--recompute", action="store_true",
@@ -60,15 +84,23 @@ def main():
     ap.add_argument("--json-out", default=None)
     a = ap.parse_args()
 
-    set_attention_backend(a.attn)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and a.gpus > 1:
+        sys.exit(_launch_ranks(a.gpus))
+    if int(env_world or 1) != a.gpus:
+        print(f"bench: --gpus {a.gpus} but WORLD_SIZE={env_world}: refusing to report a "
+              "different GPU count", file=sys.stderr)
+        sys.exit(2)
     st = init_distributed(tp=a.tp, pp=a.pp)
     world = st.world_size
+    backend = dist.get_backend() if dist.is_initialized() else "none"
+    world_seen = dist.get_world_size() if dist.is_initialized() else 1
+    assert world_seen == a.gpus, (world_seen, a.gpus)
     if a.zero1 is None:
         a.zero1 = st.dp > 1 and a.pp == 1
-    if world != a.gpus and st.rank == 0:
-        print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     tcfg = TrainConfig(model=a.model, seq_len=a.seq_len, micro_batch=a.micro_batch,
                        grad_accum=a.grad_accum, zero1=a.zero1, bucket_mb=a.bucket_mb,
+                       grad_reduce=a.grad_reduce,
                        n_layers=a.layers, recompute=a.recompute)
     t0 = time.time()
     if a.pp > 1:
@@ -134,12 +166,15 @@ def main():
                 "parallelism": "".join(f"{k}{v}" for k, v in (("dp", st.dp), ("tp", a.tp), ("pp", a.pp))
                                        if v > 1 or k == "dp"),
                 "optimizer_sharding": "zero1" if a.zero1 else "none",
+                "grad_reduce": a.grad_reduce,
                 "micro_batch": a.micro_batch,
                 "grad_accum": a.grad_accum,
                 "n_layers": tr.mcfg.n_layers,
-                "attention": a.attn,
+                "attention": "hip",
                 "activation_recompute": a.recompute,
             },
+            "backend": backend,
+            "world_size_seen": world_seen,
             "tokens_per_s_per_gpu": round(value / world, 1),
             "model_tflops_per_gpu": round(value / world * flops_tok / 1e12, 1),
             "peak_mem_gib": round(peak_mem, 1),

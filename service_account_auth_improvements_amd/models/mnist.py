@@ -47,6 +47,26 @@ class MnistTrainer:
         if dist.is_initialized() and dist.get_world_size() > 1:
             self.model = nn.parallel.DistributedDataParallel(self.model)
         self.opt = torch.optim.SGD(self.model.parameters(), lr=lr, momentum=0.9)
+        self.step_idx = 0
+
+    def _module(self):
+        return self.model.module if hasattr(self.model, "module") else self.model
+
+    def state_tensors(self) -> dict:
+        """Weights and SGD momentum buffers as a flat name -> tensor dict (safetensors)."""
+        out = {f"w/{k}": v.detach() for k, v in self._module().state_dict().items()}
+        for i, p in enumerate(self._module().parameters()):
+            buf = self.opt.state.get(p, {}).get("momentum_buffer")
+            if buf is not None:
+                out[f"momentum/{i}"] = buf.detach()
+        return out
+
+    def load_state_tensors(self, t: dict):
+        m = self._module()
+        m.load_state_dict({k[2:]: v for k, v in t.items() if k.startswith("w/")})
+        for i, p in enumerate(m.parameters()):
+            if f"momentum/{i}" in t:
+                self.opt.state[p]["momentum_buffer"] = t[f"momentum/{i}"].to(p.device).clone()
 
     def train_step(self, batches):
         """One optimizer step over a list of micro-batches (gradient accumulation)."""
@@ -57,4 +77,5 @@ class MnistTrainer:
             loss.backward()
             tot += float(loss)
         self.opt.step()
+        self.step_idx += 1
         return torch.tensor(tot)

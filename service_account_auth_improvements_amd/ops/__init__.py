@@ -14,8 +14,7 @@ from __future__ import annotations
 import torch
 
 from . import _ext, reference
-from .attention import (attention, attention_bwd, attention_fwd, decode_attention,  # noqa: F401
-                        set_attention_backend, get_attention_backend)
+from .attention import attention, attention_bwd, attention_fwd, decode_attention  # noqa: F401
 
 
 def _k():
@@ -251,8 +250,38 @@ def adamw_(p, w, m, v, g, n_decay, lr, b1, b2, eps, wd, step, gscale=1.0, sumsq=
                          None if sumsq is None else float(sumsq.reshape(-1)[0]), max_norm)
 
 
+def shard_sum_(recv, nranks: int, out, accumulate: bool = False):
+    """out (+)= sum over r of recv[r*n:(r+1)*n] (bf16 shards summed in fp32, rank order):
+    the local half of the fp32 all-to-all gradient reduction (ops/csrc/grad_reduce.hip)."""
+    if recv.is_cuda:
+        _k().shard_sum_(recv, int(nranks), out, accumulate)
+        return out
+    s = recv.view(int(nranks), -1).float()
+    acc = out.clone() if accumulate else torch.zeros_like(out)
+    for r in range(int(nranks)):
+        acc += s[r]
+    out.copy_(acc)
+    return out
+
+
+GRAD_SET, GRAD_ADD, GRAD_FOLD = 0, 1, 2
+
+
+def grad_accum_(main, g, mode: int):
+    """fp32 micro-batch gradient accumulation: GRAD_SET main = g; GRAD_ADD main += g;
+    GRAD_FOLD g = bf16(main + g) (one rounding, right before the bucket is sent)."""
+    if g.is_cuda:
+        _k().grad_accum_(main, g, int(mode))
+    elif mode == GRAD_SET:
+        main.copy_(g)
+    elif mode == GRAD_ADD:
+        main.add_(g.float())
+    else:
+        g.copy_(main + g.float())
+
+
 def sumsq_(g, out, accumulate=False):
-    """out[0] (+)= sum(g^2) (fp32, deterministic)."""
+    """out[0] (+)= sum(g^2) (fp32, deterministic); g is bf16 or fp32."""
     if g.is_cuda:
         _k().sumsq(g, out, accumulate)
     else:

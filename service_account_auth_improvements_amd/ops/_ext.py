@@ -33,12 +33,11 @@ def load(build_if_missing: bool = True) -> bool:
             return True
         path = _build.LIB_PATH
         if build_if_missing and os.environ.get("KFAMD_NO_BUILD") != "1":
-            # incremental: a no-op when the stamp matches the sources
-            try:
-                _build.build()
-            except Exception:
-                if not path.exists():
-                    raise
+            # incremental: a no-op when the stamp matches the sources.  A failed rebuild
+            # raises -- loading the previous .so would silently run stale kernels.  Loading a
+            # prebuilt library whose stamp may not match is only done on explicit request
+            # (KFAMD_NO_BUILD=1).
+            _build.build()
         if not path.exists():
             return False
         torch.ops.load_library(str(path))

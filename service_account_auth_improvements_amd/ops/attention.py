@@ -5,31 +5,17 @@ GEMM, RoPE in place).  The gfx950 flash kernels read q/k/v straight out of that 
 with its row stride, so no transpose/copy to [B, H, S, D] is ever made, and write the
 output as [T, Hq*D] -- exactly the operand the O-projection GEMM wants.
 
-Backends:
-  * ``hip``  -- hand-written MFMA flash attention (ops/csrc/flash_attn.hip); the default.
-  * ``sdpa`` -- torch SDPA (AOTriton on ROCm); kept only as a measured baseline to beat.
-  * CPU tensors always use the fp32 reference.
+GPU tensors always run the hand-written MFMA flash attention (ops/csrc/flash_attn.hip);
+there is no second GPU backend in the dispatch (the torch-SDPA comparison lives in
+``tools/bench_attn.py``).  CPU tensors use the fp32 reference.
 """
 from __future__ import annotations
 
 import math
 
 import torch
-import torch.nn.functional as F
 
 from . import _ext, reference
-
-_BACKEND = "hip"
-
-
-def set_attention_backend(name: str) -> None:
-    global _BACKEND
-    assert name in ("hip", "sdpa"), name
-    _BACKEND = name
-
-
-def get_attention_backend() -> str:
-    return _BACKEND
 
 
 def _split(qkv, B, S, Hq, Hkv, D):
@@ -42,31 +28,24 @@ def _split(qkv, B, S, Hq, Hkv, D):
 def attention_fwd(qkv, B, S, Hq, Hkv, D, causal=True):
     """Returns (o [T, Hq*D] bf16, lse [B, Hq, S] fp32)."""
     scale = 1.0 / math.sqrt(D)
-    if qkv.is_cuda and _BACKEND == "hip":
+    if qkv.is_cuda:
         return _ext.ops().flash_fwd(qkv, B, S, Hq, Hkv, D, scale, causal)
     q, k, v = _split(qkv, B, S, Hq, Hkv, D)
-    if qkv.is_cuda:  # sdpa baseline
-        o = F.scaled_dot_product_attention(q, k, v, is_causal=causal, enable_gqa=True)
-        lse = torch.empty(B, Hq, S, device=qkv.device, dtype=torch.float32)
-    else:
-        o, lse = reference.attention(q, k, v, causal, scale)
-        o = o.to(qkv.dtype)
+    o, lse = reference.attention(q, k, v, causal, scale)
+    o = o.to(qkv.dtype)
     return o.transpose(1, 2).reshape(B * S, Hq * D), lse
 
 
 def attention_bwd(qkv, o, lse, do, B, S, Hq, Hkv, D, causal=True):
     """Returns dqkv [T, (Hq + 2*Hkv)*D] in the fused layout."""
     scale = 1.0 / math.sqrt(D)
-    if qkv.is_cuda and _BACKEND == "hip":
+    if qkv.is_cuda:
         return _ext.ops().flash_bwd(qkv, o, lse, do.contiguous(), B, S, Hq, Hkv, D, scale, causal)
-    # baseline / CPU: recompute through autograd
+    # CPU: recompute the fp32 reference through autograd
     with torch.enable_grad():
         x = qkv.detach().requires_grad_(True)
         q, k, v = _split(x, B, S, Hq, Hkv, D)
-        if qkv.is_cuda:
-            oo = F.scaled_dot_product_attention(q, k, v, is_causal=causal, enable_gqa=True)
-        else:
-            oo = reference.attention(q, k, v, causal, scale)[0].to(qkv.dtype)
+        oo = reference.attention(q, k, v, causal, scale)[0].to(qkv.dtype)
         oo = oo.transpose(1, 2).reshape(B * S, Hq * D)
         (dqkv,) = torch.autograd.grad(oo, x, do)
     return dqkv

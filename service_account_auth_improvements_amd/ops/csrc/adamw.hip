@@ -7,6 +7,10 @@
 // multi-tensor-apply pointer lists -- moving 30 B/param (bf16 g, fp32 w/m/v r+w, bf16 w).
 // For Llama-3-8B that is ~240 GB -> ~40 ms at the measured ~6 TB/s HBM roof.
 //
+// The gradient operand is bf16 (the flat gradient buffer, single-rank or bf16-reduced) or
+// fp32 (the fp32 DP reduction's shard / the fp32 micro-batch accumulator, see
+// grad_reduce.hip); the element loop is the same template.
+//
 // Gradient clipping never syncs with the host: the global sum of squares is produced on
 // device (kf_sumsq, deterministic two-level reduce) and the AdamW kernel derives the clip
 // coefficient from it.  Elements [0, n_decay) receive decoupled weight decay; the tail
@@ -15,9 +19,22 @@
 
 using namespace kf;
 
+template <bool G32>
+__device__ __forceinline__ void load_grad8(const void* g, size_t e, float* gf) {
+  if constexpr (G32) {
+    const float* gp = reinterpret_cast<const float*>(g) + e;
+    f32x4 a = ldf4(gp), b = ldf4(gp + 4);
+    gf[0] = a[0]; gf[1] = a[1]; gf[2] = a[2]; gf[3] = a[3];
+    gf[4] = b[0]; gf[5] = b[1]; gf[6] = b[2]; gf[7] = b[3];
+  } else {
+    unpack8(ld16(reinterpret_cast<const bf16_t*>(g) + e), gf);
+  }
+}
+
+template <bool G32>
 __global__ __launch_bounds__(256) void adamw_kernel(
     bf16_t* __restrict__ p, float* __restrict__ w, float* __restrict__ m, float* __restrict__ v,
-    const bf16_t* __restrict__ g, size_t nvec, size_t n_decay, float lr, float b1, float b2,
+    const void* __restrict__ g, size_t nvec, size_t n_decay, float lr, float b1, float b2,
     float eps, float wd, float inv_bc1, float inv_sqrt_bc2, float gscale,
     const float* __restrict__ sumsq, float max_norm) {
   float coef = gscale;
@@ -29,7 +46,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(
        i += (size_t)gridDim.x * blockDim.x) {
     const size_t e = i * 8;
     float gf[8];
-    unpack8(ld16(g + e), gf);
+    load_grad8<G32>(g, e, gf);
     f32x4 w0 = ldf4(w + e), w1 = ldf4(w + e + 4);
     f32x4 m0 = ldf4(m + e), m1 = ldf4(m + e + 4);
     f32x4 v0 = ldf4(v + e), v1 = ldf4(v + e + 4);
@@ -52,16 +69,17 @@ __global__ __launch_bounds__(256) void adamw_kernel(
   }
 }
 
-// Sum of squares of a bf16 vector: per-block partials, then one block folds them
+// Sum of squares of a bf16 or fp32 vector: per-block partials, then one block folds them
 // in a fixed order (bitwise reproducible, no float atomics).
-__global__ __launch_bounds__(256) void sumsq_partial_kernel(const bf16_t* __restrict__ g, size_t nvec,
+template <bool G32>
+__global__ __launch_bounds__(256) void sumsq_partial_kernel(const void* __restrict__ g, size_t nvec,
                                                             float* __restrict__ part) {
   __shared__ float red[4];
   float s = 0.f;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec;
        i += (size_t)gridDim.x * blockDim.x) {
     float f[8];
-    unpack8(ld16(g + i * 8), f);
+    load_grad8<G32>(g, i * 8, f);
 #pragma unroll
     for (int j = 0; j < 8; ++j) s += f[j] * f[j];
   }
@@ -80,7 +98,7 @@ __global__ __launch_bounds__(256) void sum_final_kernel(const float* __restrict_
 
 extern "C" {
 
-int kf_adamw(void* p, float* w, float* m, float* v, const void* g, size_t n, size_t n_decay,
+int kf_adamw(void* p, float* w, float* m, float* v, const void* g, int g_fp32, size_t n, size_t n_decay,
              float lr, float b1, float b2, float eps, float wd, int step, float gscale,
              const float* sumsq, float max_norm, hipStream_t s) {
   if (n % 8) return 1;
@@ -89,20 +107,26 @@ int kf_adamw(void* p, float* w, float* m, float* v, const void* g, size_t n, siz
   size_t grid = (nvec + 255) / 256;
   if (grid > 8192) grid = 8192;
   if (grid < 1) grid = 1;
-  adamw_kernel<<<(int)grid, 256, 0, s>>>((bf16_t*)p, w, m, v, (const bf16_t*)g, nvec, n_decay, lr,
-                                         b1, b2, eps, wd, 1.f / bc1, 1.f / sqrtf(bc2), gscale,
-                                         sumsq, max_norm);
+  if (g_fp32)
+    adamw_kernel<true><<<(int)grid, 256, 0, s>>>((bf16_t*)p, w, m, v, g, nvec, n_decay, lr, b1, b2, eps, wd,
+                                                 1.f / bc1, 1.f / sqrtf(bc2), gscale, sumsq, max_norm);
+  else
+    adamw_kernel<false><<<(int)grid, 256, 0, s>>>((bf16_t*)p, w, m, v, g, nvec, n_decay, lr, b1, b2, eps, wd,
+                                                  1.f / bc1, 1.f / sqrtf(bc2), gscale, sumsq, max_norm);
   return 0;
 }
 
 // part must hold 2048 floats. out[0] = sum(g^2) (+ out[0] if accumulate).
-int kf_sumsq(const void* g, size_t n, float* part, float* out, int accumulate, hipStream_t s) {
+int kf_sumsq(const void* g, int g_fp32, size_t n, float* part, float* out, int accumulate, hipStream_t s) {
   if (n % 8) return 1;
   const size_t nvec = n / 8;
   size_t grid = (nvec + 255) / 256;
   if (grid > 2048) grid = 2048;
   if (grid < 1) grid = 1;
-  sumsq_partial_kernel<<<(int)grid, 256, 0, s>>>((const bf16_t*)g, nvec, part);
+  if (g_fp32)
+    sumsq_partial_kernel<true><<<(int)grid, 256, 0, s>>>(g, nvec, part);
+  else
+    sumsq_partial_kernel<false><<<(int)grid, 256, 0, s>>>(g, nvec, part);
   sum_final_kernel<<<1, 256, 0, s>>>(part, (int)grid, out, accumulate);
   return 0;
 }

@@ -25,9 +25,11 @@ int kf_rope(void*, long, int, int, int, const float*, const float*, const int*, 
             hipStream_t);
 int kf_swiglu_fwd(const void*, void*, int, int, hipStream_t);
 int kf_swiglu_bwd(const void*, const void*, void*, int, int, hipStream_t);
-int kf_adamw(void*, float*, float*, float*, const void*, size_t, size_t, float, float, float, float,
+int kf_adamw(void*, float*, float*, float*, const void*, int, size_t, size_t, float, float, float, float,
              float, int, float, const float*, float, hipStream_t);
-int kf_sumsq(const void*, size_t, float*, float*, int, hipStream_t);
+int kf_sumsq(const void*, int, size_t, float*, float*, int, hipStream_t);
+int kf_shard_sum(const void*, int, size_t, float*, int, hipStream_t);
+int kf_grad_accum(float*, void*, size_t, int, hipStream_t);
 int kf_cross_entropy(void*, long, int, int, const long*, long, long, float*, float*, float*, float*,
                      float*, const float*, float, int, hipStream_t);
 int kf_flash_fwd(const void*, long, void*, long, float*, int, int, int, int, int, float, int,
@@ -188,7 +190,8 @@ void adamw_(at::Tensor p, at::Tensor w, at::Tensor m, at::Tensor v, const at::Te
             int64_t n_decay, double lr, double b1, double b2, double eps, double wd, int64_t step,
             double gscale, const std::optional<at::Tensor>& sumsq, double max_norm) {
   check_bf16_cuda(p, "p");
-  check_bf16_cuda(g, "g");
+  TORCH_CHECK(g.is_cuda() && (g.scalar_type() == at::kBFloat16 || g.scalar_type() == at::kFloat),
+              "adamw: g must be a bf16 or fp32 GPU tensor");
   const int64_t n = p.numel();
   TORCH_CHECK(w.numel() == n && m.numel() == n && v.numel() == n && g.numel() == n, "adamw: sizes");
   TORCH_CHECK(w.scalar_type() == at::kFloat && m.scalar_type() == at::kFloat && v.scalar_type() == at::kFloat,
@@ -199,17 +202,18 @@ void adamw_(at::Tensor p, at::Tensor w, at::Tensor m, at::Tensor v, const at::Te
   if (sumsq.has_value()) sp = sumsq->data_ptr<float>();
   c10::hip::HIPGuardMasqueradingAsCUDA gd(p.device());
   check_rc(kf_adamw(p.data_ptr(), w.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
-                    g.data_ptr(), (size_t)n, (size_t)n_decay, (float)lr, (float)b1, (float)b2,
+                    g.data_ptr(), g.scalar_type() == at::kFloat ? 1 : 0, (size_t)n, (size_t)n_decay, (float)lr, (float)b1, (float)b2,
                     (float)eps, (float)wd, (int)step, (float)gscale, sp, (float)max_norm, cur_stream()),
            "adamw");
 }
 
 void sumsq(const at::Tensor& g, at::Tensor out, bool accumulate) {
-  check_bf16_cuda(g, "g");
+  TORCH_CHECK(g.is_cuda() && (g.scalar_type() == at::kBFloat16 || g.scalar_type() == at::kFloat),
+              "sumsq: g must be a bf16 or fp32 GPU tensor");
   TORCH_CHECK(g.is_contiguous() && out.scalar_type() == at::kFloat, "sumsq: args");
   c10::hip::HIPGuardMasqueradingAsCUDA gd(g.device());
   auto part = at::empty({2048}, g.options().dtype(at::kFloat));
-  check_rc(kf_sumsq(g.data_ptr(), (size_t)g.numel(), part.data_ptr<float>(), out.data_ptr<float>(),
+  check_rc(kf_sumsq(g.data_ptr(), g.scalar_type() == at::kFloat ? 1 : 0, (size_t)g.numel(), part.data_ptr<float>(), out.data_ptr<float>(),
                     accumulate ? 1 : 0, cur_stream()),
            "sumsq");
 }
@@ -597,6 +601,30 @@ void embed_bwd_(const at::Tensor& tok, const at::Tensor& g, at::Tensor& dE, int6
 
 }  // namespace
 
+// ---------------- fp32 DP gradient reduction / accumulation (grad_reduce.hip) ----------------
+// out (+)= sum of the R equal bf16 shards of `recv` (fp32, rank order)
+void shard_sum_(const at::Tensor& recv, int64_t R, at::Tensor out, bool accumulate) {
+  check_bf16_cuda(recv, "recv");
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.is_contiguous() && recv.is_contiguous(),
+              "shard_sum: out must be contiguous fp32 on the GPU");
+  TORCH_CHECK(R >= 1 && recv.numel() == R * out.numel() && out.numel() % 8 == 0, "shard_sum: sizes");
+  c10::hip::HIPGuardMasqueradingAsCUDA gd(recv.device());
+  check_rc(kf_shard_sum(recv.data_ptr(), (int)R, (size_t)out.numel(), out.data_ptr<float>(), accumulate ? 1 : 0,
+                        cur_stream()),
+           "shard_sum");
+}
+
+// mode 0: main = g; 1: main += g; 2: g = bf16(main + g)
+void grad_accum_(at::Tensor main_, at::Tensor g, int64_t mode) {
+  check_bf16_cuda(g, "g");
+  TORCH_CHECK(main_.is_cuda() && main_.scalar_type() == at::kFloat && main_.is_contiguous() && g.is_contiguous(),
+              "grad_accum: main must be contiguous fp32 on the GPU");
+  TORCH_CHECK(main_.numel() == g.numel() && g.numel() % 8 == 0, "grad_accum: sizes");
+  c10::hip::HIPGuardMasqueradingAsCUDA gd(g.device());
+  check_rc(kf_grad_accum(main_.data_ptr<float>(), g.data_ptr(), (size_t)g.numel(), (int)mode, cur_stream()),
+           "grad_accum");
+}
+
 TORCH_LIBRARY(kfamd, m) {
   m.def("rmsnorm_fwd", &rmsnorm_fwd);
   m.def("rmsnorm_bwd", &rmsnorm_bwd);
@@ -605,6 +633,8 @@ TORCH_LIBRARY(kfamd, m) {
   m.def("swiglu_bwd", &swiglu_bwd);
   m.def("adamw_", &adamw_);
   m.def("sumsq", &sumsq);
+  m.def("shard_sum_(Tensor recv, int R, Tensor(a!) out, bool accumulate) -> ()", &shard_sum_);
+  m.def("grad_accum_(Tensor(a!) main, Tensor(b!) g, int mode) -> ()", &grad_accum_);
   m.def("cross_entropy_", &cross_entropy_);
   m.def("flash_fwd", &flash_fwd);
   m.def("flash_bwd", &flash_bwd);

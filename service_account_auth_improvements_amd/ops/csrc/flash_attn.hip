@@ -34,6 +34,8 @@
 //    dK/dV on a per-device side stream (event fork/join, see kf_flash_bwd).
 #include "common.h"
 
+#include <mutex>
+
 #include <cstdlib>
 
 using namespace kf;
@@ -733,10 +735,15 @@ int kf_flash_fwd(const void* qkv, long ld, void* out, long ldo, float* lse, int 
 // legal under hipGraph capture): the accumulator memset overlaps the delta pre-pass and the
 // dQ blocks fill CUs as dK/dV blocks retire instead of waiting for that grid's tail.  One
 // side stream and its events per device (one process per GPU).  KFAMD_FA_BWD_FORK=0 serialises.
+// The lazy per-device init and every use of the shared events run under the device's mutex
+// (two host threads may call backward on one device), and every exit after the fork joins the
+// side stream back, so an error return never leaves forked work dangling (which would also
+// invalidate a hipGraph capture).
 namespace {
 struct BwdFork {
   hipStream_t side = nullptr;
   hipEvent_t fork = nullptr, pre = nullptr, join = nullptr;
+  std::mutex mu;
 };
 bool bwd_fork_enabled() {
   static const bool on = [] {
@@ -750,6 +757,7 @@ BwdFork* bwd_fork() {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
   BwdFork& f = per_dev[dev];
+  std::lock_guard<std::mutex> lk(f.mu);
   if (!f.side) {
     if (hipStreamCreateWithFlags(&f.side, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&f.fork, hipEventDisableTiming) != hipSuccess ||
@@ -773,18 +781,25 @@ int kf_flash_bwd(const void* qkv, long ld, const void* o, long ldo, const void* 
   const int T = B * S;
   const size_t acc_bytes = (size_t)T * Hkv * D * sizeof(float);
   BwdFork* fk = bwd_fork_enabled() ? bwd_fork() : nullptr;
+  std::unique_lock<std::mutex> lk;
+  if (fk) lk = std::unique_lock<std::mutex>(fk->mu);
   hipStream_t skv = st;
   if (fk && hipEventRecord(fk->fork, st) == hipSuccess &&
       hipStreamWaitEvent(fk->side, fk->fork, 0) == hipSuccess)
     skv = fk->side;
+  // error exit after the fork: join the side stream back before returning
+  auto fail = [&](int rc) {
+    if (skv != st && hipEventRecord(fk->join, skv) == hipSuccess) (void)hipStreamWaitEvent(st, fk->join, 0);
+    return rc;
+  };
   if (hipMemsetAsync(dk_acc, 0, acc_bytes, skv) != hipSuccess ||
       hipMemsetAsync(dv_acc, 0, acc_bytes, skv) != hipSuccess)
-    return 2;
+    return fail(2);
   flash_bwd_pre_kernel<<<(T * Hq + 15) / 16, 256, 0, st>>>((const bf16_t*)o, ldo, (const bf16_t*)dout,
                                                            lddo, delta, B, S, Hq);
   if (skv != st &&
       (hipEventRecord(fk->pre, st) != hipSuccess || hipStreamWaitEvent(skv, fk->pre, 0) != hipSuccess))
-    return 2;
+    return fail(2);
   int items = 0;
   for (int kb = 0; kb < S / BKV; ++kb) items += (S - (causal ? kb * BKV : 0) + QCH - 1) / QCH;
   const int g_kv = B * Hkv * items, g_q = B * Hq * ((S + BQ8 - 1) / BQ8);

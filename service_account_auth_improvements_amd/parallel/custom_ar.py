@@ -47,6 +47,7 @@ class OneShotAllReduce:
                 self._opened.append(p)
                 self.ptrs.append(p)
         dist.barrier(group=group)
+        self.failed = False
 
     def supports(self, x: torch.Tensor) -> bool:
         return (x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and x.numel() % 8 == 0
@@ -63,6 +64,19 @@ class OneShotAllReduce:
     def error(self) -> int:
         """1 when a peer failed to arrive within the kernel's spin budget since the last check."""
         return int(_ext.ops().car_error(self._own))
+
+    def check(self):
+        """Raise if any all-reduce since the last check timed out waiting for a peer.
+
+        A timed-out kernel summed whatever sat in the peer slots, so the step's outputs are
+        garbage, and the ranks' device epochs are out of step from then on: the communicator
+        is poisoned for good (``failed``) and every later check raises too -- the serving
+        process must be restarted (the predictor's readiness probe reports it)."""
+        if self.failed or self.error():
+            self.failed = True
+            raise RuntimeError("one-shot all-reduce: a tensor-parallel peer did not arrive within the "
+                               "spin budget; this step's results are invalid and the communicator is "
+                               "out of step (restart the predictor)")
 
     def close(self):
         k = _ext.ops()

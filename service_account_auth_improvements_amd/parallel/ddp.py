@@ -15,6 +15,20 @@ Two modes:
     bf16 parameters are all-gathered bucket by bucket.  Same bytes on the wire as an
     all-reduce (RS + AG = AR) but 1/dp of the optimizer traffic and state per GPU.
 
+Reduction precision (``reduce_dtype``):
+  * ``bf16``: the bucket is reduced in bf16 by RCCL (a ring rounds every partial sum:
+    N-1 bf16 roundings per element at N ranks).
+  * ``fp32`` (default for N > 1): no partial sum is ever rounded.
+      - ZeRO-1: each bucket moves as an ALL-TO-ALL of its bf16 shards (same bytes per GPU
+        as a bf16 reduce-scatter; on the fully connected xGMI mesh each shard rides its own
+        point-to-point link) and the N received shards are summed in fp32 by a HIP kernel
+        (ops/csrc/grad_reduce.hip) into an fp32 gradient shard that AdamW reads directly.
+      - all-reduce DDP: the bucket is staged into an fp32 buffer and all-reduced in fp32
+        (2x the wire bytes; the ZeRO-1 path is the default for N > 1).
+      - grad_accum > 1: micro-batches accumulate in an fp32 main-gradient buffer instead of
+        bf16 beta=1 GEMM accumulation; the last micro-batch is folded in (one rounding)
+        right before its bucket is sent.
+
 Sizing for xGMI: a ring collective is bound by one ~153 GB/s link per hop, so per-call
 latency matters little at these sizes and large buckets (default 256 MB) minimise launch
 count; the whole 8B gradient is 16 GB -> ~64 buckets.
@@ -26,23 +40,29 @@ from typing import List, Optional, Tuple
 import torch
 import torch.distributed as dist
 
+from .. import ops
 from ..runtime.flat import FlatGroup
 
 
 class Bucket:
-    __slots__ = ("group", "lo", "hi", "work", "launched", "staged")
+    __slots__ = ("group", "lo", "hi", "idx", "work", "launched", "staged", "recv")
 
-    def __init__(self, group: FlatGroup, lo: int, hi: int):
-        self.group, self.lo, self.hi = group, lo, hi
+    def __init__(self, group: FlatGroup, lo: int, hi: int, idx: int):
+        self.group, self.lo, self.hi, self.idx = group, lo, hi, idx
         self.work = None
         self.launched = False
         self.staged = None      # (shard view, separate output) when the backend must not alias
+        self.recv = None        # fp32 ZeRO-1: the bucket's received bf16 shards [dp * n]
 
 
 class GradReducer:
     def __init__(self, groups: List[FlatGroup], dp_group=None, dp_size: int = 1,
-                 bucket_bytes: int = 256 << 20, mode: str = "allreduce"):
+                 bucket_bytes: int = 256 << 20, mode: str = "allreduce",
+                 reduce_dtype: str = "bf16", grad_accum: int = 1, force_collectives: bool = False):
+        """``force_collectives`` runs the DP collectives even at dp_size 1 (a one-rank RCCL
+        group exercises the exact call sequence on a one-GPU box)."""
         assert mode in ("allreduce", "reduce_scatter")
+        assert reduce_dtype in ("bf16", "fp32"), reduce_dtype
         self.dp_group, self.dp = dp_group, dp_size
         self.mode = mode
         self.groups = groups
@@ -56,12 +76,70 @@ class GradReducer:
             bl, lo = [], 0
             while lo < g.numel:
                 hi = min(g.numel, lo + elems)
-                bl.append(Bucket(g, lo, hi))
+                bl.append(Bucket(g, lo, hi, len(bl)))
                 lo = hi
             self.buckets[g.name] = bl
-        self.enabled = dp_size > 1
+        self.enabled = dp_size > 1 or force_collectives
+        self.fp32 = reduce_dtype == "fp32"
+        self.reduce_dtype = reduce_dtype
+        self.grad_accum = grad_accum
         self._pending: List[Bucket] = []
         self._gathers: dict = {}          # (group name, bucket index) -> async all-gather work
+        # fp32 buffers: main[g] = full fp32 gradient (micro-batch accumulator and/or the
+        # all-reduce staging buffer); out32[g] = this rank's reduced fp32 shards (ZeRO-1),
+        # bucket i's shard at out32[g][off32[g][i] : + n_i]
+        self.main: dict = {}
+        self.out32: dict = {}
+        self.off32: dict = {}
+        self.a2a = self.fp32 and self.enabled and mode == "reduce_scatter"
+        self._accumulated = False     # accumulate_micro ran in this step
+        if self.fp32:
+            for g in groups:
+                dev = g.grads.device
+                if grad_accum > 1 or (self.enabled and mode == "allreduce"):
+                    self.main[g.name] = torch.zeros(g.numel, device=dev, dtype=torch.float32)
+                if self.a2a:
+                    offs, tot = [], 0
+                    for b in self.buckets[g.name]:
+                        offs.append(tot)
+                        tot += (b.hi - b.lo) // self.dp
+                    self.off32[g.name] = offs
+                    self.out32[g.name] = torch.zeros(tot, device=dev, dtype=torch.float32)
+
+    @property
+    def fp32_accumulation(self) -> bool:
+        """True when micro-batch gradients accumulate in the fp32 main buffer (the model
+        then writes each micro-batch's gradients fresh, ``accumulate=False``)."""
+        return self.fp32 and self.grad_accum > 1
+
+    def accumulate_micro(self, first: bool):
+        """After a NON-final micro-batch's backward: main (=|+=) grads, in fp32."""
+        if not self.fp32_accumulation:
+            return
+        self._accumulated = True
+        for g in self.groups:
+            ops.grad_accum_(self.main[g.name], g.grads, ops.GRAD_SET if first else ops.GRAD_ADD)
+
+    def grad_view(self, group: FlatGroup, lo: int, hi: int) -> torch.Tensor:
+        """The optimizer's gradient operand for flat range [lo, hi) of ``group``: the reduced
+        fp32 shard (fp32 ZeRO-1), the fp32 main buffer (fp32 all-reduce / accumulation), or
+        the bf16 flat gradients."""
+        if self.a2a:
+            for b in self.buckets[group.name]:
+                n = (b.hi - b.lo) // self.dp
+                r0 = b.lo + self._rank() * n
+                if r0 <= lo and hi <= r0 + n:
+                    off = self.off32[group.name][b.idx] + (lo - r0)
+                    return self.out32[group.name][off:off + (hi - lo)]
+            raise ValueError(f"[{lo}, {hi}) is not inside one of this rank's shards")
+        if group.name in self.main:
+            return self.main[group.name][lo:hi]
+        return group.grads[lo:hi]
+
+    def _rank(self) -> int:
+        if not dist.is_initialized():
+            return 0
+        return dist.get_rank(self.dp_group) if self.dp_group is not None else dist.get_rank()
 
     # -- shard geometry (reduce_scatter mode): rank r owns [lo + r*n/dp, lo + (r+1)*n/dp) of each bucket
     def shard_ranges(self, group: FlatGroup, rank: int) -> List[Tuple[int, int]]:
@@ -76,16 +154,31 @@ class GradReducer:
             for b in bl:
                 b.work, b.launched = None, False
         self._pending = []
+        self._accumulated = False
 
     def _launch(self, b: Bucket):
         if b.launched:
             return
         b.launched = True
+        x = b.group.grads[b.lo:b.hi]
+        main = self.main.get(b.group.name)
+        if main is not None:
+            m = main[b.lo:b.hi]
+            if self._accumulated:
+                # earlier micro-batches sit in main: fold the last one in -- one rounding
+                # before an all-to-all send, none when the fp32 buffer itself is reduced /
+                # read by the optimizer
+                ops.grad_accum_(m, x, ops.GRAD_FOLD if self.a2a else ops.GRAD_ADD)
+            elif not self.a2a:
+                ops.grad_accum_(m, x, ops.GRAD_SET)       # fp32 all-reduce / optimizer operand
         if not self.enabled:
             return
-        x = b.group.grads[b.lo:b.hi]
-        if self.mode == "allreduce":
-            b.work = dist.all_reduce(x, group=self.dp_group, async_op=True)
+        self._drain_completed()
+        if self.a2a:
+            b.recv = torch.empty_like(x)
+            b.work = dist.all_to_all_single(b.recv, x, group=self.dp_group, async_op=True)
+        elif self.mode == "allreduce":
+            b.work = dist.all_reduce(main[b.lo:b.hi] if self.fp32 else x, group=self.dp_group, async_op=True)
         else:
             n = (b.hi - b.lo) // self.dp
             r = dist.get_rank(self.dp_group) if self.dp_group is not None else dist.get_rank()
@@ -108,17 +201,32 @@ class GradReducer:
             else:
                 break
 
+    def _complete(self, b: Bucket):
+        if b.work is not None:
+            b.work.wait()
+            b.work = None
+        if b.staged is not None:
+            b.staged[0].copy_(b.staged[1])
+            b.staged = None
+        if b.recv is not None:      # fp32 sum of the dp received shards -> this rank's fp32 shard
+            n = (b.hi - b.lo) // self.dp
+            off = self.off32[b.group.name][b.idx]
+            ops.shard_sum_(b.recv, self.dp, self.out32[b.group.name][off:off + n])
+            b.recv = None
+
+    def _drain_completed(self):
+        """Reduce (and release the receive buffers of) buckets whose all-to-all already
+        finished, oldest first -- a non-blocking poll, so backward never waits here."""
+        while self._pending and self._pending[0].recv is not None and self._pending[0].work.is_completed():
+            self._complete(self._pending.pop(0))
+
     def finish(self):
         """Launch whatever is left and wait for every collective (stream-ordered wait)."""
         for bl in self.buckets.values():
             for b in bl:
                 self._launch(b)
         for b in self._pending:
-            if b.work is not None:
-                b.work.wait()
-            if b.staged is not None:
-                b.staged[0].copy_(b.staged[1])
-                b.staged = None
+            self._complete(b)
         self._pending = []
 
     def all_gather_params(self, overlap: bool = False):

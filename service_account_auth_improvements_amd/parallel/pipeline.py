@@ -107,9 +107,11 @@ class P2P:
 
 
 def one_f_one_b(model: Llama, p2p: P2P, micro_batches: List[Tuple[torch.Tensor, torch.Tensor]],
-                scale: float, on_last_backward=None) -> Optional[torch.Tensor]:
+                scale: float, on_last_backward=None, reducer=None) -> Optional[torch.Tensor]:
     """Run one optimizer step's worth of micro-batches through this stage.
-    Returns the summed (scaled) loss on the last stage, None elsewhere."""
+    Returns the summed (scaled) loss on the last stage, None elsewhere.  With a ``reducer``
+    doing fp32 micro-batch accumulation every backward writes fresh gradients and the
+    non-final ones are added into its fp32 buffer."""
     st = p2p.st
     M = len(micro_batches)
     B, S = micro_batches[0][0].shape
@@ -134,7 +136,10 @@ def one_f_one_b(model: Llama, p2p: P2P, micro_batches: List[Tuple[torch.Tensor, 
         ctx = ctxs.pop(0)
         if n_bwd == M - 1 and on_last_backward is not None:
             on_last_backward(True)
-        gin = model.stage_backward(ctx, g, B, S, accumulate=n_bwd > 0)
+        f32acc = reducer is not None and reducer.fp32_accumulation
+        gin = model.stage_backward(ctx, g, B, S, accumulate=n_bwd > 0 and not f32acc)
+        if reducer is not None and n_bwd < M - 1:
+            reducer.accumulate_micro(first=n_bwd == 0)
         n_bwd += 1
         return gin
 
@@ -176,12 +181,15 @@ class PipelineTrainer:
         self.model.recompute = tcfg.recompute
         self.model.allocate()
         self.reducer = GradReducer(self.model.groups, st.dp_group, st.dp,
-                                   bucket_bytes=tcfg.bucket_mb << 20)
+                                   bucket_bytes=tcfg.bucket_mb << 20,
+                                   reduce_dtype=getattr(tcfg, "grad_reduce", "bf16"),
+                                   grad_accum=tcfg.grad_accum)
         self.opt = FlatAdamW(self.model.groups,
                              AdamWConfig(lr=tcfg.lr, weight_decay=tcfg.weight_decay,
                                          max_grad_norm=tcfg.max_grad_norm),
                              norm_groups=[st.pp_group] if st.pp > 1 else None,
-                             tp_sharded={"matrices": st.tp_group} if st.tp > 1 else None)
+                             tp_sharded={"matrices": st.tp_group} if st.tp > 1 else None,
+                             grad_view=self.reducer.grad_view)
         T = tcfg.micro_batch * tcfg.seq_len
         self.p2p = P2P(st, (T, mcfg.hidden), torch.bfloat16, st.device)
 
@@ -191,7 +199,7 @@ class PipelineTrainer:
     def train_step(self, micro_batches):
         ntok = sum(t.numel() for t, _ in micro_batches)
         self.reducer.start_step()
-        loss = one_f_one_b(self.model, self.p2p, micro_batches, 1.0 / ntok, self._hook)
+        loss = one_f_one_b(self.model, self.p2p, micro_batches, 1.0 / ntok, self._hook, reducer=self.reducer)
         self.reducer.finish()
         self.opt.step(grad_scale=1.0 / self.st.dp)
         return loss

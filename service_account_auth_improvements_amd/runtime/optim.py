@@ -41,7 +41,7 @@ class _Shard:
 class FlatAdamW:
     def __init__(self, groups: List[FlatGroup], cfg: AdamWConfig = AdamWConfig(),
                  shard_ranges: Optional[dict] = None, dp_group=None, norm_groups=None,
-                 tp_sharded: Optional[dict] = None):
+                 tp_sharded: Optional[dict] = None, grad_view=None):
         """``shard_ranges[group.name] = [(lo, hi), ...]`` restricts state to this rank's
         ZeRO-1 shard; None keeps full state.  ``tp_sharded[group.name] = process group``
         marks flat groups whose parameters are split over that (tensor-parallel) group: their
@@ -49,6 +49,7 @@ class FlatAdamW:
         counted once -- so every TP rank clips with the same global norm."""
         self.cfg = cfg
         self.groups = groups
+        self.grad_view = grad_view or (lambda g, lo, hi: g.grads[lo:hi])
         self.step_count = 0
         self.dp_group = dp_group
         # extra groups whose members hold DISJOINT parameters (pipeline stages): the
@@ -74,10 +75,10 @@ class FlatAdamW:
         first, first_tp = True, True
         for sh in self.shards:
             if sh.group.name in self.tp_sharded:
-                ops.sumsq_(sh.group.grads[sh.lo:sh.hi], self._sumsq_tp, accumulate=not first_tp)
+                ops.sumsq_(self.grad_view(sh.group, sh.lo, sh.hi), self._sumsq_tp, accumulate=not first_tp)
                 first_tp = False
             else:
-                ops.sumsq_(sh.group.grads[sh.lo:sh.hi], self._sumsq, accumulate=not first)
+                ops.sumsq_(self.grad_view(sh.group, sh.lo, sh.hi), self._sumsq, accumulate=not first)
                 first = False
         if first:
             self._sumsq.zero_()
@@ -110,7 +111,7 @@ class FlatAdamW:
 
         def upd(sh, a, b):
             ops.adamw_(sh.group.params[a:b], sh.master[a - sh.lo:b - sh.lo], sh.m[a - sh.lo:b - sh.lo],
-                       sh.v[a - sh.lo:b - sh.lo], sh.group.grads[a:b], (b - a) if sh.decay else 0,
+                       sh.v[a - sh.lo:b - sh.lo], self.grad_view(sh.group, a, b), (b - a) if sh.decay else 0,
                        lr, c.betas[0], c.betas[1], c.eps, c.weight_decay, self.step_count,
                        grad_scale, sumsq, c.max_grad_norm)
 

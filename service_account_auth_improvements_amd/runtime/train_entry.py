@@ -66,6 +66,9 @@ def main(argv=None):
         from ..models.mnist import MnistTrainer, SyntheticMnist
         tr = MnistTrainer(st.device)
         data = SyntheticMnist(a.micro_batch, st.device, seed=17, rank=st.dp_rank)
+        if a.resume:
+            from .checkpoint import load_checkpoint
+            tr.step_idx = int(load_checkpoint(a.resume, tr, data=data)["step"])
         return _loop(a, tr, data, st, t_start)
     tcfg = TrainConfig(model=a.model, seq_len=a.seq_len, micro_batch=a.micro_batch, grad_accum=a.grad_accum,
                        zero1=a.zero1, n_layers=a.layers)
@@ -74,29 +77,33 @@ def main(argv=None):
         tr = PipelineTrainer(tcfg, st)
     else:
         tr = Trainer(tcfg, st)
-    if a.resume:
-        from .checkpoint import load_checkpoint
-        load_checkpoint(a.resume, tr)
     data = SyntheticData(tr.mcfg.vocab_size, a.micro_batch, a.seq_len, st.device, seed=17, rank=st.dp_rank)
+    if a.resume:
+        # weights, optimizer state, step, RNG and the data stream position: the resumed job
+        # continues exactly where it stopped instead of replaying batches it already saw
+        from .checkpoint import load_checkpoint
+        meta = load_checkpoint(a.resume, tr, data=data)
+        _event("resumed", path=a.resume, step=int(meta["step"]))
     return _loop(a, tr, data, st, t_start)
 
 
 def _loop(a, tr, data, st, t_start):
     import torch
     _event("init_done", seconds=time.time() - t_start, **getattr(tr, "init_times", {}))
-    for step in range(a.steps):
+    start = int(getattr(tr, "step_idx", 0))
+    for step in range(start, start + a.steps):
         batch = [data.next() for _ in range(a.grad_accum)]
         loss = tr.train_step(batch)
         if st.device.type == "cuda":
             torch.cuda.synchronize()
         lv = float(loss) if loss is not None else None
-        if step == 0:
+        if step == start:
             _event("first_step", loss=lv)
         _event("step", step=step, loss=lv)
         _heartbeat()
     if a.save:
         from .checkpoint import save_checkpoint
-        save_checkpoint(a.save, tr)
+        save_checkpoint(a.save, tr, data=data)
         _event("checkpoint_saved", path=a.save)
     _event("done")
     import torch.distributed as dist

@@ -33,6 +33,11 @@ class TrainConfig:
     # at 8B (profiles/async_optimizer_overlap.txt), so it is off by default.
     async_optimizer: bool = False
     bucket_mb: int = 256
+    # DP gradient reduction precision (parallel/ddp.py): "fp32" sums every rank's bf16
+    # gradient in fp32 (all-to-all + HIP fp32 shard sum under ZeRO-1) and accumulates
+    # micro-batches in fp32; "bf16" reduces in bf16 with RCCL and accumulates in bf16
+    grad_reduce: str = "fp32"
+    force_collectives: bool = False  # run the DP collectives at dp=1 (one-GPU RCCL test)
     lr: float = 3e-4
     weight_decay: float = 0.1
     max_grad_norm: float = 1.0
@@ -60,9 +65,11 @@ class Trainer:
         self._sync()
         self.init_times = {"params_alloc_init_s": time.time() - t0}
         t0 = time.time()
-        mode = "reduce_scatter" if (tcfg.zero1 and self.st.dp > 1) else "allreduce"
+        mode = "reduce_scatter" if (tcfg.zero1 and (self.st.dp > 1 or tcfg.force_collectives)) else "allreduce"
         self.reducer = GradReducer(self.model.groups, self.st.dp_group, self.st.dp,
-                                   bucket_bytes=tcfg.bucket_mb << 20, mode=mode)
+                                   bucket_bytes=tcfg.bucket_mb << 20, mode=mode,
+                                   reduce_dtype=tcfg.grad_reduce, grad_accum=tcfg.grad_accum,
+                                   force_collectives=tcfg.force_collectives)
         # identical replicas: broadcast from the first rank of this DP group (C2)
         if self.st.dp > 1:
             src = self.st.rank - self.st.dp_rank * self.st.tp
@@ -74,7 +81,8 @@ class Trainer:
                              AdamWConfig(lr=tcfg.lr, weight_decay=tcfg.weight_decay,
                                          max_grad_norm=tcfg.max_grad_norm),
                              shard_ranges=shard, dp_group=self.st.dp_group,
-                             tp_sharded={"matrices": self.st.tp_group} if self.st.tp > 1 else None)
+                             tp_sharded={"matrices": self.st.tp_group} if self.st.tp > 1 else None,
+                             grad_view=self.reducer.grad_view)
         self._sync()
         self.init_times["optimizer_state_s"] = time.time() - t0
         self.step_idx = 0
@@ -104,6 +112,17 @@ class Trainer:
         self.reducer.wait_all_params()
         self.opt.wait_all()
 
+    def reduced_grads(self, group) -> torch.Tensor:
+        """fp32 copy of the DP-summed gradient of a flat group as the optimizer saw it in the
+        last step.  Under ZeRO-1 only this rank's shards are reduced: other elements are NaN."""
+        r = self.reducer
+        if r.mode == "reduce_scatter" and r.enabled:
+            out = torch.full((group.numel,), float("nan"), device=group.grads.device)
+            for lo, hi in r.shard_ranges(group, self.st.dp_rank):
+                out[lo:hi] = r.grad_view(group, lo, hi).float()
+            return out
+        return r.grad_view(group, 0, group.numel).float().clone()
+
     @property
     def tokens_per_step(self) -> int:
         """Tokens processed by THIS rank per step."""
@@ -114,10 +133,13 @@ class Trainer:
         ntok = sum(t.numel() for t, _ in micro_batches)
         scale = 1.0 / ntok
         self.reducer.start_step()
+        f32acc = self.reducer.fp32_accumulation
         total = None
         for j, (tok, lab) in enumerate(micro_batches):
             self.model.on_grad_ready = self.reducer.grad_ready if j == n - 1 else None
-            loss = self.model.forward_backward(tok, lab, accumulate=j > 0, scale=scale)
+            loss = self.model.forward_backward(tok, lab, accumulate=j > 0 and not f32acc, scale=scale)
+            if j < n - 1:
+                self.reducer.accumulate_micro(first=j == 0)
             total = loss if total is None else total + loss
         self.model.on_grad_ready = None
         self.reducer.wait_all_params()     # a bucket the forward never read (padding) must land too
@@ -138,6 +160,8 @@ class SyntheticData:
         self.g = torch.Generator(device="cpu").manual_seed(seed * 7919 + rank)
 
     def next(self):
+        """The next micro-batch; the stream position lives in the generator state, which
+        checkpoints save and resume restores (runtime/checkpoint.py)."""
         x = torch.randint(0, self.vocab, (self.mb, self.S + 1), generator=self.g)
         x = x.to(self.device, non_blocking=True)
         return x[:, :-1].contiguous(), x[:, 1:].contiguous()

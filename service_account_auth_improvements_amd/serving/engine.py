@@ -198,7 +198,9 @@ class Engine:
             t = torch.tensor(tokens, dtype=torch.long, device=dev)
             sl = torch.tensor(slots, dtype=torch.int32, device=dev)
             p = torch.tensor(pos, dtype=torch.int32, device=dev)
-            return self._decode_body(t, sl, p, p + 1)
+            out = self._decode_body(t, sl, p, p + 1)
+            self._check_comm()
+            return out
         Bb = next((b for b in BUCKETS if b >= B), None)
         if Bb is None:
             raise ValueError(f"decode batch {B} exceeds the largest graph bucket {BUCKETS[-1]}")
@@ -212,7 +214,19 @@ class Engine:
         gp.copy_(dev_rows[2])
         gl.copy_(dev_rows[2] + 1)
         graph.replay()
+        self._check_comm()
         return out[:B]
+
+    def _check_comm(self):
+        """TP decode: fail the step (and the engine) when a one-shot all-reduce timed out on a
+        peer, instead of returning logits summed from stale peer slots.  The check waits for
+        the step (the scheduler reads the logits on the host right after anyway)."""
+        if self.car is not None:
+            self.car.check()
+
+    @property
+    def healthy(self) -> bool:
+        return self.car is None or not self.car.failed
 
     def release(self, slot: int):
         pass   # slots are overwritten in place; nothing to free

@@ -90,7 +90,10 @@ def create_app(sched: Scheduler, model_name: str, tokenizer=None, registry=None)
 
     @app.get("/v2/health/ready")
     def ready():
-        return jsonify({"ready": True})
+        # a poisoned tensor-parallel communicator (one-shot all-reduce timeout) makes the
+        # predictor unready so the InferenceService pod is taken out of rotation / restarted
+        ok = getattr(sched.e, "healthy", True)
+        return jsonify({"ready": ok}), (200 if ok else 503)
 
     @app.get("/v1/models")
     def models():

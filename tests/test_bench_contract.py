@@ -53,3 +53,24 @@ def test_bench_two_ranks_torchrun_json():
     assert len(recs) == 1, r.stdout          # rank 0 only
     _check(recs[0], 2)
     assert recs[0]["config"]["optimizer_sharding"] == "zero1"
+
+
+def test_bench_self_launches_ranks_without_torchrun():
+    """``bench.py --gpus 2`` with no WORLD_SIZE starts its own 2 ranks (child torch.distributed.run)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", *ARGS],
+                       capture_output=True, text=True, timeout=300, env=env, cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-2000:]
+    recs = _json_lines(r.stdout)
+    assert len(recs) == 1, r.stdout
+    _check(recs[0], 2)
+    assert recs[0]["backend"] == "gloo" and recs[0]["world_size_seen"] == 2
+
+
+def test_bench_refuses_world_size_mismatch():
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", WORLD_SIZE="1", RANK="0",
+               LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", *ARGS],
+                       capture_output=True, text=True, timeout=300, env=env, cwd="/tmp")
+    assert r.returncode != 0 and not _json_lines(r.stdout)

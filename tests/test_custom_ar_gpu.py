@@ -58,3 +58,47 @@ def test_one_shot_allreduce_two_ranks_one_gpu():
         assert err_flag == 0
         assert graph_ok
         assert max_err < 0.05, max_err     # bf16 output rounding of a 2-term sum
+
+
+def _stall_body(rank, world):
+    import time
+
+    import torch.distributed as dist
+
+    from service_account_auth_improvements_amd.parallel.custom_ar import OneShotAllReduce
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    car = OneShotAllReduce(max_bytes=1 << 20, blocks=4)
+    x = torch.ones(4096, device="cuda:0", dtype=torch.bfloat16)
+    car(x.clone())                        # both ranks: a healthy all-reduce first
+    torch.cuda.synchronize()
+    car.check()
+    dist.barrier()
+    raised = False
+    if rank == 0:                          # rank 1 stalls: rank 0's kernel times out on it
+        car(x.clone())
+        torch.cuda.synchronize()
+        try:
+            car.check()
+        except RuntimeError:
+            raised = True
+        # poisoned from now on, even though the error word was cleared by the read
+        try:
+            car.check()
+            sticky = False
+        except RuntimeError:
+            sticky = True
+    else:
+        time.sleep(0.5)
+        sticky = True
+    dist.barrier()
+    car.close()
+    return rank, raised, sticky
+
+
+def test_one_shot_allreduce_peer_stall_raises():
+    """a stalled peer must surface as an error, not as silently wrong sums."""
+    res = run_ranks(_stall_body, world=2, timeout=240)
+    (r0, raised0, sticky0), _ = res
+    assert r0 == 0 and raised0 and sticky0

@@ -141,6 +141,62 @@ def test_adamw_flat_and_sumsq():
     assert torch.equal(p, w.to(torch.bfloat16))
 
 
+def test_adamw_and_sumsq_fp32_gradients():
+    """The fp32-gradient AdamW / sum-of-squares variants (fp32 DP reduction operand)."""
+    torch.manual_seed(6)
+    n = (1 << 20) + 8
+    g = torch.randn(n, device=DEV) * 1e-3
+    w = torch.randn(n, device=DEV)
+    p, m, v = w.to(torch.bfloat16), torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)
+    w2, m2, v2, p2 = w.clone(), m.clone(), v.clone(), p.clone()
+    ss = torch.zeros(1, device=DEV)
+    ops.sumsq_(g, ss)
+    assert math.isclose(float(ss), float(g.double().pow(2).sum()), rel_tol=1e-5)
+    nd = n // 16 * 8        # the kernel's decay boundary has 8-element granularity (groups are 64-aligned)
+    for step in (1, 2):
+        ops.adamw_(p, w, m, v, g, nd, 1e-3, 0.9, 0.95, 1e-8, 0.1, step, 0.25, ss, 1e-4)
+        reference.adamw_(p2, w2, m2, v2, g, nd, 1e-3, 0.9, 0.95, 1e-8, 0.1, step, 0.25, float(ss), 1e-4)
+    assert torch.allclose(w, w2, atol=1e-6, rtol=1e-5)
+    assert torch.allclose(m, m2, atol=1e-9, rtol=1e-5)
+    assert torch.equal(p, w.to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("R", [1, 2, 8])
+def test_shard_sum_fp32(R):
+    """fp32 sum of R received bf16 shards (ZeRO-1 all-to-all reduction), rank order, vs float64."""
+    g = torch.Generator().manual_seed(R)
+    n = 3 * 4096 + 64
+    recv = torch.randn(R * n, generator=g).to(torch.bfloat16)
+    exact = recv.double().view(R, n).sum(0)
+    out = torch.empty(n, device=DEV)
+    ops.shard_sum_(recv.to(DEV), R, out)
+    assert ((out.double().cpu() - exact).abs().max() / exact.abs().max()).item() < 1e-6
+    base = torch.randn(n, generator=g)
+    out2 = base.to(DEV)
+    ops.shard_sum_(recv.to(DEV), R, out2, accumulate=True)
+    assert torch.allclose(out2.cpu().double(), exact + base.double(), rtol=1e-6, atol=1e-6)
+    # bit-identical to the CPU path (same fixed summation order)
+    cpu = torch.empty(n)
+    ops.shard_sum_(recv, R, cpu)
+    assert torch.equal(cpu, out.cpu())
+
+
+def test_grad_accum_modes():
+    g = torch.Generator().manual_seed(11)
+    n = 8192 + 8
+    a = torch.randn(n, generator=g).to(torch.bfloat16)
+    b = torch.randn(n, generator=g).to(torch.bfloat16)
+    main = torch.empty(n, device=DEV)
+    ops.grad_accum_(main, a.to(DEV), ops.GRAD_SET)
+    assert torch.equal(main.cpu(), a.float())
+    ops.grad_accum_(main, b.to(DEV), ops.GRAD_ADD)
+    assert torch.equal(main.cpu(), a.float() + b.float())
+    c = torch.randn(n, generator=g).to(torch.bfloat16)
+    cd = c.to(DEV)
+    ops.grad_accum_(main, cd, ops.GRAD_FOLD)
+    assert torch.equal(cd.cpu(), (a.float() + b.float() + c.float()).to(torch.bfloat16))
+
+
 @pytest.mark.parametrize("vstart,vl,accumulate", [(0, 1000, False), (500, 250, True)])
 def test_embedding_fwd_bwd(vstart, vl, accumulate):
     """K7: gather + deterministic sorted-run scatter-add vs the fp32 CPU reference (ids repeat)."""

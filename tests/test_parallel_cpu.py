@@ -22,7 +22,7 @@ def _dp_body(rank, world, zero1, overlap=True):
     lr = tr.opt.cfg.lr
     tr.opt.cfg.lr = 0.0
     tr.train_step(mine)
-    grads = tr.model.mats.grads.float().clone() / world
+    grads = tr.reduced_grads(tr.model.mats) / world
     tr.opt.cfg.lr = lr
     losses = [float(tr.train_step(mine)) for _ in range(3)]
     tr.sync_params()
@@ -37,7 +37,7 @@ def _single_body(world):
     # one big step = mean over both ranks' batches == accumulate 2 micro-batches
     tr.opt.cfg.lr = 0.0
     tr.train_step(batches)
-    return tr.model.mats.grads.float().clone()
+    return tr.reduced_grads(tr.model.mats)
 
 
 def _close(a, b, tol):

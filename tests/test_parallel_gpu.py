@@ -32,12 +32,7 @@ def _dp_body(rank, world, zero1):
     mine = [(b[0].to(st.device), b[1].to(st.device))]
     tr.opt.cfg.lr = 0.0
     tr.train_step(mine)                      # lr 0: exposes the reduced gradients
-    grads = tr.model.mats.grads.float().clone() / world
-    if zero1:   # after the reduce-scatter only this rank's shard of each bucket is reduced
-        mask = torch.zeros_like(grads, dtype=torch.bool)
-        for lo, hi in tr.reducer.shard_ranges(tr.model.mats, st.dp_rank):
-            mask[lo:hi] = True
-        grads = torch.where(mask, grads, torch.full_like(grads, float("nan")))
+    grads = tr.reduced_grads(tr.model.mats) / world   # ZeRO-1: NaN outside this rank's shards
     tr.opt.cfg.lr = 1e-3
     losses = [float(tr.train_step(mine)) for _ in range(3)]
     tr.sync_params()
@@ -53,7 +48,7 @@ def _single_grads(world):
     tr = Trainer(TrainConfig(model="small", seq_len=256, micro_batch=2, n_layers=2, lr=0.0), st)
     batches = [(x.to(st.device), y.to(st.device)) for x, y in _batches(tr.mcfg.vocab_size, world)]
     tr.train_step(batches)                   # both ranks' batches as 2 accumulated micro-batches
-    return tr.model.mats.grads.float().cpu()
+    return tr.reduced_grads(tr.model.mats).cpu()
 
 
 @pytest.mark.parametrize("zero1", [False, True])
