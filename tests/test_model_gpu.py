@@ -66,3 +66,58 @@ def test_activation_recompute_bit_identical_gpu():
         out.append((losses, tr.model.mats.params.clone(), tr.model.mats.grads.clone()))
     assert out[0][0] == out[1][0]
     assert torch.equal(out[0][1], out[1][1]) and torch.equal(out[0][2], out[1][2])
+
+
+def test_grad_accumulation_at_llama3_8b_widths():
+    """Micro-batch accumulation on the bench's kernels (Llama-3-8B widths, vocab 128256, 2 layers):
+    both the fp32 main-gradient path and the bf16 beta=1 path must equal the float64 sum of the
+    per-micro-batch gradients, parameter by parameter; fp32 to fp32 rounding."""
+    S = 2048
+    st = ParallelState(device=torch.device("cuda:0"))
+    g = torch.Generator().manual_seed(21)
+    mbs = [(torch.randint(0, 128256, (1, S), generator=g).cuda(), torch.randint(0, 128256, (1, S), generator=g).cuda())
+           for _ in range(2)]
+    tr = Trainer(TrainConfig(model="llama3-8b", seq_len=S, micro_batch=1, grad_accum=1, n_layers=2, lr=0.0), st)
+    exact = {}
+    for mb in mbs:
+        tr.train_step([mb])
+        for grp in tr.model.groups:
+            gr = grp.grads.double() / 2
+            exact[grp.name] = gr if grp.name not in exact else exact[grp.name] + gr
+    specs = [(grp.name, s) for grp in tr.model.groups for s in grp.specs]
+    del tr
+    torch.cuda.empty_cache()
+    worst = {}
+    for mode in ("fp32", "bf16"):
+        tr = Trainer(TrainConfig(model="llama3-8b", seq_len=S, micro_batch=1, grad_accum=2, n_layers=2, lr=0.0,
+                                 grad_reduce=mode), st)
+        tr.train_step(mbs)
+        got = {grp.name: tr.reduced_grads(grp).double() for grp in tr.model.groups}
+        errs = {}
+        for gname, s in specs:
+            a = got[gname][s.offset:s.offset + s.numel]
+            b = exact[gname][s.offset:s.offset + s.numel]
+            errs[s.name] = ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
+        worst[mode] = max(errs.items(), key=lambda kv: kv[1])
+        assert worst[mode][1] < (1e-5 if mode == "fp32" else 1.6e-2), (mode, sorted(errs.items(), key=lambda kv: -kv[1])[:5])
+        del tr
+        torch.cuda.empty_cache()
+    print("worst per-parameter relative error:", worst)
+
+
+def test_fp32_and_bf16_accumulation_train_alike_at_llama3_8b_widths():
+    """Same data, AdamW + clipping, 6 steps: the two accumulation precisions track each other."""
+    S = 2048
+    st = ParallelState(device=torch.device("cuda:0"))
+    curves = {}
+    for mode in ("fp32", "bf16"):
+        tr = Trainer(TrainConfig(model="llama3-8b", seq_len=S, micro_batch=1, grad_accum=2, n_layers=2,
+                                 grad_reduce=mode), st)
+        data = SyntheticData(tr.mcfg.vocab_size, 1, S, "cuda:0", seed=1)
+        batches = [[data.next() for _ in range(2)] for _ in range(2)]
+        curves[mode] = [float(tr.train_step(batches[i % 2])) for i in range(6)]
+        del tr
+        torch.cuda.empty_cache()
+    print("loss curves:", curves)
+    for a, b in zip(curves["fp32"], curves["bf16"]):
+        assert abs(a - b) < 0.05 * a, curves
