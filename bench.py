@@ -80,6 +80,8 @@ def main():
     ap.add_argument("--pp", type=int, default=1, help="pipeline parallel degree (1F1B)")
     ap.add_argument("--recompute", action="store_true",
                     help="per-layer activation recomputation (memory plans that need it, e.g. 70B at long S)")
+    ap.add_argument("--head-chunk", type=int, default=4096,
+                    help="LM head + cross-entropy row chunk in tokens (0 = materialise all logits)")
     ap.add_argument("--layers", type=int, default=None, help="DEBUG ONLY: invalid for reporting")
     ap.add_argument("--json-out", default=None)
     a = ap.parse_args()
@@ -101,7 +103,7 @@ def main():
     tcfg = TrainConfig(model=a.model, seq_len=a.seq_len, micro_batch=a.micro_batch,
                        grad_accum=a.grad_accum, zero1=a.zero1, bucket_mb=a.bucket_mb,
                        grad_reduce=a.grad_reduce,
-                       n_layers=a.layers, recompute=a.recompute)
+                       n_layers=a.layers, recompute=a.recompute, head_chunk=a.head_chunk)
     t0 = time.time()
     if a.pp > 1:
         from service_account_auth_improvements_amd.parallel.pipeline import PipelineTrainer
@@ -137,6 +139,7 @@ def main():
     tok_replica = a.micro_batch * a.seq_len * a.grad_accum    # one DP replica (TP/PP ranks share it)
     value = st.dp * tok_replica * a.steps / el
     peak_mem = torch.cuda.max_memory_allocated() / 2**30 if st.device.type == "cuda" else 0.0
+    peak_res = torch.cuda.max_memory_reserved() / 2**30 if st.device.type == "cuda" else 0.0
     flops_tok = tr.mcfg.flops_per_token(a.seq_len)
     losses = [l for l in losses if l is not None]   # only the last pipeline stage computes the loss
     if losses:
@@ -172,12 +175,14 @@ def main():
                 "n_layers": tr.mcfg.n_layers,
                 "attention": "hip",
                 "activation_recompute": a.recompute,
+                "head_chunk": a.head_chunk,
             },
             "backend": backend,
             "world_size_seen": world_seen,
             "tokens_per_s_per_gpu": round(value / world, 1),
             "model_tflops_per_gpu": round(value / world * flops_tok / 1e12, 1),
             "peak_mem_gib": round(peak_mem, 1),
+            "peak_reserved_gib": round(peak_res, 1),
             "init_s": round(init_s, 1),
             "loss_first": round(float(lt[0]), 4),
             "loss_last": round(float(lt[1]), 4),

@@ -143,6 +143,9 @@ class Llama:
         # re-run the layer's forward right before its backward (memory plans where the saved
         # activations do not fit: 70B at long sequence / larger micro-batch)
         self.recompute = False
+        # K5: LM head + cross-entropy in row chunks of this many tokens (0 = one chunk): the
+        # [T, vocab] logits are never materialised -- only one [chunk, vocab] slab at a time
+        self.head_chunk = 4096
         cos, sin = ops.rope_tables(cfg.max_seq, D, cfg.rope_theta)
         self.cos = cos.to(self.device)
         self.sin = sin.to(self.device)
@@ -298,29 +301,59 @@ class Llama:
 
     # ------------------------------------------------------------------ LM head + CE
     def head_fwd(self, r, d, labels: torch.Tensor, scale: float):
-        """Returns (loss_sum fp32 0-d tensor already multiplied by scale, ctx)."""
+        """Final RMSNorm only.  Returns (loss, ctx): ``loss`` is a 0-d fp32 device tensor that
+        :meth:`head_bwd` fills in (already multiplied by ``scale``) -- the logits are produced,
+        consumed and discarded chunk by chunk there (K5), never as one [T, vocab] buffer."""
         cfg = self.cfg
         y, h, rstd = ops.rmsnorm_fwd(r, self.P("final_norm"), cfg.norm_eps, residual=d)
-        logits = torch.mm(y, self.P("lm_head").t())
+        loss = torch.zeros((), device=y.device, dtype=torch.float32)
+        return loss, (h, rstd, y, labels, scale, loss)
+
+    def _ce_chunk(self, logits, labels, scale):
+        """Cross-entropy of one row chunk: loss rows (fp32); ``logits`` now hold dlogits."""
         if self.tp == 1:
             loss_rows, _ = ops.cross_entropy_fused_(logits, labels, scale)
-        else:
-            m, s, xy = ops.cross_entropy_stats(logits, labels, self.vstart)
-            M = m.clone()
-            dist.all_reduce(M, op=dist.ReduceOp.MAX, group=self.st.tp_group)
-            s = s * torch.exp(m - M)
-            sx = torch.stack([s, xy])
-            dist.all_reduce(sx, group=self.st.tp_group)
-            lse = M + torch.log(sx[0])
-            loss_rows = torch.where(labels != -100, lse - sx[1], torch.zeros_like(lse))
-            ops.cross_entropy_grad_(logits, labels, lse, scale, self.vstart)
-        loss = loss_rows.sum() * scale
-        return loss, (h, rstd, y, logits)
+            return loss_rows
+        m, s, xy = ops.cross_entropy_stats(logits, labels, self.vstart)
+        M = m.clone()
+        dist.all_reduce(M, op=dist.ReduceOp.MAX, group=self.st.tp_group)
+        s = s * torch.exp(m - M)
+        sx = torch.stack([s, xy])
+        dist.all_reduce(sx, group=self.st.tp_group)
+        lse = M + torch.log(sx[0])
+        ops.cross_entropy_grad_(logits, labels, lse, scale, self.vstart)
+        return torch.where(labels != -100, lse - sx[1], torch.zeros_like(lse))
 
     def head_bwd(self, ctx, accumulate: bool):
-        h, rstd, y, dlogits = ctx
-        dy = tp_all_reduce(self._mm_dx(dlogits, self.P("lm_head")), self.st)
-        self._mm_into(self.G("lm_head"), dlogits.t(), y, accumulate)
+        """Row-chunked LM head + CE (K5): per chunk of ``head_chunk`` tokens, logits = y W^T
+        (one [chunk, vocab] slab), the fused CE kernel turns them into dlogits in place and
+        writes the loss rows, dy = dlogits W and dW_head (+)= dlogits^T y; the slab is then
+        reused by the next chunk.  At Llama-3-8B, micro-batch 2 x 8192 that replaces a 4.2 GB
+        [16384, 128256] buffer by a 1.05 GB one.  The weight is transposed once per step for
+        the dy products (forward operand layout, see _mm_dx).  dW_head is accumulated across
+        chunks by the dW kernel (bf16 output, fp32 inside each chunk)."""
+        h, rstd, y, labels, scale, loss = ctx
+        W = self.P("lm_head")
+        T = y.shape[0]
+        tc = self.head_chunk if self.head_chunk and self.head_chunk < T else T
+        Wt = ops.transpose(W) if (_DX_T and y.is_cuda and ops.transpose_ok(W)) else None
+        dy = torch.empty_like(y)
+        tot = None
+        for c0 in range(0, T, tc):
+            c1 = min(T, c0 + tc)
+            yc = y[c0:c1]
+            logits = torch.mm(yc, W.t())
+            rows = self._ce_chunk(logits, labels[c0:c1], scale)
+            tot = rows.sum() if tot is None else tot + rows.sum()
+            if Wt is not None:
+                torch.mm(logits, Wt.t(), out=dy[c0:c1])
+            else:
+                torch.mm(logits, W, out=dy[c0:c1])
+            self._mm_into(self.G("lm_head"), logits.t(), yc, accumulate or c0 > 0)
+            del logits, rows
+        loss.add_(tot * scale)
+        del Wt
+        dy = tp_all_reduce(dy, self.st)
         self._ready(self.mats, "lm_head")
         dh = ops.rmsnorm_bwd(dy, h, rstd, self.P("final_norm"), self.G("final_norm"), accumulate)
         return dh

@@ -117,17 +117,16 @@ def one_f_one_b(model: Llama, p2p: P2P, micro_batches: List[Tuple[torch.Tensor, 
     B, S = micro_batches[0][0].shape
     warm = min(st.pp - st.pp_rank - 1, M)
     steady = M - warm
-    ctxs, total = [], None
+    ctxs, total, losses = [], None, []
     n_bwd = 0
 
     def fwd(i, x):
-        nonlocal total
         tok, lab = micro_batches[i]
         inp = tok.reshape(-1) if model.first else x
         out, ctx = model.stage_forward(inp, B, S, lab.reshape(-1), scale)
         ctxs.append(ctx)
         if model.last:
-            total = out if total is None else total + out
+            losses.append(out)     # filled in by this micro-batch's head backward (K5)
             return None
         return out
 
@@ -160,6 +159,8 @@ def one_f_one_b(model: Llama, p2p: P2P, micro_batches: List[Tuple[torch.Tensor, 
         p2p.send_backward(bwd(g))
     if on_last_backward is not None:
         on_last_backward(False)
+    for lv in losses:
+        total = lv if total is None else total + lv
     return total
 
 
@@ -179,6 +180,7 @@ class PipelineTrainer:
         lr = stage_layers(mcfg.n_layers, st.pp, st.pp_rank)
         self.model = Llama(mcfg, st, layer_range=lr, seed=tcfg.seed, full_init=full_init)
         self.model.recompute = tcfg.recompute
+        self.model.head_chunk = getattr(tcfg, "head_chunk", self.model.head_chunk)
         self.model.allocate()
         self.reducer = GradReducer(self.model.groups, st.dp_group, st.dp,
                                    bucket_bytes=tcfg.bucket_mb << 20,

@@ -44,6 +44,7 @@ class TrainConfig:
     seed: int = 1234
     n_layers: Optional[int] = None   # override (tests only; benches must use the full model)
     recompute: bool = False          # per-layer activation recomputation (memory for compute)
+    head_chunk: int = 4096           # K5: LM head + CE row chunk (tokens); 0 = whole micro-batch
 
 
 class Trainer:
@@ -61,6 +62,7 @@ class Trainer:
         t0 = time.time()
         self.model = Llama(mcfg, self.st, seed=tcfg.seed, full_init=full_init)
         self.model.recompute = tcfg.recompute
+        self.model.head_chunk = tcfg.head_chunk
         self.model.allocate(pad_to=self.st.dp * 64 if tcfg.zero1 else 1)
         self._sync()
         self.init_times = {"params_alloc_init_s": time.time() - t0}

@@ -90,3 +90,42 @@ def test_flash_bwd_stream_fork_ordering():
         assert torch.equal(x[:, :Hq * 128], ref[:, :Hq * 128])
         err = ((x - ref).abs().max() / ref.abs().max()).item()
         assert err < 1e-2, err
+
+
+@pytest.mark.parametrize("b,g", [(0, 0), (1, 5)])
+def test_flash_fwd_bwd_at_bench_shape(b, g):
+    """The bench's exact launch: B=2, S=8192, Hq=32, Hkv=8, causal (64 heavy-first q-blocks, the
+    XCD remap and the dK/dV work-item split as in the training step), checked on one (batch,
+    kv-head) GQA group -- its 4 query heads' O / lse / dQ and the group's dK / dV -- against an
+    fp32 autograd reference of that slice."""
+    B, S, Hq, Hkv, D = 2, 8192, 32, 8, 128
+    G = Hq // Hkv
+    sc = 1 / math.sqrt(D)
+    qkv = _qkv(B, S, Hq, Hkv, seed=99)
+    o, lse = torch.ops.kfamd.flash_fwd(qkv, B, S, Hq, Hkv, D, sc, True)
+    do = torch.randn(o.shape, generator=torch.Generator(device="cpu").manual_seed(13)).to(DEV, torch.bfloat16)
+    dqkv = torch.ops.kfamd.flash_bwd(qkv, o, lse, do, B, S, Hq, Hkv, D, sc, True)
+    torch.cuda.synchronize()
+    rows = slice(b * S, (b + 1) * S)
+    heads = range(g * G, (g + 1) * G)
+    q = torch.stack([qkv[rows, h * D:(h + 1) * D] for h in heads]).float().requires_grad_(True)   # [G, S, D]
+    k = qkv[rows, (Hq + g) * D:(Hq + g + 1) * D].float().requires_grad_(True)
+    v = qkv[rows, (Hq + Hkv + g) * D:(Hq + Hkv + g + 1) * D].float().requires_grad_(True)
+    s = (q @ k.t()) * sc
+    mask = torch.ones(S, S, dtype=torch.bool, device=DEV).triu(1)
+    s = s.masked_fill(mask, float("-inf"))
+    lse_ref = torch.logsumexp(s, -1)
+    o_ref = torch.softmax(s, -1) @ v
+    do_s = torch.stack([do[rows, h * D:(h + 1) * D] for h in heads]).float()
+    dq_r, dk_r, dv_r = torch.autograd.grad(o_ref, (q, k, v), do_s)
+    o_s = torch.stack([o[rows, h * D:(h + 1) * D] for h in heads]).float()
+    assert (o_s - o_ref).abs().max().item() < 2e-2
+    lse_s = torch.stack([lse[b, h] for h in heads])
+    assert torch.allclose(lse_s, lse_ref, atol=2e-3, rtol=1e-4)
+
+    def rel(a, r):
+        return ((a - r).abs().max() / r.abs().max()).item()
+    dq_s = torch.stack([dqkv[rows, h * D:(h + 1) * D] for h in heads]).float()
+    assert rel(dq_s, dq_r) < 3e-2
+    assert rel(dqkv[rows, (Hq + g) * D:(Hq + g + 1) * D].float(), dk_r) < 3e-2
+    assert rel(dqkv[rows, (Hq + Hkv + g) * D:(Hq + Hkv + g + 1) * D].float(), dv_r) < 3e-2

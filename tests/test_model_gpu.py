@@ -121,3 +121,23 @@ def test_fp32_and_bf16_accumulation_train_alike_at_llama3_8b_widths():
     print("loss curves:", curves)
     for a, b in zip(curves["fp32"], curves["bf16"]):
         assert abs(a - b) < 0.05 * a, curves
+
+
+def test_chunked_lm_head_at_llama3_8b_vocab_matches_fp32_reference():
+    """K5 at the bench's head shape (hidden 4096, vocab 128256): the row-chunked LM head + fused
+    CE (4 chunks here) against an fp32 autograd reference of the same 1-layer model."""
+    cfg = LlamaConfig.preset("llama3-8b").with_(n_layers=1, max_seq=4096)
+    m = Llama(cfg, ParallelState(device=torch.device("cuda:0")), device="cuda:0", seed=7).allocate()
+    m.head_chunk = 1024
+    torch.manual_seed(0)
+    tok = torch.randint(0, cfg.vocab_size, (1, 4096), device="cuda:0")
+    lab = torch.randint(0, cfg.vocab_size, (1, 4096), device="cuda:0")
+    lab[0, 100:110] = -100
+    loss = m.forward_backward(tok, lab, scale=1.0 / 4086)
+    ref, W = reference_loss(m, tok, lab)
+    ref.backward()
+    assert abs(float(loss) - float(ref)) < 2e-3 * float(ref), (float(loss), float(ref))
+    for n in ("lm_head", "final_norm", "l0.wd", "l0.wqkv", "embed"):
+        g, r = m.G(n).float(), W[n].grad
+        rel = ((g - r).abs().max() / r.abs().max().clamp_min(1e-8)).item()
+        assert rel < 5e-2, (n, rel)
