@@ -17,7 +17,12 @@ API semantics the controllers, webhooks and web apps depend on:
 * finalizers + ``deletionTimestamp``; ownerReference garbage collection with
   Background / Foreground / Orphan propagation (the JWA deletes notebooks in foreground);
   namespace deletion cascades;
-* watches (ADDED / MODIFIED / DELETED) delivered synchronously to subscribers;
+* watches (ADDED / MODIFIED / DELETED) delivered synchronously to subscribers, with
+  kube-apiserver resourceVersion semantics: every event carries a cluster-wide increasing
+  RV (a deletion gets an RV of its own), lists report the RV they were taken at, a watch
+  started from an RV first replays the retained event history after it (a bounded ring,
+  like the watch cache) and is refused with 410 Gone/Expired when that history no longer
+  reaches back far enough -- the client then re-lists;
 * admission chain: mutating then validating webhooks (in-process callables receiving
   an AdmissionReview-shaped request), e.g. the PodDefault mutator and the PVCViewer
   defaulter/validator;
@@ -28,7 +33,6 @@ from __future__ import annotations
 import copy
 import datetime as _dt
 import fnmatch
-import itertools
 import json
 import threading
 import uuid
@@ -61,6 +65,11 @@ def Conflict(msg=""):
 
 def Invalid(msg=""):
     return ApiError(422, "Invalid", msg)
+
+
+def Gone(msg=""):
+    """410: the requested resourceVersion is older than the retained watch history."""
+    return ApiError(410, "Expired", msg)
 
 
 def Forbidden(msg=""):
@@ -385,18 +394,39 @@ class Webhook:
     failure_policy: str = "Fail"
 
 
+class _RVCounter:
+    """Cluster-wide resourceVersion sequence (``next()`` issues, ``value`` = last issued)."""
+
+    def __init__(self):
+        self.value = 0
+
+    def __iter__(self):
+        return self
+
+    def __next__(self) -> int:
+        self.value += 1
+        return self.value
+
+
 class APIServer:
     """Thread-safe in-memory API server. All returned objects are deep copies."""
 
-    def __init__(self, types: Optional[List[ResourceType]] = None):
+    HISTORY = 4096        # retained watch events (kube-apiserver's watch cache window)
+
+    def __init__(self, types: Optional[List[ResourceType]] = None, history: Optional[int] = None):
         self._lock = threading.RLock()
         self._types: Dict[Tuple[str, str], ResourceType] = {}
         self._by_plural: Dict[Tuple[str, str], ResourceType] = {}
         for t in (types or BUILTIN_TYPES):
             self.register_type(t)
         self._store: Dict[Tuple[str, str], Dict[Tuple[str, str], dict]] = {}
-        self._rv = itertools.count(1)
+        self._rv = _RVCounter()
         self._watchers: List[Tuple[Optional[str], Optional[str], WatchFn]] = []
+        # event history for resourceVersion-based watches: (rv, type, group, kind, obj)
+        self._history_max = history or self.HISTORY
+        self._history: List[Tuple[int, str, str, str, dict]] = []
+        self._history_head = 0          # index of the oldest retained event
+        self._history_floor = 0         # rv of the newest DROPPED event
         self._schemas: Dict[Tuple[str, str], Dict[str, Optional[dict]]] = {}
         self.mutating: List[Webhook] = []
         self.validating: List[Webhook] = []
@@ -464,7 +494,28 @@ class APIServer:
     def _key(t: ResourceType, ns: Optional[str], name: str):
         return (ns if t.namespaced else "", name)
 
+    @property
+    def resource_version(self) -> str:
+        """The latest issued resourceVersion (what a list taken now reports)."""
+        return str(self._rv.value)
+
+    def _record(self, etype: str, t: ResourceType, obj: dict):
+        h = self._history
+        h.append((int(obj["metadata"]["resourceVersion"]), etype, t.group, t.kind, obj))
+        if len(h) - self._history_head > self._history_max:
+            self._history_floor = h[self._history_head][0]
+            self._history_head += 1
+            if self._history_head > self._history_max:      # compact the ring occasionally
+                del h[:self._history_head]
+                self._history_head = 0
+
     def _emit(self, etype: str, t: ResourceType, obj: dict):
+        if etype == "DELETED":      # a deletion is a write of its own: fresh resourceVersion
+            obj = copy.deepcopy(obj)
+            obj["metadata"]["resourceVersion"] = str(next(self._rv))
+        obj = copy.deepcopy(obj)
+        obj["apiVersion"] = t.api_version()
+        self._record(etype, t, obj)
         for g, k, fn in list(self._watchers):
             if (g is None or g == t.group) and (k is None or k == t.kind):
                 try:
@@ -473,11 +524,24 @@ class APIServer:
                     import logging
                     logging.getLogger("apiserver").exception("watch handler failed")
 
-    def watch(self, fn: WatchFn, api_version: Optional[str] = None, kind: Optional[str] = None):
-        """Subscribe to events; returns an unsubscribe callable."""
+    def watch(self, fn: WatchFn, api_version: Optional[str] = None, kind: Optional[str] = None,
+              resource_version: Optional[str] = None):
+        """Subscribe to events; returns an unsubscribe callable.
+
+        ``resource_version`` (an RV from a list or an earlier event): the retained events
+        newer than it are delivered first, then live events -- atomically, so none is
+        missed or repeated.  Raises 410 Gone when events after it were already dropped.
+        None / "" / "0" start from now."""
         g = split_api_version(api_version)[0] if api_version else None
         entry = (g, kind, fn)
         with self._lock:
+            if resource_version not in (None, "", "0"):
+                rv = int(resource_version)
+                if rv < self._history_floor:
+                    raise Gone(f"too old resource version: {rv} ({self._history_floor})")
+                for erv, et, eg, ek, o in self._history[self._history_head:]:
+                    if erv > rv and (g is None or g == eg) and (kind is None or kind == ek):
+                        fn(et, copy.deepcopy(o))
             self._watchers.append(entry)
 
         def cancel():
@@ -591,6 +655,12 @@ class APIServer:
             out = copy.deepcopy(o)
         out["apiVersion"] = api_version if "/" in api_version or not t.group else t.api_version()
         return out
+
+    def list_with_rv(self, api_version: str, kind: str, namespace: Optional[str] = None,
+                     label_selector=None, field_selector: Optional[str] = None) -> Tuple[List[dict], str]:
+        """A list and the resourceVersion it is consistent with (watch from it to follow)."""
+        with self._lock:
+            return self.list(api_version, kind, namespace, label_selector, field_selector), self.resource_version
 
     def list(self, api_version: str, kind: str, namespace: Optional[str] = None,
              label_selector=None, field_selector: Optional[str] = None) -> List[dict]:

@@ -33,7 +33,7 @@ class Client:
     def update_status(self, obj) -> dict: ...
     def patch(self, api_version, kind, name, namespace, patch, patch_type="merge", subresource=None) -> dict: ...
     def delete(self, api_version, kind, name, namespace=None, propagation="Background") -> dict: ...
-    def watch(self, fn, api_version=None, kind=None) -> Callable[[], None]: ...
+    def watch(self, fn, api_version=None, kind=None, resource_version=None) -> Callable[[], None]: ...
 
     # helpers shared by all implementations
     def get_or_none(self, api_version, kind, name, namespace=None):
@@ -88,8 +88,11 @@ class InMemoryClient(Client):
     def delete(self, api_version, kind, name, namespace=None, propagation="Background"):
         return self.server.delete(api_version, kind, name, namespace, propagation)
 
-    def watch(self, fn, api_version=None, kind=None):
-        return self.server.watch(fn, api_version, kind)
+    def list_with_rv(self, api_version, kind, namespace=None, label_selector=None, field_selector=None):
+        return self.server.list_with_rv(api_version, kind, namespace, label_selector, field_selector)
+
+    def watch(self, fn, api_version=None, kind=None, resource_version=None):
+        return self.server.watch(fn, api_version, kind, resource_version=resource_version)
 
 
 class RestClient(Client):
@@ -164,7 +167,8 @@ class RestClient(Client):
     def get(self, api_version, kind, name, namespace=None):
         return self._req("GET", self._path(api_version, kind, namespace, name))
 
-    def list(self, api_version, kind, namespace=None, label_selector=None, field_selector=None):
+    def list_with_rv(self, api_version, kind, namespace=None, label_selector=None, field_selector=None):
+        """Items plus the list's ``metadata.resourceVersion`` (the point to watch from)."""
         if isinstance(label_selector, dict):
             parts = [f"{k}={v}" for k, v in (label_selector.get("matchLabels") or {}).items()]
             label_selector = ",".join(parts)
@@ -174,7 +178,10 @@ class RestClient(Client):
         for it in items:
             it.setdefault("apiVersion", api_version)
             it.setdefault("kind", kind)
-        return items
+        return items, (out.get("metadata") or {}).get("resourceVersion")
+
+    def list(self, api_version, kind, namespace=None, label_selector=None, field_selector=None):
+        return self.list_with_rv(api_version, kind, namespace, label_selector, field_selector)[0]
 
     def create(self, obj, dry_run=False):
         ns = obj.get("metadata", {}).get("namespace")
@@ -201,21 +208,81 @@ class RestClient(Client):
         return self._req("DELETE", self._path(api_version, kind, namespace, name),
                          {"kind": "DeleteOptions", "apiVersion": "v1", "propagationPolicy": propagation})
 
-    def watch(self, fn, api_version=None, kind=None):
-        """Streaming watch in a daemon thread; returns a cancel callable."""
+    WATCH_TIMEOUT = 300        # seconds per watch request before it is re-opened from the last RV
+
+    def watch(self, fn, api_version=None, kind=None, resource_version=None):
+        """List-then-watch with kube-apiserver resourceVersion semantics (client-go reflector):
+
+        * before returning, the current state is LISTed (unless ``resource_version`` is given)
+          and the stream is opened from that list's RV, so every change made after
+          ``watch()`` returns is delivered -- also one that happens before the streaming
+          connection is up (the server replays its event history from that RV);
+        * a dropped connection or a ``timeoutSeconds`` end re-opens the watch from the last
+          RV seen (events or BOOKMARKs);
+        * a 410 Expired (the RV fell out of the server's history) triggers a RE-LIST, diffed
+          against the objects this watch knows about, so the handler gets the ADDED /
+          MODIFIED / DELETED events it missed instead of silently losing them.
+
+        Runs in a daemon thread; returns a cancel callable."""
         stop = threading.Event()
+        known: dict = {}          # (namespace, name) -> last object seen
+        state = {"rv": resource_version}
+
+        def key(o):
+            m = o.get("metadata", {})
+            return (m.get("namespace"), m.get("name"))
+
+        def relist(deliver: bool):
+            items, rv = self.list_with_rv(api_version, kind)
+            seen = set()
+            for o in items:
+                k = key(o)
+                seen.add(k)
+                old = known.get(k)
+                known[k] = o
+                if deliver and (old is None or old["metadata"].get("resourceVersion") !=
+                                o["metadata"].get("resourceVersion")):
+                    fn("ADDED" if old is None else "MODIFIED", o)
+            for k in [k for k in known if k not in seen]:
+                o = known.pop(k)
+                if deliver:
+                    fn("DELETED", o)
+            state["rv"] = rv
+
+        if state["rv"] is None:
+            relist(deliver=False)
 
         def run():
             while not stop.is_set():
                 try:
-                    resp = self._req("GET", self._path(api_version, kind), params={"watch": "true"}, stream=True)
+                    resp = self._req("GET", self._path(api_version, kind),
+                                     params={"watch": "true", "resourceVersion": state["rv"],
+                                             "allowWatchBookmarks": "true",
+                                             "timeoutSeconds": str(self.WATCH_TIMEOUT)}, stream=True)
+                    expired = False
                     for line in resp:
                         if stop.is_set():
                             break
                         line = line.strip()
-                        if line:
-                            ev = json.loads(line)
-                            fn(ev["type"], ev["object"])
+                        if not line:
+                            continue
+                        ev = json.loads(line)
+                        et, obj = ev["type"], ev["object"]
+                        if et == "ERROR":
+                            expired = obj.get("code") == 410
+                            break
+                        rv = (obj.get("metadata") or {}).get("resourceVersion")
+                        if rv:
+                            state["rv"] = rv
+                        if et == "BOOKMARK":
+                            continue
+                        if et == "DELETED":
+                            known.pop(key(obj), None)
+                        else:
+                            known[key(obj)] = obj
+                        fn(et, obj)
+                    if expired and not stop.is_set():
+                        relist(deliver=True)
                 except Exception:
                     if stop.wait(1.0):
                         break

@@ -11,6 +11,7 @@ from __future__ import annotations
 import json
 import queue
 import threading
+import time
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from urllib.parse import parse_qs, urlparse
 
@@ -33,6 +34,9 @@ def _parse(path: str):
     name = rest[1] if len(rest) > 1 else None
     sub = rest[2] if len(rest) > 2 else None
     return g, v, ns, plural, name, sub
+
+
+BOOKMARK_PERIOD = 5.0     # seconds between BOOKMARK events on an idle watch that asked for them
 
 
 def make_handler(server: APIServer):
@@ -70,13 +74,15 @@ def make_handler(server: APIServer):
                 av = f"{g}/{v}" if g else v
                 dry = q.get("dryRun") == "All"
                 if method == "GET" and q.get("watch") in ("true", "1"):
-                    return self._watch(av, t.kind, ns)
+                    return self._watch(av, t.kind, ns, q.get("resourceVersion"),
+                                       q.get("allowWatchBookmarks") in ("true", "1"),
+                                       float(q["timeoutSeconds"]) if q.get("timeoutSeconds") else None)
                 if method == "GET" and name:
                     return self._send(200, server.get(av, t.kind, name, ns))
                 if method == "GET":
-                    items = server.list(av, t.kind, ns, q.get("labelSelector"), q.get("fieldSelector"))
+                    items, rv = server.list_with_rv(av, t.kind, ns, q.get("labelSelector"), q.get("fieldSelector"))
                     return self._send(200, {"apiVersion": av, "kind": f"{t.kind}List", "items": items,
-                                            "metadata": {}})
+                                            "metadata": {"resourceVersion": rv}})
                 if method == "POST":
                     body = self._body()
                     body.setdefault("apiVersion", av)
@@ -104,26 +110,44 @@ def make_handler(server: APIServer):
                 self._send(400, {"kind": "Status", "status": "Failure", "code": 400,
                                  "reason": "BadRequest", "message": str(e)})
 
-        def _watch(self, av, kind, ns):
+        def _chunk(self, ev):
+            data = (json.dumps(ev) + "\n").encode()
+            self.wfile.write(f"{len(data):x}\r\n".encode() + data + b"\r\n")
+            self.wfile.flush()
+
+        def _watch(self, av, kind, ns, rv, bookmarks, timeout):
             qq: "queue.Queue" = queue.Queue()
 
             def fn(etype, obj):
                 if ns is None or obj.get("metadata", {}).get("namespace") == ns:
                     qq.put({"type": etype, "object": obj})
-            cancel = server.watch(fn, av, kind)
             self.send_response(200)
             self.send_header("Content-Type", "application/json")
             self.send_header("Transfer-Encoding", "chunked")
             self.end_headers()
             try:
-                while True:
+                cancel = server.watch(fn, av, kind, resource_version=rv)
+            except ApiError as e:       # 410 Expired: one ERROR event, then the stream ends
+                try:
+                    self._chunk({"type": "ERROR", "object": e.status()})
+                    self.wfile.write(b"0\r\n\r\n")
+                except (BrokenPipeError, ConnectionResetError):
+                    pass
+                return
+            deadline = time.time() + timeout if timeout else None
+            try:
+                while deadline is None or time.time() < deadline:
+                    wait = BOOKMARK_PERIOD if deadline is None else max(0.01, min(BOOKMARK_PERIOD, deadline - time.time()))
                     try:
-                        ev = qq.get(timeout=30)
+                        ev = qq.get(timeout=wait)
                     except queue.Empty:
+                        if bookmarks:
+                            self._chunk({"type": "BOOKMARK", "object": {
+                                "apiVersion": av, "kind": kind,
+                                "metadata": {"resourceVersion": server.resource_version}}})
                         continue
-                    data = (json.dumps(ev) + "\n").encode()
-                    self.wfile.write(f"{len(data):x}\r\n".encode() + data + b"\r\n")
-                    self.wfile.flush()
+                    self._chunk(ev)
+                self.wfile.write(b"0\r\n\r\n")       # timeoutSeconds reached: clean end
             except (BrokenPipeError, ConnectionResetError):
                 pass
             finally:

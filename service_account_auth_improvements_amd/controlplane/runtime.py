@@ -6,7 +6,15 @@ controller in this repo.
   controller owner of the object), or an arbitrary map function, each with an optional
   predicate -- the shapes used by the reference controllers (e.g. the Notebook
   controller watches Pods labelled ``notebook-name`` and re-emits Pod/STS Events).
-* ``Manager``: de-duplicating work queue, per-item exponential back-off on error
+* ``Informer``: one shared list+watch per watched kind (LIST, then a watch from the list's
+  resourceVersion, so no event between them is lost), keeping a local object store.
+  Controllers added to a caching Manager read through :class:`CachedClient`: ``get`` /
+  ``list`` of watched kinds are served from the informer stores (controller-runtime's
+  cache-backed client), writes and other kinds go to the API server.
+* ``Manager``: de-duplicating work queue with client-go semantics in O(1) (FIFO deque +
+  dirty set + processing set: a key is never reconciled by two workers at once, and a key
+  re-added while in flight runs again once after it finishes), per-item exponential
+  back-off on error
   (5 ms doubling to 1000 s, controller-runtime's default rate limiter),
   ``RequeueAfter`` timers, worker threads, optional leader election through a
   ``coordination.k8s.io/v1`` Lease, ``/healthz`` ``/readyz`` ``/metrics`` endpoints
@@ -14,15 +22,17 @@ controller in this repo.
 """
 from __future__ import annotations
 
+import copy
 import heapq
 import logging
 import threading
 import time
+from collections import deque
 from dataclasses import dataclass, field
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from typing import Callable, Dict, List, Optional, Tuple
 
-from .apiserver import ApiError, now_rfc3339
+from .apiserver import ApiError, NotFound, fields_match, labels_match, now_rfc3339, split_api_version
 from .client import Client
 
 log = logging.getLogger("controlplane.runtime")
@@ -101,15 +111,164 @@ class RateLimiter:
         self.failures.pop(key, None)
 
 
+class WorkQueue:
+    """client-go ``workqueue`` semantics, every operation O(1): ``add`` de-duplicates (a key
+    waiting in the queue is not queued twice); a key added while a worker processes it is
+    marked dirty and re-queued by ``done``, so it is never processed concurrently and never
+    lost."""
+
+    def __init__(self):
+        self._q: deque = deque()
+        self._dirty: set = set()
+        self._processing: set = set()
+
+    def add(self, item):
+        if item in self._dirty:
+            return
+        self._dirty.add(item)
+        if item not in self._processing:
+            self._q.append(item)
+
+    def get(self):
+        """Next item to process (marked in flight) or None."""
+        if not self._q:
+            return None
+        item = self._q.popleft()
+        self._processing.add(item)
+        self._dirty.discard(item)
+        return item
+
+    def done(self, item):
+        self._processing.discard(item)
+        if item in self._dirty:
+            self._q.append(item)
+
+    def __len__(self):
+        return len(self._q)
+
+    def __contains__(self, item):
+        return item in self._dirty
+
+
+class Informer:
+    """Shared list+watch of one kind with a local store (client-go SharedIndexInformer)."""
+
+    def __init__(self, client: Client, api_version: str, kind: str):
+        self.client, self.api_version, self.kind = client, api_version, kind
+        self.group = split_api_version(api_version)[0]
+        self.store: Dict[Tuple[Optional[str], str], dict] = {}
+        self.handlers: List[Callable[[str, dict], None]] = []
+        self.synced = False
+        self._lock = threading.RLock()
+        self._cancel: Optional[Callable] = None
+
+    @staticmethod
+    def _key(o: dict):
+        m = o.get("metadata", {})
+        return (m.get("namespace"), m["name"])
+
+    def _on_event(self, et: str, obj: dict):
+        with self._lock:
+            if et == "DELETED":
+                self.store.pop(self._key(obj), None)
+            else:
+                self.store[self._key(obj)] = obj
+        for h in list(self.handlers):
+            h(et, obj)
+
+    def start(self):
+        lister = getattr(self.client, "list_with_rv", None)
+        if lister is not None:
+            items, rv = lister(self.api_version, self.kind)
+        else:
+            items, rv = self.client.list(self.api_version, self.kind), None
+        with self._lock:
+            for o in items:
+                self.store[self._key(o)] = o
+            self.synced = True
+        try:
+            self._cancel = self.client.watch(self._on_event, self.api_version, self.kind, resource_version=rv)
+        except TypeError:       # a client without resourceVersion support
+            self._cancel = self.client.watch(self._on_event, self.api_version, self.kind)
+        return self
+
+    def stop(self):
+        if self._cancel:
+            self._cancel()
+
+    def get(self, name: str, namespace: Optional[str]) -> Optional[dict]:
+        with self._lock:
+            o = self.store.get((namespace, name))
+            if o is None and namespace is not None:       # cluster-scoped kind asked with a namespace
+                o = self.store.get((None, name))
+            return copy.deepcopy(o) if o is not None else None
+
+    def list(self, namespace=None, label_selector=None, field_selector=None) -> List[dict]:
+        with self._lock:
+            items = [o for (ns, _), o in sorted(self.store.items(), key=lambda kv: (kv[0][0] or "", kv[0][1]))
+                     if (namespace is None or ns == namespace or ns is None)]
+            return [copy.deepcopy(o) for o in items
+                    if labels_match(o.get("metadata", {}).get("labels"), label_selector)
+                    and fields_match(o, field_selector)]
+
+
+class CachedClient(Client):
+    """Cache-backed reads for the kinds the manager watches; everything else is delegated."""
+
+    def __init__(self, live: Client, informers: Dict[Tuple[str, str], Informer]):
+        self.live = live
+        self.informers = informers
+
+    def _inf(self, api_version, kind) -> Optional[Informer]:
+        inf = self.informers.get((split_api_version(api_version)[0], kind))
+        return inf if inf is not None and inf.synced else None
+
+    def get(self, api_version, kind, name, namespace=None):
+        inf = self._inf(api_version, kind)
+        if inf is None:
+            return self.live.get(api_version, kind, name, namespace)
+        o = inf.get(name, namespace)
+        if o is None:
+            raise NotFound(f'{kind} "{name}" not found')
+        return o
+
+    def list(self, api_version, kind, namespace=None, label_selector=None, field_selector=None):
+        inf = self._inf(api_version, kind)
+        if inf is None:
+            return self.live.list(api_version, kind, namespace, label_selector, field_selector)
+        return inf.list(namespace, label_selector, field_selector)
+
+    def create(self, obj, dry_run=False):
+        return self.live.create(obj, dry_run)
+
+    def update(self, obj, dry_run=False):
+        return self.live.update(obj, dry_run)
+
+    def update_status(self, obj):
+        return self.live.update_status(obj)
+
+    def patch(self, api_version, kind, name, namespace, patch, patch_type="merge", subresource=None):
+        return self.live.patch(api_version, kind, name, namespace, patch, patch_type, subresource)
+
+    def delete(self, api_version, kind, name, namespace=None, propagation="Background"):
+        return self.live.delete(api_version, kind, name, namespace, propagation)
+
+    def watch(self, fn, api_version=None, kind=None, resource_version=None):
+        return self.live.watch(fn, api_version, kind, resource_version=resource_version)
+
+    def __getattr__(self, name):          # server-specific extras of the live client
+        return getattr(self.live, name)
+
+
 class Manager:
     def __init__(self, client: Client, leader_election: bool = False, leader_election_id: str = "",
                  leader_election_namespace: str = "kubeflow", identity: Optional[str] = None,
-                 metrics_registry=None, clock: Callable[[], float] = time.time):
+                 metrics_registry=None, clock: Callable[[], float] = time.time, cache: bool = True):
         self.client = client
         self.controllers: Dict[str, Controller] = {}
-        self._queue: List[Tuple[str, Request]] = []
-        self._queued: set = set()
-        self._processing: set = set()
+        self.wq = WorkQueue()
+        self.informers: Dict[Tuple[str, str], Informer] = {}
+        self.cache = cache
         self._timers: List[Tuple[float, int, str, Request]] = []
         self._seq = 0
         self._cv = threading.Condition()
@@ -129,6 +288,20 @@ class Manager:
         self._http = None
 
     # --- wiring
+    def informer(self, api_version: str, kind: str) -> Informer:
+        """The shared informer of a kind (started on first use)."""
+        key = (split_api_version(api_version)[0], kind)
+        inf = self.informers.get(key)
+        if inf is None:
+            inf = Informer(self.client, api_version, kind)
+            self.informers[key] = inf
+            try:
+                inf.start()
+            except ApiError:
+                inf.synced = False
+            self._cancels.append(inf.stop)
+        return inf
+
     def add(self, ctrl: Controller):
         self.controllers[ctrl.name] = ctrl
         for src in ctrl.sources():
@@ -137,13 +310,13 @@ class Manager:
                     return
                 for req in src.mapper(et, obj):
                     self.enqueue(cname, req)
-            self._cancels.append(self.client.watch(handler, src.api_version, src.kind))
-            # informer initial LIST: objects that existed before the watch started
-            try:
-                for obj in self.client.list(src.api_version, src.kind):
-                    handler("ADDED", obj)
-            except ApiError:
-                pass
+            inf = self.informer(src.api_version, src.kind)
+            inf.handlers.append(handler)
+            # objects that existed before this controller joined the informer
+            for obj in inf.list():
+                handler("ADDED", obj)
+        if self.cache and not isinstance(ctrl.client, CachedClient):
+            ctrl.client = CachedClient(ctrl.client, self.informers)
         return self
 
     def enqueue(self, cname: str, req: Request, after: float = 0.0):
@@ -151,35 +324,28 @@ class Manager:
             if after > 0:
                 self._seq += 1
                 heapq.heappush(self._timers, (self.clock() + after, self._seq, cname, req))
-            elif (cname, req) not in self._queued:
-                self._queued.add((cname, req))
-                self._queue.append((cname, req))
+            else:
+                self.wq.add((cname, req))
             self._cv.notify()
 
     def _pop_due(self):
         now = self.clock()
         while self._timers and self._timers[0][0] <= now:
             _, _, c, r = heapq.heappop(self._timers)
-            if (c, r) not in self._queued:
-                self._queued.add((c, r))
-                self._queue.append((c, r))
+            self.wq.add((c, r))
 
     def _process_one(self) -> bool:
         with self._cv:
             self._pop_due()
-            # a key is never reconciled by two workers at once (client-go workqueue
-            # "processing" set): skip keys in flight, they are re-queued as dirty
-            idx = next((i for i, it in enumerate(self._queue) if it not in self._processing), None)
-            if idx is None:
+            item = self.wq.get()
+            if item is None:
                 return False
-            cname, req = self._queue.pop(idx)
-            self._queued.discard((cname, req))
-            self._processing.add((cname, req))
+        cname, req = item
         try:
             return self._reconcile_one(cname, req)
         finally:
             with self._cv:
-                self._processing.discard((cname, req))
+                self.wq.done(item)
                 self._cv.notify()
 
     def _reconcile_one(self, cname, req) -> bool:
@@ -212,9 +378,7 @@ class Manager:
                     break
                 # pull the earliest due timer forward
                 t = heapq.heappop(self._timers)
-                if (t[2], t[3]) not in self._queued:
-                    self._queued.add((t[2], t[3]))
-                    self._queue.append((t[2], t[3]))
+                self.wq.add((t[2], t[3]))
         return n
 
     def enqueue_all(self, cname: str, api_version: str, kind: str):
