@@ -142,7 +142,10 @@ BUILTIN_TYPES = [
 
 
 def _check_schema(v, sch: dict, path: str, errs: List[str]):
-    """Structural openAPI subset used by CRD validation."""
+    """Structural openAPI subset used by CRD validation: type, required, properties,
+    additionalProperties (maps), items, enum, minimum, minLength, minItems, maxItems, pattern,
+    x-kubernetes-int-or-string and x-kubernetes-preserve-unknown-fields (an object that declares
+    properties AND preserves unknown fields validates the declared ones and keeps the rest)."""
     if not sch or sch.get("x-kubernetes-preserve-unknown-fields") and "properties" not in sch:
         return
     if sch.get("x-kubernetes-int-or-string"):
@@ -163,6 +166,14 @@ def _check_schema(v, sch: dict, path: str, errs: List[str]):
         errs.append(f"{path}: must be >= {sch['minimum']}")
     if "minLength" in sch and isinstance(v, str) and len(v) < sch["minLength"]:
         errs.append(f"{path}: must be at least {sch['minLength']} characters")
+    if "minItems" in sch and isinstance(v, list) and len(v) < sch["minItems"]:
+        errs.append(f"{path}: must have at least {sch['minItems']} items")
+    if "maxItems" in sch and isinstance(v, list) and len(v) > sch["maxItems"]:
+        errs.append(f"{path}: must have at most {sch['maxItems']} items")
+    if "pattern" in sch and isinstance(v, str):
+        import re
+        if not re.search(sch["pattern"], v):
+            errs.append(f"{path}: must match {sch['pattern']!r}")
     if typ == "object" and isinstance(v, dict):
         for r in sch.get("required") or []:
             if r not in v:
@@ -171,6 +182,11 @@ def _check_schema(v, sch: dict, path: str, errs: List[str]):
         for k, sub in props.items():
             if k in v and v[k] is not None:
                 _check_schema(v[k], sub, f"{path}.{k}", errs)
+        extra = sch.get("additionalProperties")
+        if isinstance(extra, dict):        # map types (resources.limits, nodeSelector, ...)
+            for k, x in v.items():
+                if k not in props:
+                    _check_schema(x, extra, f"{path}.{k}", errs)
     if typ == "array" and isinstance(v, list) and sch.get("items"):
         for i, x in enumerate(v):
             _check_schema(x, sch["items"], f"{path}[{i}]", errs)

@@ -3,10 +3,16 @@ kustomize renderer (``build``) used by the local cluster and the manifest tests.
 
 Reference layout: components/*/config/{crd,default,manager,rbac,overlays/{kubeflow,
 standalone}} and components/*/manifests/{base,overlays/{istio,cert-manager,kserve}}.
-The group/version/kind/plural/scope/served/storage of every CRD matches the reference
-(API compatibility); the schemas are this repo's own structural schemas -- PodSpec-typed
-fields are ``x-kubernetes-preserve-unknown-fields`` objects -- carrying the validations
-the controllers depend on (required fields, enums, minimums).
+The group / versions (in the reference's order) / served / storage / kind / plural / scope of
+every reference CRD match the reference (tests/test_crd_compat.py pins them against a table
+transcribed from the reference CRD files), e.g. Notebook serves v1 (storage), v1alpha1 and
+v1beta1 (``notebook-controller/config/crd/bases/kubeflow.org_notebooks.yaml:18,3144,3147,6276``).
+The schemas are this repo's own structural schemas: the core/v1 PodSpec subset the
+controllers and web apps read (containers, initContainers, volumes, env/envFrom, resources,
+ports, volumeMounts, tolerations, affinity, nodeSelector, securityContext, ...) is typed,
+anything outside it is preserved (``x-kubernetes-preserve-unknown-fields``), and the
+Notebook CRD carries the reference's ``config/crd/patches/validation_patches.yaml``
+constraints (containers minItems 1; every container requires name and image).
 
 CLI::
 
@@ -49,7 +55,93 @@ INT = {"type": "integer"}
 BOOL = {"type": "boolean"}
 CONDITIONS = arr(obj({"type": STR, "status": STR, "reason": STR, "message": STR,
                       "lastProbeTime": STR, "lastTransitionTime": STR, "lastUpdateTime": STR}))
-POD_TEMPLATE = obj({"metadata": OBJ_ANY, "spec": OBJ_ANY})
+INT_OR_STR = {"x-kubernetes-int-or-string": True}
+STR_MAP = {"type": "object", "additionalProperties": STR}
+QUANTITY_MAP = {"type": "object", "additionalProperties": INT_OR_STR}
+
+
+def open_obj(props=None, required=None):
+    """An object whose listed fields are typed and whose other fields are kept as-is."""
+    o = obj(props, required)
+    o["x-kubernetes-preserve-unknown-fields"] = True
+    return o
+
+
+# ---- core/v1 PodSpec subset (k8s.io/api/core/v1 types the controllers and web apps read)
+KEY_REF = open_obj({"name": STR, "key": STR, "optional": BOOL}, ["key"])
+ENV_VAR = open_obj({"name": STR, "value": STR,
+                    "valueFrom": open_obj({"configMapKeyRef": KEY_REF, "secretKeyRef": KEY_REF,
+                                           "fieldRef": open_obj({"fieldPath": STR, "apiVersion": STR},
+                                                                ["fieldPath"]),
+                                           "resourceFieldRef": open_obj({"resource": STR, "containerName": STR,
+                                                                         "divisor": INT_OR_STR}, ["resource"])})},
+                   ["name"])
+ENV_FROM = open_obj({"prefix": STR, "configMapRef": open_obj({"name": STR, "optional": BOOL}),
+                     "secretRef": open_obj({"name": STR, "optional": BOOL})})
+RESOURCES = open_obj({"limits": QUANTITY_MAP, "requests": QUANTITY_MAP})
+CONTAINER_PORT = open_obj({"containerPort": {"type": "integer", "minimum": 1}, "name": STR, "hostPort": INT,
+                           "protocol": {"type": "string", "enum": ["TCP", "UDP", "SCTP"]}}, ["containerPort"])
+VOLUME_MOUNT = open_obj({"name": STR, "mountPath": STR, "subPath": STR, "readOnly": BOOL,
+                         "mountPropagation": STR}, ["name", "mountPath"])
+PROBE = open_obj({"httpGet": open_obj({"path": STR, "port": INT_OR_STR, "scheme": STR}, ["port"]),
+                  "tcpSocket": open_obj({"port": INT_OR_STR}, ["port"]),
+                  "exec": open_obj({"command": arr(STR)}),
+                  "initialDelaySeconds": INT, "periodSeconds": INT, "timeoutSeconds": INT,
+                  "failureThreshold": INT, "successThreshold": INT})
+SECURITY_CONTEXT = open_obj({"runAsUser": INT, "runAsGroup": INT, "runAsNonRoot": BOOL, "privileged": BOOL,
+                             "allowPrivilegeEscalation": BOOL, "readOnlyRootFilesystem": BOOL})
+
+
+def container(required=("name",)):
+    return open_obj({"name": STR, "image": STR, "command": arr(STR), "args": arr(STR), "workingDir": STR,
+                     "env": arr(ENV_VAR), "envFrom": arr(ENV_FROM), "ports": arr(CONTAINER_PORT),
+                     "resources": RESOURCES, "volumeMounts": arr(VOLUME_MOUNT),
+                     "imagePullPolicy": {"type": "string", "enum": ["Always", "Never", "IfNotPresent"]},
+                     "livenessProbe": PROBE, "readinessProbe": PROBE, "startupProbe": PROBE,
+                     "securityContext": SECURITY_CONTEXT, "stdin": BOOL, "tty": BOOL}, list(required))
+
+
+VOLUME = open_obj({"name": STR,
+                   "persistentVolumeClaim": open_obj({"claimName": STR, "readOnly": BOOL}, ["claimName"]),
+                   "emptyDir": open_obj({"medium": STR, "sizeLimit": INT_OR_STR}),
+                   "configMap": open_obj({"name": STR, "defaultMode": INT, "optional": BOOL, "items": arr(OBJ_ANY)}),
+                   "secret": open_obj({"secretName": STR, "defaultMode": INT, "optional": BOOL,
+                                       "items": arr(OBJ_ANY)}),
+                   "hostPath": open_obj({"path": STR, "type": STR}, ["path"]),
+                   "csi": open_obj({"driver": STR}, ["driver"])}, ["name"])
+TOLERATION = open_obj({"key": STR, "operator": {"type": "string", "enum": ["Exists", "Equal"]}, "value": STR,
+                       "effect": {"type": "string", "enum": ["NoSchedule", "PreferNoSchedule", "NoExecute", ""]},
+                       "tolerationSeconds": INT})
+NODE_SELECTOR_TERM = open_obj({"matchExpressions": arr(open_obj({"key": STR, "operator": STR, "values": arr(STR)},
+                                                                ["key", "operator"])),
+                               "matchFields": arr(OBJ_ANY)})
+AFFINITY = open_obj({
+    "nodeAffinity": open_obj({
+        "requiredDuringSchedulingIgnoredDuringExecution": open_obj({"nodeSelectorTerms": arr(NODE_SELECTOR_TERM)},
+                                                                   ["nodeSelectorTerms"]),
+        "preferredDuringSchedulingIgnoredDuringExecution": arr(open_obj({"weight": {"type": "integer", "minimum": 1},
+                                                                         "preference": NODE_SELECTOR_TERM},
+                                                                        ["weight", "preference"]))}),
+    "podAffinity": OBJ_ANY, "podAntiAffinity": OBJ_ANY})
+
+
+def pod_spec(containers_min=0, container_required=("name",)):
+    c = arr(container(container_required))
+    if containers_min:
+        c["minItems"] = containers_min
+    return open_obj({"containers": c, "initContainers": arr(container()), "volumes": arr(VOLUME),
+                     "tolerations": arr(TOLERATION), "affinity": AFFINITY, "nodeSelector": STR_MAP,
+                     "serviceAccountName": STR, "automountServiceAccountToken": BOOL,
+                     "imagePullSecrets": arr(open_obj({"name": STR})),
+                     "securityContext": open_obj({"fsGroup": INT, "runAsUser": INT, "runAsGroup": INT,
+                                                  "runAsNonRoot": BOOL, "supplementalGroups": arr(INT)}),
+                     "restartPolicy": {"type": "string", "enum": ["Always", "OnFailure", "Never"]},
+                     "hostIPC": BOOL, "hostNetwork": BOOL, "priorityClassName": STR, "schedulerName": STR,
+                     "terminationGracePeriodSeconds": INT})
+
+
+OBJECT_META = open_obj({"labels": STR_MAP, "annotations": STR_MAP, "name": STR, "namespace": STR})
+POD_TEMPLATE = obj({"metadata": OBJECT_META, "spec": pod_spec(containers_min=1)})
 REPLICA_SPEC = obj({"replicas": {"type": "integer", "minimum": 0},
                     "restartPolicy": {"type": "string", "enum": ["Always", "OnFailure", "Never", "ExitCode"]},
                     "template": POD_TEMPLATE})
@@ -77,21 +169,25 @@ def crd(group, kind, plural, scope, versions, short=None, categories=None, print
 
 
 def crds() -> Dict[str, dict]:
-    nb_spec = obj({"template": obj({"spec": OBJ_ANY}, ["spec"])}, ["template"])
+    # Notebook: spec.template.spec is a full corev1.PodSpec plus the reference's validation
+    # patches (containers minItems 1, name + image required per container)
+    nb_spec = obj({"template": obj({"metadata": OBJECT_META,
+                                    "spec": pod_spec(containers_min=1, container_required=("name", "image"))})})
     nb_status = obj({"conditions": CONDITIONS, "readyReplicas": INT, "containerState": OBJ_ANY})
     prof_spec = obj({"owner": obj({"kind": {"type": "string", "enum": ["User", "Group", "ServiceAccount"]},
                                    "name": STR, "apiGroup": STR, "namespace": STR}, ["kind", "name"]),
                      "plugins": arr(obj({"kind": STR, "spec": OBJ_ANY}, ["kind"])),
                      "resourceQuotaSpec": OBJ_ANY}, ["owner"])
     prof_status = obj({"conditions": CONDITIONS})
-    pd_spec = obj({"selector": OBJ_ANY, "desc": STR, "serviceAccountName": STR,
-                   "automountServiceAccountToken": BOOL, "env": arr(OBJ_ANY), "envFrom": arr(OBJ_ANY),
-                   "volumes": arr(OBJ_ANY), "volumeMounts": arr(OBJ_ANY), "initContainers": arr(OBJ_ANY),
-                   "sidecars": arr(OBJ_ANY), "tolerations": arr(OBJ_ANY), "annotations": OBJ_ANY,
-                   "labels": OBJ_ANY, "args": arr(STR), "command": arr(STR)}, ["selector"])
+    pd_spec = obj({"selector": open_obj({"matchLabels": STR_MAP, "matchExpressions": arr(OBJ_ANY)}), "desc": STR,
+                   "serviceAccountName": STR, "automountServiceAccountToken": BOOL, "env": arr(ENV_VAR),
+                   "envFrom": arr(ENV_FROM), "volumes": arr(VOLUME), "volumeMounts": arr(VOLUME_MOUNT),
+                   "initContainers": arr(container()), "sidecars": arr(container()), "tolerations": arr(TOLERATION),
+                   "imagePullSecrets": arr(open_obj({"name": STR})), "annotations": STR_MAP, "labels": STR_MAP,
+                   "args": arr(STR), "command": arr(STR)}, ["selector"])
     tb_spec = obj({"logspath": STR}, ["logspath"])
     tb_status = obj({"conditions": arr(obj({"deploymentState": STR, "lastProbeTime": STR})), "readyReplicas": INT})
-    pv_spec = obj({"pvc": {"type": "string", "minLength": 1}, "podSpec": OBJ_ANY,
+    pv_spec = obj({"pvc": {"type": "string", "minLength": 1}, "podSpec": pod_spec(),
                    "networking": obj({"targetPort": {"x-kubernetes-int-or-string": True}, "basePrefix": STR,
                                       "rewrite": STR, "timeout": STR}, ["targetPort", "basePrefix"]),
                    "rwoScheduling": BOOL}, ["pvc"])
@@ -121,12 +217,12 @@ def crds() -> Dict[str, dict]:
     age = [{"name": "Age", "type": "date", "jsonPath": ".metadata.creationTimestamp"}]
     return {
         "kubeflow.org_notebooks.yaml": crd("kubeflow.org", "Notebook", "notebooks", "Namespaced",
-                                           [("v1alpha1", True, False, nb_spec, nb_status),
-                                            ("v1beta1", True, True, nb_spec, nb_status),
-                                            ("v1", True, False, nb_spec, nb_status)]),
+                                           [("v1", True, True, nb_spec, nb_status),
+                                            ("v1alpha1", True, False, nb_spec, nb_status),
+                                            ("v1beta1", True, False, nb_spec, nb_status)]),
         "kubeflow.org_profiles.yaml": crd("kubeflow.org", "Profile", "profiles", "Cluster",
-                                          [("v1beta1", True, False, prof_spec, prof_status),
-                                           ("v1", True, True, prof_spec, prof_status)]),
+                                          [("v1", True, True, prof_spec, prof_status),
+                                           ("v1beta1", True, False, prof_spec, prof_status)]),
         "kubeflow.org_poddefaults.yaml": crd("kubeflow.org", "PodDefault", "poddefaults", "Namespaced",
                                              [("v1alpha1", True, True, pd_spec, OBJ_ANY)]),
         "kubeflow.org_pvcviewers.yaml": crd("kubeflow.org", "PVCViewer", "pvcviewers", "Namespaced",

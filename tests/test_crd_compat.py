@@ -1,0 +1,137 @@
+"""CRD API compatibility with the reference: every reference CRD's group,
+kind, plural, scope and versions (order, served, storage) match a table transcribed from the
+reference CRD files; the Notebook CRD carries the reference's validation patches and the typed
+PodSpec subset, so the API server rejects invalid Notebooks and accepts what the JWA creates."""
+import copy
+
+import pytest
+
+from service_account_auth_improvements_amd import manifests
+from service_account_auth_improvements_amd.controlplane.apiserver import APIServer, ApiError, BUILTIN_TYPES
+from service_account_auth_improvements_amd.controlplane.client import InMemoryClient
+
+# (file, group, kind, plural, scope, [(version, served, storage), ...]) -- transcribed from
+#   components/notebook-controller/config/crd/bases/kubeflow.org_notebooks.yaml:10-16,18,3143-3144,3147,6272-6273,6276,9401-9402
+#   components/profile-controller/config/crd/bases/kubeflow.org_profiles.yaml:10-16,18,164-165,168,314-315
+#   components/admission-webhook/manifests/base/crd.yaml:10-16,18,2059-2060
+#   components/pvcviewer-controller/config/crd/bases/kubeflow.org_pvcviewers.yaml:9-15,17,3425-3426
+#   components/tensorboard-controller/config/crd/bases/tensorboard.kubeflow.org_tensorboards.yaml:10-16,18,77-78
+REFERENCE = [
+    ("kubeflow.org_notebooks.yaml", "kubeflow.org", "Notebook", "notebooks", "Namespaced",
+     [("v1", True, True), ("v1alpha1", True, False), ("v1beta1", True, False)]),
+    ("kubeflow.org_profiles.yaml", "kubeflow.org", "Profile", "profiles", "Cluster",
+     [("v1", True, True), ("v1beta1", True, False)]),
+    ("kubeflow.org_poddefaults.yaml", "kubeflow.org", "PodDefault", "poddefaults", "Namespaced",
+     [("v1alpha1", True, True)]),
+    ("kubeflow.org_pvcviewers.yaml", "kubeflow.org", "PVCViewer", "pvcviewers", "Namespaced",
+     [("v1alpha1", True, True)]),
+    ("tensorboard.kubeflow.org_tensorboards.yaml", "tensorboard.kubeflow.org", "Tensorboard", "tensorboards",
+     "Namespaced", [("v1alpha1", True, True)]),
+]
+# north-star CRDs (external upstream projects: training-operator, mpi-operator, KServe)
+NORTH_STAR = [
+    ("kubeflow.org_pytorchjobs.yaml", "kubeflow.org", "PyTorchJob", "pytorchjobs", "Namespaced", [("v1", True, True)]),
+    ("kubeflow.org_mpijobs.yaml", "kubeflow.org", "MPIJob", "mpijobs", "Namespaced", [("v2beta1", True, True)]),
+    ("serving.kserve.io_inferenceservices.yaml", "serving.kserve.io", "InferenceService", "inferenceservices",
+     "Namespaced", [("v1beta1", True, True)]),
+]
+
+
+@pytest.mark.parametrize("row", REFERENCE + NORTH_STAR, ids=lambda r: r[2])
+def test_crd_identity_matches_reference(row):
+    fname, group, kind, plural, scope, versions = row
+    c = manifests.crds()[fname]
+    sp = c["spec"]
+    assert c["metadata"]["name"] == f"{plural}.{group}"
+    assert (sp["group"], sp["names"]["kind"], sp["names"]["plural"], sp["scope"]) == (group, kind, plural, scope)
+    assert [(v["name"], v["served"], v["storage"]) for v in sp["versions"]] == versions
+    assert sum(v["storage"] for v in sp["versions"]) == 1
+    # the in-memory API server agrees on the storage version and scope
+    t = next(t for t in BUILTIN_TYPES if (t.group, t.kind) == (group, kind))
+    assert t.storage_version == next(v for v, _, st in versions if st)
+    assert t.namespaced == (scope == "Namespaced")
+    assert set(t.versions) == {v for v, _, _ in versions}
+
+
+def test_notebook_validation_patches_are_encoded():
+    c = manifests.crds()["kubeflow.org_notebooks.yaml"]
+    for v in c["spec"]["versions"]:     # validation_patches.yaml:1-29 applies to all three versions
+        ctrs = v["schema"]["openAPIV3Schema"]["properties"]["spec"]["properties"]["template"]["properties"]["spec"][
+            "properties"]["containers"]
+        assert ctrs["minItems"] == 1
+        assert ctrs["items"]["required"] == ["name", "image"]
+
+
+def _server():
+    srv = APIServer(types=[t for t in BUILTIN_TYPES if t.group not in ("kubeflow.org", "tensorboard.kubeflow.org",
+                                                                        "serving.kserve.io")])
+    c = InMemoryClient(srv)
+    for crd in manifests.crds().values():
+        c.create(crd)
+    srv.ensure_namespace("ns1")
+    return c
+
+
+def _nb(containers, version="v1beta1", **spec_extra):
+    return {"apiVersion": f"kubeflow.org/{version}", "kind": "Notebook",
+            "metadata": {"name": "nb", "namespace": "ns1"},
+            "spec": {"template": {"spec": {"containers": containers, **spec_extra}}}}
+
+
+GOOD = {"name": "nb", "image": "kfamd/jupyter-pytorch-rocm:latest",
+        "resources": {"requests": {"cpu": "0.5", "memory": "1Gi"}, "limits": {"amd.com/gpu": 1}},
+        "env": [{"name": "NB_PREFIX", "value": "/notebook/ns1/nb"}],
+        "volumeMounts": [{"name": "dshm", "mountPath": "/dev/shm"}],
+        "ports": [{"containerPort": 8888, "name": "notebook-port", "protocol": "TCP"}]}
+
+
+@pytest.mark.parametrize("version", ["v1", "v1beta1", "v1alpha1"])
+def test_valid_notebook_accepted_in_every_served_version(version):
+    c = _server()
+    nb = _nb([GOOD], version, volumes=[{"name": "dshm", "emptyDir": {"medium": "Memory"}}],
+             tolerations=[{"key": "amd.com/gpu", "operator": "Exists", "effect": "NoSchedule"}],
+             affinity={"nodeAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": {
+                 "nodeSelectorTerms": [{"matchExpressions": [{"key": "gpu", "operator": "In", "values": ["mi355x"]}]}]}}},
+             securityContext={"fsGroup": 100}, someFutureField={"kept": True})
+    out = c.create(nb)
+    assert out["apiVersion"] == "kubeflow.org/v1"          # stored in the storage version
+    assert out["spec"]["template"]["spec"]["someFutureField"] == {"kept": True}
+
+
+@pytest.mark.parametrize("containers,extra,why", [
+    ([], {}, "containers: must have at least 1 items"),
+    ([{"name": "nb"}], {}, "image: Required value"),
+    ([{"image": "x"}], {}, "name: Required value"),
+    ([dict(GOOD, resources={"limits": {"cpu": [1]}})], {}, "must be an integer or a string"),
+    ([dict(GOOD, ports=[{"name": "p"}])], {}, "containerPort: Required value"),
+    ([dict(GOOD, imagePullPolicy="Sometimes")], {}, "unsupported value"),
+    ([GOOD], {"volumes": [{"emptyDir": {}}]}, "name: Required value"),
+    ([GOOD], {"tolerations": [{"key": "k", "operator": "Maybe"}]}, "unsupported value"),
+])
+def test_invalid_notebooks_rejected(containers, extra, why):
+    c = _server()
+    with pytest.raises(ApiError) as ei:
+        c.create(_nb(containers, **extra))
+    assert ei.value.code == 422 and why in str(ei.value), str(ei.value)
+
+
+def test_jwa_created_notebook_passes_the_schema():
+    """The JWA form pipeline's Notebook (template + spawner defaults, GPUs, volumes, shm,
+    PodDefault labels) is valid against the typed CRD schema of the API server it posts to."""
+    from service_account_auth_improvements_amd.controlplane.profile import default_cluster_roles
+    from service_account_auth_improvements_amd.webapps import jupyter
+    from test_webapps import USER, _csrf, _nb_body
+    c = _server()
+    for cr in default_cluster_roles():
+        c.create(cr)
+    c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "alice"}})
+    c.create({"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "RoleBinding",
+              "metadata": {"name": "namespaceAdmin", "namespace": "alice"},
+              "roleRef": {"apiGroup": "rbac.authorization.k8s.io", "kind": "ClusterRole", "name": "kubeflow-admin"},
+              "subjects": [{"apiGroup": "rbac.authorization.k8s.io", "kind": "User", "name": "alice@example.com"}]})
+    tc = jupyter.create_app(c, settings_env={"APP_SECURE_COOKIES": "false"}).test_client()
+    h = dict(USER, **_csrf(tc))
+    r = tc.post("/api/namespaces/alice/notebooks", json=_nb_body(), headers=h)
+    assert r.status_code == 200, r.json
+    nb = c.get("kubeflow.org/v1", "Notebook", "nb1", "alice")
+    assert nb["spec"]["template"]["spec"]["containers"][0]["image"] == "kfamd/jupyter-pytorch-rocm:latest"
