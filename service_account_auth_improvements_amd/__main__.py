@@ -108,8 +108,10 @@ def main(argv=None):
     if comp == "profile-controller":
         from .controlplane import profile
         m, reg = _manager(a, client, "kubeflow-profile-controller")
+        from .controlplane.cloud_iam import iam_backend
         r = profile.ProfileReconciler(client, user_id_header=a.userid_header, user_id_prefix=a.userid_prefix,
-                                      workload_identity=a.workload_identity, labels_path=a.namespace_labels_path)
+                                      workload_identity=a.workload_identity, labels_path=a.namespace_labels_path,
+                                      iam=iam_backend())
         m.add(r)
         r.watch_labels_file(m)
         return _run_manager(m, a)

@@ -13,8 +13,9 @@ owner RoleBinding ``namespaceAdmin`` -> ``kubeflow-admin``, optional ResourceQuo
 A namespace owned by someone else is never taken over (a ``Failed`` condition is added).
 
 Cloud IAM calls sit behind the small ``IamBackend`` interface; the policy-document
-manipulation is implemented here exactly.  The in-process backends model GCP/AWS IAM
-state for tests (no cloud egress exists on this platform).
+manipulation is implemented here exactly.  The deployed controller talks to the real clouds
+through ``controlplane/cloud_iam.py`` (GCP IAM REST with ADC tokens, AWS IAM Query API with
+SigV4); ``InMemoryIam`` models both for the local cluster and tests.
 """
 from __future__ import annotations
 
