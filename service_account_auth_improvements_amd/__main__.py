@@ -158,9 +158,7 @@ def main(argv=None):
         host = os.environ.get("PROFILES_KFAM_SERVICE_HOST", "localhost")
         port = os.environ.get("PROFILES_KFAM_SERVICE_PORT", "8081")
         prof = dashboard.ProfilesService(dashboard.http_transport(f"http://{host}:{port}/kfam"))
-        prom = os.environ.get("PROMETHEUS_URL")
-        metrics = (dashboard.PrometheusMetricsService(prom, os.environ.get("METRICS_DASHBOARD")) if prom
-                   else dashboard.LocalMetricsService())
+        metrics = dashboard.metrics_service_for(client)
         return _serve_flask(dashboard.create_app(client, prof, metrics), a.port or 8082)
     print(f"unknown component {comp!r}\n\n{__doc__}", file=sys.stderr)
     return 2

@@ -14,9 +14,10 @@ prometheus_metrics_service.ts, metrics_service_factory.ts}.
   ``nuke-self``, ``get-all-namespaces``, ``get-contributors/<ns>``,
   ``add-contributor/<ns>``, ``remove-contributor/<ns>`` -- all through KFAM, forwarding
   only the identity headers.  Roles map admin<->owner, edit<->contributor, view<->viewer.
-* Metrics: Prometheus range queries when ``PROMETHEUS_URL`` is set; otherwise a local
-  sampler (host CPU via psutil, kubelet pod CPU/RSS, and MI355X busy % / VRAM from
-  ``amd-smi``/``rocm-smi`` when present) so a single-node install still has charts.
+* Metrics (``metrics_service_for``, the provider factory): Stackdriver / Cloud Monitoring
+  on GCE/GKE nodes, Prometheus range queries when ``PROMETHEUS_URL`` is set, otherwise a
+  local sampler (host CPU via psutil, kubelet pod CPU/RSS, and MI355X busy % / VRAM from
+  ``rocm-smi`` when present) so a single-node install still has charts.
 """
 from __future__ import annotations
 
@@ -161,6 +162,137 @@ class PrometheusMetricsService(MetricsService):
 
     def charts_link(self):
         return {"resourceChartsLink": self.dashboard_url, "resourceChartsLinkText": "View in dashboard"}
+
+
+class StackdriverMetricsService(MetricsService):
+    """Cloud Monitoring (Stackdriver) time series for GKE clusters
+    (reference: centraldashboard/app/stackdriver_metrics_service.ts:15-204).
+
+    ``projects.timeSeries.list`` over the Monitoring REST API v3, aligned to 1-minute means
+    (ALIGN_MEAN, REDUCE_NONE) over the requested interval, with the reference's filters:
+    node CPU = ``kubernetes.io/node/cpu/allocatable_utilization`` of this cluster's nodes,
+    pod CPU = ``kubernetes.io/container/cpu/limit_utilization`` and pod memory =
+    ``kubernetes.io/container/memory/used_bytes`` (non-evictable) of this cluster (its name
+    from the GCE metadata server).  Points come back chronologically sorted; a failed query
+    yields no points (logged), as in the reference.  The access token comes from the same
+    ADC code the Profile controller uses (controlplane/cloud_iam.GcpToken)."""
+
+    BASE = "kubernetes.io"
+    NODE_CPU = f"{BASE}/node/cpu/allocatable_utilization"
+    CONTAINER_CPU = f"{BASE}/container/cpu/limit_utilization"
+    CONTAINER_MEM = f"{BASE}/container/memory/used_bytes"
+    CLUSTER_NAME_URL = "http://metadata.google.internal/computeMetadata/v1/instance/attributes/cluster-name"
+    API = "https://monitoring.googleapis.com/v3"
+
+    def __init__(self, project_id: str, node_names: List[str], transport=None, token=None,
+                 clock: Callable[[], float] = time.time):
+        from ..controlplane.cloud_iam import GcpToken
+        from ..utils import iap
+        self.project_id, self.node_names = project_id, list(node_names)
+        self.t = transport or iap.urllib_transport
+        self.token = token or GcpToken(self.t, scope="https://www.googleapis.com/auth/monitoring.read")
+        self.clock = clock
+        self._cluster: Optional[str] = None
+
+    def cluster_name(self) -> str:
+        if self._cluster is None:
+            try:
+                code, text = self.t("GET", self.CLUSTER_NAME_URL, {"Metadata-Flavor": "Google"}, None)
+                self._cluster = text.strip() if code == 200 else ""
+            except ConnectionError:
+                log.warning("Unable to obtain cluster name from Metadata server")
+                self._cluster = ""
+        return self._cluster
+
+    def _fetch(self, flt: str, minutes: int) -> List[dict]:
+        now = int(self.clock())
+        fmt = lambda t: time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime(t))   # noqa: E731
+        params = {"filter": flt, "interval.startTime": fmt(now - 60 * minutes), "interval.endTime": fmt(now),
+                  "aggregation.alignmentPeriod": "60s", "aggregation.perSeriesAligner": "ALIGN_MEAN",
+                  "aggregation.crossSeriesReducer": "REDUCE_NONE"}
+        series, page = [], None
+        while True:
+            q = dict(params, **({"pageToken": page} if page else {}))
+            url = f"{self.API}/projects/{self.project_id}/timeSeries?" + urllib.parse.urlencode(q)
+            code, text = self.t("GET", url, {"Authorization": f"Bearer {self.token.token()}"}, None)
+            if code != 200:
+                raise RuntimeError(f"timeSeries.list HTTP {code}: {text[:200]}")
+            body = json.loads(text or "{}")
+            series.extend(body.get("timeSeries") or [])
+            page = body.get("nextPageToken")
+            if not page:
+                return series
+
+    @staticmethod
+    def _ts(point) -> float:
+        end = (point.get("interval") or {}).get("endTime", "")
+        try:
+            import datetime as _dt
+            return _dt.datetime.strptime(end[:19], "%Y-%m-%dT%H:%M:%S").replace(tzinfo=_dt.timezone.utc).timestamp()
+        except ValueError:
+            return 0.0
+
+    def _points(self, flt, minutes, label_fn, what) -> List[dict]:
+        out = []
+        try:
+            for ts in self._fetch(flt, minutes):
+                labels = (ts.get("resource") or {}).get("labels") or {}
+                for p in ts.get("points") or []:
+                    v = (p.get("value") or {})
+                    val = v.get("doubleValue", v.get("int64Value", 0))
+                    out.append({"timestamp": self._ts(p), "label": label_fn(labels), "value": float(val)})
+        except Exception as e:        # the reference logs and returns what it has
+            log.error("Unable to fetch %s metrics: %s", what, e)
+        out.sort(key=lambda x: x["timestamp"])
+        return out
+
+    def node_cpu(self, minutes):
+        names = self.node_names
+        flt = f'metric.type="{self.NODE_CPU}" AND resource.label.node_name='
+        flt += ('one_of("' + '", "'.join(names) + '")') if len(names) > 1 else f'"{names[0] if names else ""}"'
+        return self._points(flt, minutes, lambda lab: lab.get("node_name"), "Node CPU Utilization")
+
+    def _cluster_filter(self, flt):
+        c = self.cluster_name()
+        return flt + (f' AND resource.label.cluster_name="{c}"' if c else "")
+
+    def pod_cpu(self, minutes):
+        return self._points(self._cluster_filter(f'metric.type="{self.CONTAINER_CPU}"'), minutes,
+                            lambda lab: lab.get("container_name") or lab.get("pod_name"), "Pod CPU Utilization")
+
+    def pod_mem(self, minutes):
+        flt = self._cluster_filter(f'metric.type="{self.CONTAINER_MEM}" AND metric.label.memory_type = "non-evictable"')
+        return self._points(flt, minutes, lambda lab: lab.get("container_name") or lab.get("pod_name"),
+                            "Pod Memory Utilization")
+
+    def charts_link(self):
+        return {"resourceChartsLink": f"https://app.google.stackdriver.com/kubernetes?project={self.project_id}",
+                "resourceChartsLinkText": "View in Stackdriver"}
+
+
+def metrics_service_for(kube: Client, env: Optional[dict] = None, transport=None) -> Optional[MetricsService]:
+    """Provider factory (reference: centraldashboard/app/metrics_service_factory.ts:13-35): on GCE/GKE
+    (node ``providerID`` ``gce://<project>/<zone>/<instance>``) the Stackdriver service over this
+    cluster's nodes; else Prometheus when ``PROMETHEUS_URL`` is set; else the local sampler
+    (single-node installs: host CPU, pod CPU/RSS, MI355X busy %).  ``KFAMD_METRICS=none``
+    disables metrics (the reference's unsupported-platform ``null``)."""
+    env = dict(os.environ if env is None else env)
+    if env.get("KFAMD_METRICS") == "none":
+        return None
+    try:
+        nodes = kube.list("v1", "Node")
+    except ApiError:
+        nodes = []
+    provider = next(((n.get("spec") or {}).get("providerID") for n in nodes
+                     if (n.get("spec") or {}).get("providerID")), "other://")
+    if provider.split(":")[0] == "gce":
+        project = provider.split("/")[2]
+        return StackdriverMetricsService(project, [n["metadata"]["name"] for n in nodes], transport=transport)
+    if env.get("PROMETHEUS_URL"):
+        return PrometheusMetricsService(env["PROMETHEUS_URL"], env.get("METRICS_DASHBOARD"))
+    log.warning('"%s" is not a supported platform for cloud metrics; using the local sampler',
+                provider.split(":")[0])
+    return LocalMetricsService()
 
 
 def read_gpu_stats() -> List[dict]:

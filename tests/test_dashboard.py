@@ -118,3 +118,92 @@ def test_dashboard_serves_spa(dash):
     assert b"kfamd web UI" in app.get("/static/kfamd-ui.js").data
     assert b'data-app="dashboard"' in app.get("/").data
     assert b'data-app="dashboard"' in app.get("/some/client/route").data
+
+
+# ------------------------------------------------------------------ Stackdriver + provider factory
+def _sd_transport(calls, pages):
+    import json as _json
+    import urllib.parse as up
+
+    def t(method, url, headers, body):
+        calls.append((method, url, dict(headers)))
+        if "default/token" in url:
+            return 200, _json.dumps({"access_token": "ya29.mon", "expires_in": 3600})
+        if url.endswith("/attributes/cluster-name"):
+            return 200, "kf-cluster"
+        assert headers["Authorization"] == "Bearer ya29.mon"
+        q = dict(up.parse_qsl(up.urlsplit(url).query))
+        return 200, _json.dumps(pages[q.get("pageToken", "")](q))
+    return t
+
+
+def test_stackdriver_metrics_service_queries_and_parses():
+    from service_account_auth_improvements_amd.webapps.dashboard import StackdriverMetricsService
+    seen = []
+
+    def page0(q):
+        seen.append(q)
+        assert q["aggregation.alignmentPeriod"] == "60s" and q["aggregation.perSeriesAligner"] == "ALIGN_MEAN"
+        assert q["aggregation.crossSeriesReducer"] == "REDUCE_NONE"
+        return {"timeSeries": [{"resource": {"labels": {"node_name": "n2"}},
+                                "points": [{"interval": {"endTime": "2024-01-01T00:02:00Z"}, "value": {"doubleValue": 0.5}},
+                                           {"interval": {"endTime": "2024-01-01T00:01:00Z"}, "value": {"doubleValue": 0.25}}]}],
+                "nextPageToken": "p1"}
+
+    def page1(q):
+        return {"timeSeries": [{"resource": {"labels": {"node_name": "n1"}},
+                                "points": [{"interval": {"endTime": "2024-01-01T00:00:30Z"}, "value": {"doubleValue": 0.1}}]}]}
+    calls = []
+    svc = StackdriverMetricsService("gcp-proj", ["n1", "n2"], transport=_sd_transport(calls, {"": page0, "p1": page1}),
+                                    clock=lambda: 1704067320.0)
+    pts = svc.node_cpu(15)
+    assert [p["value"] for p in pts] == [0.1, 0.25, 0.5]            # chronological over both pages
+    assert [p["label"] for p in pts] == ["n1", "n2", "n2"]
+    f = seen[0]["filter"]
+    assert f == 'metric.type="kubernetes.io/node/cpu/allocatable_utilization" AND resource.label.node_name=one_of("n1", "n2")'
+    assert seen[0]["interval.endTime"] == "2024-01-01T00:02:00Z" and seen[0]["interval.startTime"] == "2023-12-31T23:47:00Z"
+    assert any("/projects/gcp-proj/timeSeries?" in u for _, u, _ in calls)
+    assert svc.charts_link() == {"resourceChartsLink": "https://app.google.stackdriver.com/kubernetes?project=gcp-proj",
+                                 "resourceChartsLinkText": "View in Stackdriver"}
+
+
+def test_stackdriver_pod_filters_use_cluster_name_and_errors_yield_empty():
+    from service_account_auth_improvements_amd.webapps.dashboard import StackdriverMetricsService
+    seen = []
+
+    def pg(q):
+        seen.append(q["filter"])
+        return {"timeSeries": [{"resource": {"labels": {"pod_name": "p", "container_name": ""}},
+                                "points": [{"interval": {"endTime": "2024-01-01T00:00:00Z"}, "value": {"int64Value": "42"}}]}]}
+    svc = StackdriverMetricsService("gcp-proj", ["n1"], transport=_sd_transport([], {"": pg}), clock=lambda: 1704067200.0)
+    assert svc.pod_mem(5)[0] == {"timestamp": 1704067200.0, "label": "p", "value": 42.0}
+    svc.pod_cpu(5)
+    assert seen[0] == ('metric.type="kubernetes.io/container/memory/used_bytes" AND metric.label.memory_type = '
+                       '"non-evictable" AND resource.label.cluster_name="kf-cluster"')
+    assert seen[1] == 'metric.type="kubernetes.io/container/cpu/limit_utilization" AND resource.label.cluster_name="kf-cluster"'
+
+    def boom(m, u, h, b):
+        if "token" in u:
+            return 200, '{"access_token": "t"}'
+        return 500, "backend error"
+    bad = StackdriverMetricsService("gcp-proj", ["n1"], transport=boom)
+    bad._cluster = ""
+    assert bad.pod_cpu(5) == [] and bad.node_cpu(5) == []
+
+
+def test_metrics_service_factory_by_provider():
+    from service_account_auth_improvements_amd.controlplane.apiserver import APIServer
+    from service_account_auth_improvements_amd.controlplane.client import InMemoryClient
+    from service_account_auth_improvements_amd.webapps import dashboard as d
+    c = InMemoryClient(APIServer())
+    c.create({"apiVersion": "v1", "kind": "Node", "metadata": {"name": "gke-n1"},
+              "spec": {"providerID": "gce://my-proj/us-central1-a/gke-n1"}})
+    svc = d.metrics_service_for(c, env={})
+    assert isinstance(svc, d.StackdriverMetricsService) and svc.project_id == "my-proj" and svc.node_names == ["gke-n1"]
+    c2 = InMemoryClient(APIServer())
+    c2.create({"apiVersion": "v1", "kind": "Node", "metadata": {"name": "mi355x-0"}})
+    assert isinstance(d.metrics_service_for(c2, env={"PROMETHEUS_URL": "http://prom:9090"}), d.PrometheusMetricsService)
+    assert d.metrics_service_for(c2, env={"KFAMD_METRICS": "none"}) is None
+    local = d.metrics_service_for(c2, env={})
+    assert isinstance(local, d.LocalMetricsService)
+    local.stop()
