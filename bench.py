@@ -66,7 +66,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--model", default="llama3-8b")
     ap.add_argument("--seq-len", type=int, default=8192)
-    ap.add_argument("--micro-batch", type=int, default=2)
+    ap.add_argument("--micro-batch", type=int, default=0,
+                    help="sequences per micro-batch; 0 = auto: 4 on a 288 GB MI355X for Llama-3-8B at 8k "
+                         "(chunked LM head, ~260 GiB peak: profiles/chunked_head_microbatch.md), else 2")
     ap.add_argument("--grad-accum", type=int, default=1)
     ap.add_argument("--zero1", dest="zero1", action="store_true", default=None,
                     help="ZeRO-1: reduce-scatter grads, 1/N-sharded AdamW, parameter all-gather hidden "
@@ -95,6 +97,10 @@ def main():
         sys.exit(2)
     st = init_distributed(tp=a.tp, pp=a.pp)
     world = st.world_size
+    if a.micro_batch <= 0:
+        big = (st.device.type == "cuda" and torch.cuda.get_device_properties(st.device).total_memory >= 280e9
+               and a.model == "llama3-8b" and a.seq_len <= 8192 and a.tp == 1 and a.pp == 1)
+        a.micro_batch = 4 if big else 2
     backend = dist.get_backend() if dist.is_initialized() else "none"
     world_seen = dist.get_world_size() if dist.is_initialized() else 1
     assert world_seen == a.gpus, (world_seen, a.gpus)
