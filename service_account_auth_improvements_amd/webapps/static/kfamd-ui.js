@@ -1,262 +1,459 @@
-// kfamd web UI (T2-T7): one dependency-free script that renders the Notebooks, Volumes and
-// TensorBoards web apps and the central dashboard against the same REST APIs the reference
-// Angular/Polymer frontends use (crud-web-apps/*/frontend, centraldashboard/public).
+// kfamd web UI (T2-T7): the Notebooks, Volumes and TensorBoards web apps and the central
+// dashboard, dependency-free, against the same REST APIs the reference Angular/Polymer
+// frontends use (crud-web-apps/*/frontend, centraldashboard/public).  Shared components are
+// lib/kf-common.js (DOM) and lib/kf-logic.js (pure logic, unit-tested under node).
 //
-// Shared pieces (kubeflow-common-lib equivalents): namespace selector, resource table with
-// status icons, exponential-backoff poller (1 s doubling to 8 s, reset on change), snack
-// bar errors, CSRF double-submit header (X-XSRF-TOKEN from the XSRF-TOKEN cookie).
+// Routes (hash): #/ index, #/new create form, #/details/<ns>/<name> details page.
+//  * Notebooks (jupyter/frontend/src/app/pages): index with status/GPUs/volumes, the full
+//    new-notebook form (image or custom image, server type, CPU/memory + limits, GPUs with
+//    vendor availability, workspace + data volumes (new or existing PVCs), affinity,
+//    tolerations, PodDefault configurations, shm, environment; readOnly spawner fields are
+//    shown disabled and never sent), and the details page with Overview / Logs / Events /
+//    YAML tabs (pages/notebook-page/{overview,logs,events,yaml}).
+//  * Volumes: index with viewer buttons, details page with the pods using the volume grouped
+//    by owner kind (Notebooks, InferenceService: volume-details-page/overview), events, YAML.
+//  * TensorBoards: index + form (logs path, PodDefault configurations).
 (function () {
   "use strict";
-  const root = document.getElementById("app");
-  const APP = root ? root.dataset.app : "dashboard";
-  const base = (document.querySelector("base") || {}).href || "/";
+  var KF = self.KF, L = self.KFL, el = KF.el, api = KF.api, snack = KF.snack;
+  var root = document.getElementById("app");
+  var APP = root ? root.dataset.app : "dashboard";
+  var VIEWER_BASE = "";     // links into sibling apps (same origin behind the dashboard)
 
-  // ------------------------------------------------------------------ helpers
-  function el(tag, attrs, ...kids) {
-    const e = document.createElement(tag);
-    for (const [k, v] of Object.entries(attrs || {})) {
-      if (k.startsWith("on")) e.addEventListener(k.slice(2), v);
-      else if (k === "class") e.className = v;
-      else e.setAttribute(k, v);
+  function header(title, extra) {
+    return el("header", {}, el("h1", {}, title), extra);
+  }
+  // (re-)render the page of the current hash; the hashchange listener is registered once per app
+  function router(pages) {
+    if (!pages._go) {
+      pages._go = function () {
+        var r = L.route(location.hash);
+        (pages[r.page] || pages.index).apply(null, r.args);
+      };
+      window.addEventListener("hashchange", pages._go);
     }
-    for (const k of kids.flat()) e.append(k instanceof Node ? k : document.createTextNode(String(k == null ? "" : k)));
-    return e;
+    pages._go();
   }
-  function cookie(name) {
-    const m = document.cookie.match(new RegExp("(?:^|; )" + name + "=([^;]*)"));
-    return m ? decodeURIComponent(m[1]) : "";
-  }
-  async function api(method, path, body) {
-    const headers = { "Content-Type": "application/json" };
-    if (!["GET", "HEAD"].includes(method)) headers["X-XSRF-TOKEN"] = cookie("XSRF-TOKEN");
-    const r = await fetch(new URL(path, base), { method, headers, body: body ? JSON.stringify(body) : undefined,
-                                                  credentials: "same-origin" });
-    const j = await r.json().catch(() => ({}));
-    if (!r.ok || j.success === false) throw new Error(j.log || j.error || r.statusText);
-    return j;
-  }
-  function snack(msg, err) {
-    const s = el("div", { class: "snack" + (err ? " err" : "") }, msg);
-    document.body.append(s);
-    setTimeout(() => s.remove(), 5000);
-  }
-  const ICON = { ready: "✔", waiting: "⏳", warning: "⚠", error: "✖", stopped: "⏹",
-                 terminating: "✖", unavailable: "⚠", uninitialized: "•" };
-  function status(st) {
-    st = st || {};
-    return el("span", { class: "st st-" + (st.phase || ""), title: st.message || "" }, ICON[st.phase] || "?", " ",
-              st.phase || "");
-  }
-  function table(cols, rows) {
-    return el("table", { class: "rt" }, el("thead", {}, el("tr", {}, cols.map((c) => el("th", {}, c[0])))),
-              el("tbody", {}, rows.map((r) => el("tr", {}, cols.map((c) => el("td", {}, c[1](r)))))));
-  }
-  // exponential poller (common-lib PollerService.exponential)
-  function poll(fn) {
-    let delay = 1000, last = "", timer = null, stopped = false;
-    async function tick() {
-      try {
-        const sig = JSON.stringify(await fn());
-        delay = sig !== last ? 1000 : Math.min(delay * 2, 8000);
-        last = sig;
-      } catch (e) { snack(e.message, true); delay = Math.min(delay * 2, 8000); }
-      if (!stopped) timer = setTimeout(tick, delay);
-    }
-    tick();
-    return { reset() { delay = 1000; clearTimeout(timer); tick(); }, stop() { stopped = true; clearTimeout(timer); } };
-  }
-  async function namespaceSelect(onChange) {
-    const sel = el("select", { id: "ns" });
-    const qs = new URLSearchParams(location.search).get("ns");
-    let nss = [];
-    try { nss = (await api("GET", "api/namespaces")).namespaces || []; } catch (e) { snack(e.message, true); }
-    for (const n of nss) sel.append(el("option", { value: n }, n));
-    if (qs) sel.value = qs;
-    sel.addEventListener("change", () => onChange(sel.value));
-    window.addEventListener("message", (ev) => {            // dashboard iframe protocol
-      if (ev.data && ev.data.type === "namespace-selected") { sel.value = ev.data.value; onChange(sel.value); }
-    });
-    return sel;
-  }
-  const style = el("style", {}, `
-    body{font-family:system-ui,sans-serif;margin:0;background:#fafafa;color:#222}
-    header{background:#ed1c24;color:#fff;padding:10px 16px;display:flex;gap:16px;align-items:center}
-    header h1{font-size:18px;margin:0;flex:1} main{padding:16px}
-    table.rt{border-collapse:collapse;width:100%;background:#fff} .rt th,.rt td{border-bottom:1px solid #ddd;
-    padding:6px 8px;text-align:left;font-size:13px} .st-ready{color:#188038}.st-warning,.st-error{color:#c5221f}
-    .snack{position:fixed;bottom:16px;left:16px;background:#323232;color:#fff;padding:10px 16px;border-radius:4px}
-    .snack.err{background:#c5221f} form.card{background:#fff;padding:12px;margin:12px 0;display:grid;
-    grid-template-columns:160px 1fr;gap:6px 12px;max-width:720px} button{margin-right:4px}
-    nav a{display:block;padding:8px 12px;color:#222;text-decoration:none} nav a:hover{background:#eee}
-    .dash{display:grid;grid-template-columns:220px 1fr;height:calc(100vh - 44px)} iframe{border:0;width:100%;height:100%}`);
-  document.head.append(style);
+  function back(label) { return el("a", { href: "#/" }, "← " + (label || "back")); }
 
-  // ------------------------------------------------------------------ Jupyter (T4)
-  async function jupyter() {
-    let ns = "", config = {};
-    const list = el("div"), form = el("div");
-    const sel = await namespaceSelect((v) => { ns = v; poller.reset(); });
-    ns = sel.value;
-    root.append(el("header", {}, el("h1", {}, "Notebooks"), sel,
-                   el("button", { onclick: () => showForm() }, "+ New notebook")), el("main", {}, form, list));
-    try { config = (await api("GET", "api/config")).config; } catch (e) { snack(e.message, true); }
-    async function refresh() {
-      if (!ns) return [];
-      const nbs = (await api("GET", `api/namespaces/${ns}/notebooks`)).notebooks;
-      list.replaceChildren(table([
-        ["Status", (n) => status(n.status)], ["Name", (n) => el("a", { href: `/notebook/${n.namespace}/${n.name}/`,
-                                                                       target: "_blank" }, n.name)],
-        ["Type", (n) => n.serverType || "jupyter"], ["Age", (n) => n.age], ["Image", (n) => n.shortImage],
-        ["GPUs", (n) => n.gpus.message || "-"], ["CPU", (n) => n.cpu], ["Memory", (n) => n.memory],
-        ["", (n) => [
-          el("button", { onclick: () => act("PATCH", n, { stopped: n.status.phase !== "stopped" }) },
-             n.status.phase === "stopped" ? "Start" : "Stop"),
-          el("button", { onclick: () => confirm(`Delete ${n.name}?`) && act("DELETE", n) }, "Delete")]],
-      ], nbs));
-      return nbs;
+  // ==================================================================== Notebooks (T4)
+  function jupyter() {
+    var ns = "", config = {}, poller = null, sel = null;
+    var main = el("main"), headerExtra = el("span");
+    root.append(header("Notebooks", headerExtra), main);
+    api("GET", "api/config").then(function (j) { config = j.config || {}; }, function (e) { snack(e.message, true); })
+      .then(function () { return KF.namespaceSelect(function (v) { ns = v; router(pages); }); })
+      .then(function (s) { sel = s; ns = s.value; headerExtra.replaceChildren(sel); router(pages); });
+
+    var pages = {
+      index: function () {
+        if (poller) poller.stop();
+        var list = el("div");
+        main.replaceChildren(el("div", {}, el("a", { href: "#/new" }, el("button", {}, "+ New notebook"))), list);
+        poller = KF.poll(function () {
+          if (!ns) return [];
+          return api("GET", "api/namespaces/" + ns + "/notebooks").then(function (j) {
+            var nbs = j.notebooks;
+            list.replaceChildren(KF.table([
+              ["Status", function (n) { return KF.status(n.status); }, function (n) { return n.status.phase; }],
+              ["Name", function (n) { return el("a", { href: "#/details/" + n.namespace + "/" + n.name }, n.name); },
+               function (n) { return n.name; }],
+              ["Type", function (n) { return n.serverType || "jupyter"; }],
+              ["Age", function (n) { return L.age(n.age); }, function (n) { return n.age; }],
+              ["Image", function (n) { return n.shortImage; }],
+              ["GPUs", function (n) { return (n.gpus && n.gpus.message) || "-"; }],
+              ["CPU", function (n) { return n.cpu; }], ["Memory", function (n) { return n.memory; }],
+              ["Volumes", function (n) { return (n.volumes || []).join(", "); }],
+              ["", function (n) {
+                return [el("a", { href: "/notebook/" + n.namespace + "/" + n.name + "/", target: "_blank" },
+                           el("button", { disabled: n.status.phase !== "ready" }, "Connect")),
+                        el("button", { onclick: function () { act("PATCH", n.name, { stopped: n.status.phase !== "stopped" }); } },
+                           n.status.phase === "stopped" ? "Start" : "Stop"),
+                        el("button", { onclick: function () { if (confirm("Delete " + n.name + "?")) act("DELETE", n.name); } }, "Delete")];
+              }]], nbs, { empty: "No notebooks in this namespace." }));
+            return nbs;
+          });
+        });
+      },
+      new: function () { if (poller) poller.stop(); form(); },
+      details: function (dns, name) { if (poller) poller.stop(); notebookDetails(dns || ns, name); }
+    };
+
+    function act(method, name, body) {
+      return api(method, "api/namespaces/" + ns + "/notebooks/" + name, body)
+        .then(function () { if (poller) poller.reset(); }, function (e) { snack(e.message, true); });
     }
-    async function act(method, n, body) {
-      try { await api(method, `api/namespaces/${ns}/notebooks/${n.name}`, body); poller.reset(); }
-      catch (e) { snack(e.message, true); }
+
+    // ------------------------------------------------------------ new notebook form
+    function form() {
+      var ro = function (f) { return L.readOnly(config, f); };
+      var v = function (f, d) { return L.cfgValue(config, f, d); };
+      var vendorsInstalled = [], pvcs = [], poddefaults = [];
+      var f = el("form", { class: "card", novalidate: true });
+      main.replaceChildren(back("Notebooks"), el("h2", {}, "New notebook"), f);
+      Promise.all([api("GET", "api/gpus").then(function (j) { vendorsInstalled = j.vendors || []; }, function () {}),
+                   api("GET", "api/namespaces/" + ns + "/pvcs").then(function (j) { pvcs = j.pvcs || []; }, function () {}),
+                   api("GET", "api/namespaces/" + ns + "/poddefaults").then(function (j) { poddefaults = j.poddefaults || []; }, function () {})])
+        .then(render);
+
+      function opt(value, text, selected) { return el("option", { value: value, selected: selected ? true : null }, text); }
+      function render() {
+        var imgCfg = config.image || {}, gpu = v("gpus", {}) || {};
+        var name = el("input", { name: "name", required: true, placeholder: "my-notebook" });
+        var serverType = el("select", { name: "serverType", disabled: ro("serverType") },
+          opt("jupyter", "JupyterLab"), opt("group-one", "VS Code (code-server)"), opt("group-two", "RStudio"));
+        var imageSel = el("select", { name: "image", disabled: ro("image") });
+        function images() {
+          var key = { "jupyter": "image", "group-one": "imageGroupOne", "group-two": "imageGroupTwo" }[serverType.value];
+          var c = config[key] || imgCfg;
+          imageSel.replaceChildren.apply(imageSel, (c.options || []).map(function (o) { return opt(o, o, o === c.value); }));
+        }
+        serverType.addEventListener("change", images);
+        images();
+        var custom = el("input", { type: "checkbox", name: "customImageCheck", disabled: ro("image") });
+        var customImg = el("input", { name: "customImage", placeholder: "registry/image:tag", disabled: true });
+        custom.addEventListener("change", function () { customImg.disabled = !custom.checked; imageSel.disabled = custom.checked || ro("image"); });
+        var pull = el("select", { name: "imagePullPolicy", disabled: ro("imagePullPolicy") },
+          ["IfNotPresent", "Always", "Never"].map(function (p) { return opt(p, p, p === v("imagePullPolicy", "IfNotPresent")); }));
+        var cpu = el("input", { name: "cpu", value: v("cpu", "0.5"), disabled: ro("cpu") });
+        var cpuLimit = el("input", { name: "cpuLimit", value: v("cpuLimit", ""), placeholder: "auto (limit factor)", disabled: ro("cpu") });
+        var mem = el("input", { name: "memory", value: v("memory", "1.0Gi"), disabled: ro("memory") });
+        var memLimit = el("input", { name: "memoryLimit", value: v("memoryLimit", ""), placeholder: "auto (limit factor)", disabled: ro("memory") });
+        var gpuNum = el("select", { name: "gpus", disabled: ro("gpus") },
+          ["none", "1", "2", "4", "8"].map(function (o) { return opt(o, o, o === String(gpu.num || "none")); }));
+        var gpuVendor = el("select", { name: "gpuVendor", disabled: ro("gpus") }, (gpu.vendors || []).map(function (x) {
+          var missing = vendorsInstalled.indexOf(x.limitsKey) < 0;
+          return el("option", { value: x.limitsKey, title: missing ? "There are no " + x.uiName + " GPUs in the cluster" : null,
+                                selected: x.limitsKey === gpu.vendor ? true : null }, x.uiName + (missing ? " (not installed)" : ""));
+        }));
+        // workspace volume
+        var wsType = el("select", { disabled: ro("workspaceVolume") }, opt("new", "New volume"), opt("existing", "Existing volume"), opt("none", "None"));
+        var wsName = el("input", { placeholder: "{notebook-name}-workspace" }), wsSize = el("input", { value: "5Gi" });
+        var wsMount = el("input", { value: "/home/jovyan" });
+        var wsExisting = el("select", {}, pvcs.map(function (p) { return opt(p.name, p.name + " (" + p.size + ")"); }));
+        var wsBox = el("div");
+        function wsRender() {
+          wsBox.replaceChildren.apply(wsBox, wsType.value === "new" ? ["name ", wsName, " size ", wsSize, " mount ", wsMount]
+            : wsType.value === "existing" ? ["claim ", wsExisting, " mount ", wsMount] : []);
+        }
+        wsType.addEventListener("change", wsRender);
+        wsRender();
+        // data volumes
+        var dvList = el("div"), datavols = [];
+        function dvRender() {
+          dvList.replaceChildren.apply(dvList, datavols.map(function (d, i) {
+            var t = el("select", { onchange: function (ev) { d.type = ev.target.value; dvRender(); } },
+                       opt("new", "New", d.type === "new"), opt("existing", "Existing", d.type === "existing"));
+            var nm = d.type === "existing"
+              ? el("select", { onchange: function (ev) { d.name = ev.target.value; } }, pvcs.map(function (p) { return opt(p.name, p.name, p.name === d.name); }))
+              : el("input", { value: d.name, placeholder: "volume name", oninput: function (ev) { d.name = ev.target.value; } });
+            if (d.type === "existing" && !d.name && pvcs.length) d.name = pvcs[0].name;
+            return el("div", { class: "dv" }, t, " ", nm,
+              d.type === "new" ? [" size ", el("input", { value: d.size, size: 6, oninput: function (ev) { d.size = ev.target.value; } })] : null,
+              " mount ", el("input", { value: d.mount, oninput: function (ev) { d.mount = ev.target.value; } }),
+              el("button", { type: "button", onclick: function () { datavols.splice(i, 1); dvRender(); } }, "✖"));
+          }));
+        }
+        var addDv = el("button", { type: "button", disabled: ro("dataVolumes"), onclick: function () {
+          datavols.push({ type: "new", name: "", size: "10Gi", mount: "/home/jovyan/data-" + (datavols.length + 1) }); dvRender();
+        } }, "+ Add volume");
+        // scheduling + configurations
+        var aff = el("select", { name: "affinityConfig", disabled: ro("affinityConfig") }, opt("none", "None"),
+          ((config.affinityConfig || {}).options || []).map(function (o) { return opt(o.configKey, o.displayName || o.configKey); }));
+        var tol = el("select", { name: "tolerationGroup", disabled: ro("tolerationGroup") }, opt("none", "None"),
+          ((config.tolerationGroup || {}).options || []).map(function (o) { return opt(o.groupKey, o.displayName || o.groupKey); }));
+        var cfgBoxes = poddefaults.map(function (pd) {
+          return el("label", { title: pd.desc }, el("input", { type: "checkbox", value: pd.label, disabled: ro("configurations"),
+                                                                checked: (v("configurations", []) || []).indexOf(pd.label) >= 0 }), " ", pd.desc);
+        });
+        var shm = el("input", { type: "checkbox", name: "shm", checked: v("shm", true), disabled: ro("shm") });
+        var env = el("textarea", { rows: 3, cols: 50, placeholder: "KEY=VALUE per line", disabled: ro("environment") });
+        var errBox = el("div", { class: "err" });
+        f.replaceChildren.apply(f, [].concat(
+          KF.field("Name", name, "lower-case letters, digits and '-'"),
+          KF.field("Server type", serverType),
+          KF.field("Image", [imageSel, el("label", {}, " ", custom, " custom image "), customImg]),
+          KF.field("Image pull policy", pull),
+          KF.field("CPU request / limit", [cpu, " / ", cpuLimit]),
+          KF.field("Memory request / limit", [mem, " / ", memLimit]),
+          KF.field("GPUs", [gpuNum, " ", gpuVendor]),
+          KF.field("Workspace volume", [wsType, " ", wsBox]),
+          KF.field("Data volumes", [dvList, addDv]),
+          KF.field("Affinity", aff), KF.field("Tolerations", tol),
+          KF.field("Configurations", cfgBoxes.length ? cfgBoxes : el("span", { class: "muted" }, "no PodDefaults in this namespace")),
+          KF.field("Shared memory (/dev/shm)", shm),
+          KF.field("Environment", env),
+          [el("span"), el("div", {}, errBox, el("button", { type: "submit" }, "Launch"), el("a", { href: "#/" }, el("button", { type: "button" }, "Cancel")))]));
+        f.onsubmit = function (ev) {
+          ev.preventDefault();
+          var vals;
+          try {
+            vals = { name: name.value, serverType: serverType.value, image: imageSel.value, customImageCheck: custom.checked,
+                     customImage: customImg.value, imagePullPolicy: pull.value, cpu: cpu.value, cpuLimit: cpuLimit.value,
+                     memory: mem.value, memoryLimit: memLimit.value, gpus: gpuNum.value, gpuVendor: gpuVendor.value,
+                     affinityConfig: aff.value, tolerationGroup: tol.value, shm: shm.checked,
+                     configurations: cfgBoxes.map(function (l) { return l.querySelector("input"); })
+                       .filter(function (i) { return i.checked; }).map(function (i) { return i.value; }),
+                     environment: L.parseEnv(env.value),
+                     workspace: { type: wsType.value, name: wsType.value === "existing" ? wsExisting.value : (wsName.value || name.value + "-workspace"),
+                                  size: wsSize.value, mount: wsMount.value },
+                     datavols: datavols };
+          } catch (e) { errBox.textContent = e.message; return; }
+          var errs = L.jwaFormErrors(vals);
+          if (errs.length) { errBox.textContent = errs.join("; "); return; }
+          api("POST", "api/namespaces/" + ns + "/notebooks", L.jwaFormBody(vals, config, ns))
+            .then(function () { snack("Notebook " + vals.name + " created"); location.hash = "#/"; },
+                  function (e) { errBox.textContent = e.message; });
+        };
+      }
     }
-    async function showForm() {
-      let vendors = [];
-      try { vendors = (await api("GET", "api/gpus")).vendors; } catch (e) { /* optional */ }
-      const g = config.gpus || { value: {} };
-      const f = el("form", { class: "card" },
-        el("label", {}, "Name"), el("input", { name: "name", required: "" }),
-        el("label", {}, "Image"), el("select", { name: "image" },
-          ((config.image || {}).options || []).map((o) => el("option", { value: o }, o))),
-        el("label", {}, "CPU"), el("input", { name: "cpu", value: (config.cpu || {}).value || "0.5" }),
-        el("label", {}, "Memory"), el("input", { name: "memory", value: (config.memory || {}).value || "1.0Gi" }),
-        el("label", {}, "GPUs"), el("select", { name: "gpus" },
-          ["none", "1", "2", "4", "8"].map((o) => el("option", { value: o }, o))),
-        el("label", {}, "GPU vendor"), el("select", { name: "vendor" },
-          (g.value.vendors || []).map((v) => el("option", { value: v.limitsKey },
-            v.uiName + (vendors.includes(v.limitsKey) ? "" : " (not installed)")))),
-        el("label", {}, "Workspace size"), el("input", { name: "ws", value: "5Gi" }),
-        el("span"), el("div", {}, el("button", { type: "submit" }, "Launch"),
-                        el("button", { type: "button", onclick: () => form.replaceChildren() }, "Cancel")));
-      f.addEventListener("submit", async (ev) => {
-        ev.preventDefault();
-        const d = Object.fromEntries(new FormData(f));
-        const body = { name: d.name, namespace: ns, image: d.image, imagePullPolicy: "IfNotPresent",
-                       serverType: "jupyter", cpu: d.cpu, cpuLimit: "", memory: d.memory, memoryLimit: "",
-                       gpus: { num: d.gpus, vendor: d.vendor }, tolerationGroup: "none", affinityConfig: "none",
-                       configurations: [], shm: true, datavols: [],
-                       workspace: { mount: "/home/jovyan", newPvc: { metadata: { name: `${d.name}-workspace` },
-                         spec: { accessModes: ["ReadWriteOnce"], resources: { requests: { storage: d.ws } } } } } };
-        try { await api("POST", `api/namespaces/${ns}/notebooks`, body); form.replaceChildren(); poller.reset(); }
-        catch (e) { snack(e.message, true); }
+
+    // ------------------------------------------------------------ notebook details page
+    function notebookDetails(dns, name) {
+      var p = "api/namespaces/" + dns + "/notebooks/" + name;
+      var title = el("h2", {}, name), st = el("span");
+      main.replaceChildren(back("Notebooks"), el("div", {}, title, " ", st,
+        el("a", { href: "/notebook/" + dns + "/" + name + "/", target: "_blank" }, el("button", {}, "Connect")),
+        el("button", { onclick: function () { act("DELETE", name).then(function () { location.hash = "#/"; }); } }, "Delete")),
+        KF.tabs([
+          ["Overview", function () {
+            return api("GET", p).then(function (j) {
+              var nb = j.notebook, o = L.notebookOverview(nb);
+              st.replaceChildren(KF.status(nb.processed_status));
+              return el("div", {}, KF.details([
+                ["Status", KF.status(nb.processed_status)], ["Server type", o.serverType], ["Image", o.image],
+                ["Creator", o.creator], ["CPU (request / limit)", o.cpu + " / " + (o.cpuLimit || "-")],
+                ["Memory (request / limit)", o.memory + " / " + (o.memoryLimit || "-")],
+                ["GPUs", o.gpus.join(", ") || "none"], ["Configurations", o.configurations.join(", ")],
+                ["Environment", o.environment.join(", ")], ["Tolerations / affinity", o.tolerations + " / " + (o.affinity ? "set" : "none")],
+                ["Age", L.age(nb.metadata.creationTimestamp)]]),
+                el("h4", {}, "Volumes"),
+                KF.table([["Name", function (x) { return x.name; }], ["Source", function (x) { return x.source; }],
+                          ["Mount path", function (x) { return x.mount; }]], o.volumes),
+                el("h4", {}, "Conditions"), KF.conditionsTable((nb.status || {}).conditions));
+            });
+          }],
+          ["Logs", function () {
+            return api("GET", p + "/pod").then(function (j) {
+              var pod = j.pod.metadata.name;
+              return KF.logsViewer(function () {
+                return api("GET", p + "/pod/" + pod + "/logs").then(function (r) { return r.logs; });
+              }, name + ".log");
+            }, function () { return el("div", { class: "muted" }, "No pod for this notebook (stopped or starting)."); });
+          }],
+          ["Events", function () {
+            return api("GET", p + "/events").then(function (j) {
+              return KF.table([["Type", function (e) { return e.type; }, function (e) { return e.type; }],
+                               ["Reason", function (e) { return e.reason; }], ["Message", function (e) { return e.message; }],
+                               ["Object", function (e) { return (e.involvedObject || {}).kind + "/" + (e.involvedObject || {}).name; }],
+                               ["Last seen", function (e) { return e.lastTimestamp || e.eventTime || ""; },
+                                function (e) { return e.lastTimestamp || ""; }]], j.events, { empty: "No events." });
+            });
+          }],
+          ["YAML", function () {
+            return api("GET", p).then(function (j) {
+              var nb = j.notebook; delete nb.processed_status;
+              return KF.yamlView(nb, name + ".yaml");
+            });
+          }]]));
+    }
+  }
+
+  // ==================================================================== Volumes (T5)
+  function volumes() {
+    var ns = "", poller = null;
+    var main = el("main"), headerExtra = el("span");
+    root.append(header("Volumes", headerExtra), main);
+    KF.namespaceSelect(function (v) { ns = v; router(pages); }).then(function (s) { ns = s.value; headerExtra.replaceChildren(s); router(pages); });
+    var pages = {
+      index: function () {
+        if (poller) poller.stop();
+        var list = el("div");
+        var name = el("input", { placeholder: "name" }), size = el("input", { value: "10Gi", size: 6 });
+        var mode = el("select", {}, ["ReadWriteOnce", "ReadWriteMany", "ReadOnlyMany"].map(function (m) { return el("option", { value: m }, m); }));
+        var create = el("button", { onclick: function () {
+          var err = L.dns1123Name(name.value) || L.quantity(size.value);
+          if (err) { snack(err, true); return; }
+          api("POST", "api/namespaces/" + ns + "/pvcs", { name: name.value, mode: mode.value, class: "{empty}",
+                                                          size: size.value, type: "new" })
+            .then(function () { poller.reset(); }, function (e) { snack(e.message, true); });
+        } }, "+ New volume");
+        main.replaceChildren(el("div", { class: "card" }, el("label", {}, "New volume"), el("div", {}, name, " ", size, " ", mode, " ", create)), list);
+        poller = KF.poll(function () {
+          if (!ns) return [];
+          return api("GET", "api/namespaces/" + ns + "/pvcs").then(function (j) {
+            var pvcs = j.pvcs;
+            list.replaceChildren(KF.table([
+              ["Status", function (p) { return KF.status(p.status); }],
+              ["Name", function (p) { return el("a", { href: "#/details/" + p.namespace + "/" + p.name }, p.name); }, function (p) { return p.name; }],
+              ["Age", function (p) { return L.age(p.age); }, function (p) { return p.age; }],
+              ["Size", function (p) { return p.capacity; }], ["Access", function (p) { return (p.modes || []).join(","); }],
+              ["Class", function (p) { return p.class || "-"; }],
+              ["Used by", function (p) { return (p.notebooks || []).join(", ") || "-"; }],
+              ["", function (p) {
+                return [p.viewer.status === "ready" && p.viewer.url ? el("a", { href: p.viewer.url, target: "_blank" }, el("button", {}, "Browse"))
+                  : el("button", { onclick: function () { api("POST", "api/namespaces/" + ns + "/viewers", { name: p.name })
+                      .then(function () { poller.reset(); }, function (e) { snack(e.message, true); }); } }, "Open viewer"),
+                  el("button", { onclick: function () { if (confirm("Delete " + p.name + "?"))
+                    api("DELETE", "api/namespaces/" + ns + "/pvcs/" + p.name).then(function () { poller.reset(); },
+                                                                                   function (e) { snack(e.message, true); }); } }, "Delete")];
+              }]], pvcs, { empty: "No volumes in this namespace." }));
+            return pvcs;
+          });
+        });
+      },
+      details: function (dns, name) {
+        if (poller) poller.stop();
+        var p = "api/namespaces/" + dns + "/pvcs/" + name;
+        main.replaceChildren(back("Volumes"), el("h2", {}, name), KF.tabs([
+          ["Overview", function () {
+            return Promise.all([api("GET", p), api("GET", p + "/pods")]).then(function (r) {
+              var pvc = r[0].pvc, pods = r[1].pods, s = pvc.spec || {}, stt = pvc.status || {};
+              var groups = L.groupPodsByOwner(pods, VIEWER_BASE);
+              return el("div", {}, KF.details([
+                ["Status", stt.phase], ["Size", ((stt.capacity || {}).storage) || ((s.resources || {}).requests || {}).storage],
+                ["Access modes", (stt.accessModes || s.accessModes || []).join(", ")],
+                ["Storage class", s.storageClassName], ["Volume", s.volumeName],
+                ["Age", L.age(pvc.metadata.creationTimestamp)]]),
+                el("h4", {}, "Used by"),
+                groups.length ? groups.map(function (g) {
+                  return el("div", { class: "group" }, el("h4", {}, g.name),
+                            el("ul", {}, g.links.map(function (l) { return el("li", {}, el("a", { href: l.url, target: "_top" }, l.name)); })));
+                }) : el("div", { class: "muted" }, "No Notebook or InferenceService pods use this volume."),
+                el("h4", {}, "Conditions"), KF.conditionsTable(stt.conditions));
+            });
+          }],
+          ["Events", function () {
+            return api("GET", p + "/events").then(function (j) {
+              return KF.table([["Type", function (e) { return e.type; }], ["Reason", function (e) { return e.reason; }],
+                               ["Message", function (e) { return e.message; }],
+                               ["Last seen", function (e) { return e.lastTimestamp || ""; }]], j.events, { empty: "No events." });
+            });
+          }],
+          ["YAML", function () { return api("GET", p).then(function (j) { return KF.yamlView(j.pvc, name + ".yaml"); }); }]]));
+      }
+    };
+  }
+
+  // ==================================================================== TensorBoards (T6)
+  function tensorboards() {
+    var ns = "", poller = null;
+    var main = el("main"), headerExtra = el("span");
+    root.append(header("TensorBoards", headerExtra), main);
+    KF.namespaceSelect(function (v) { ns = v; render(); }).then(function (s) { ns = s.value; headerExtra.replaceChildren(s); render(); });
+    function render() {
+      if (poller) poller.stop();
+      var list = el("div");
+      var name = el("input", { placeholder: "name" });
+      var kind = el("select", {}, el("option", { value: "pvc" }, "PVC"), el("option", { value: "cloud" }, "Object store (gs:// s3://)"));
+      var claim = el("select"), sub = el("input", { placeholder: "sub/path" }), uri = el("input", { placeholder: "gs://bucket/logs" });
+      var cfgs = el("span");
+      Promise.all([api("GET", "api/namespaces/" + ns + "/pvcs").then(function (j) {
+        claim.replaceChildren.apply(claim, (j.pvcs || []).map(function (p) { return el("option", { value: p.name || p }, p.name || p); }));
+      }, function () {}), api("GET", "api/namespaces/" + ns + "/poddefaults").then(function (j) {
+        cfgs.replaceChildren.apply(cfgs, (j.poddefaults || []).map(function (pd) {
+          return el("label", { title: pd.desc }, el("input", { type: "checkbox", value: pd.label }), " ", pd.desc, " ");
+        }));
+      }, function () {})]);
+      var create = el("button", { onclick: function () {
+        var err = L.dns1123Name(name.value);
+        if (err) { snack(err, true); return; }
+        var logspath = kind.value === "pvc" ? "pvc://" + claim.value + "/" + sub.value.replace(/^\//, "") : uri.value;
+        var configurations = Array.prototype.map.call(cfgs.querySelectorAll("input:checked"), function (i) { return i.value; });
+        api("POST", "api/namespaces/" + ns + "/tensorboards", { name: name.value, logspath: logspath, configurations: configurations })
+          .then(function () { poller.reset(); }, function (e) { snack(e.message, true); });
+      } }, "+ New TensorBoard");
+      main.replaceChildren(el("div", { class: "card" }, KF.field("Name", name), KF.field("Logs", [kind, " ", claim, " ", sub, " ", uri]),
+                              KF.field("Configurations", cfgs), el("span"), create), list);
+      poller = KF.poll(function () {
+        if (!ns) return [];
+        return api("GET", "api/namespaces/" + ns + "/tensorboards").then(function (j) {
+          var tbs = j.tensorboards;
+          list.replaceChildren(KF.table([
+            ["Status", function (t) { return KF.status(t.status); }],
+            ["Name", function (t) { return el("a", { href: "/tensorboard/" + t.namespace + "/" + t.name + "/", target: "_blank" }, t.name); }, function (t) { return t.name; }],
+            ["Logs", function (t) { return t.logspath; }], ["Age", function (t) { return L.age(t.age); }],
+            ["", function (t) { return el("button", { onclick: function () { if (confirm("Delete " + t.name + "?"))
+              api("DELETE", "api/namespaces/" + ns + "/tensorboards/" + t.name).then(function () { poller.reset(); },
+                                                                                   function (e) { snack(e.message, true); }); } }, "Delete"); }]],
+            tbs, { empty: "No TensorBoards in this namespace." }));
+          return tbs;
+        });
       });
-      form.replaceChildren(f);
-    }
-    const poller = poll(refresh);
-  }
-
-  // ------------------------------------------------------------------ Volumes (T5)
-  async function volumes() {
-    let ns = "";
-    const list = el("div");
-    const sel = await namespaceSelect((v) => { ns = v; poller.reset(); });
-    ns = sel.value;
-    const name = el("input", { placeholder: "name" }), size = el("input", { value: "10Gi" });
-    const create = el("button", { onclick: async () => {
-      try {
-        await api("POST", `api/namespaces/${ns}/pvcs`, { name: name.value, mode: "ReadWriteOnce", class: "{empty}",
-                                                        size: size.value, type: "new" });
-        poller.reset();
-      } catch (e) { snack(e.message, true); }
-    } }, "+ New volume");
-    root.append(el("header", {}, el("h1", {}, "Volumes"), sel, name, size, create), el("main", {}, list));
-    async function refresh() {
-      if (!ns) return [];
-      const pvcs = (await api("GET", `api/namespaces/${ns}/pvcs`)).pvcs;
-      list.replaceChildren(table([
-        ["Status", (p) => status(p.status)], ["Name", (p) => p.name], ["Size", (p) => p.capacity],
-        ["Access", (p) => (p.modes || []).join(",")], ["Class", (p) => p.class || "-"],
-        ["Used by", (p) => (p.notebooks || []).join(", ") || "-"],
-        ["", (p) => [
-          p.viewer.status === "ready" && p.viewer.url ? el("a", { href: p.viewer.url, target: "_blank" }, "Browse")
-            : el("button", { onclick: () => api("POST", `api/namespaces/${ns}/viewers`, { name: p.name })
-                .then(() => poller.reset(), (e) => snack(e.message, true)) }, "Open viewer"),
-          el("button", { onclick: () => confirm(`Delete ${p.name}?`) &&
-            api("DELETE", `api/namespaces/${ns}/pvcs/${p.name}`).then(() => poller.reset(),
-                                                                     (e) => snack(e.message, true)) }, "Delete")]],
-      ], pvcs));
-      return pvcs;
-    }
-    const poller = poll(refresh);
-  }
-
-  // ------------------------------------------------------------------ TensorBoards (T6)
-  async function tensorboards() {
-    let ns = "";
-    const list = el("div");
-    const sel = await namespaceSelect((v) => { ns = v; poller.reset(); });
-    ns = sel.value;
-    const name = el("input", { placeholder: "name" }), logs = el("input", { placeholder: "pvc://claim/path" });
-    const create = el("button", { onclick: () => api("POST", `api/namespaces/${ns}/tensorboards`,
-        { name: name.value, logspath: logs.value, configurations: [] }).then(() => poller.reset(),
-                                                                           (e) => snack(e.message, true)) },
-      "+ New TensorBoard");
-    root.append(el("header", {}, el("h1", {}, "TensorBoards"), sel, name, logs, create), el("main", {}, list));
-    async function refresh() {
-      if (!ns) return [];
-      const tbs = (await api("GET", `api/namespaces/${ns}/tensorboards`)).tensorboards;
-      list.replaceChildren(table([
-        ["Status", (t) => status(t.status)],
-        ["Name", (t) => el("a", { href: `/tensorboard/${t.namespace}/${t.name}/`, target: "_blank" }, t.name)],
-        ["Logs", (t) => t.logspath], ["Age", (t) => t.age],
-        ["", (t) => el("button", { onclick: () => confirm(`Delete ${t.name}?`) &&
-          api("DELETE", `api/namespaces/${ns}/tensorboards/${t.name}`).then(() => poller.reset(),
-                                                                           (e) => snack(e.message, true)) },
-          "Delete")]], tbs));
-      return tbs;
-    }
-    const poller = poll(refresh);
-  }
-
-  // ------------------------------------------------------------------ Central dashboard (T2/T3)
-  async function dashboard() {
-    const j = (p) => fetch(new URL(p, base)).then((r) => r.json());
-    const env = await j("api/workgroup/env-info");
-    const exists = await j("api/workgroup/exists");
-    const links = await j("api/dashboard-links").catch(() => ({ menuLinks: [] }));
-    const nsSel = el("select", {}, (env.namespaces || []).map((b) =>
-      el("option", { value: b.namespace }, `${b.namespace} (${b.role})`)));
-    const frame = el("iframe", { name: "content" });
-    const post = () => frame.contentWindow &&
-      frame.contentWindow.postMessage({ type: "namespace-selected", value: nsSel.value }, "*");
-    nsSel.addEventListener("change", post);
-    frame.addEventListener("load", post);
-    const nav = el("nav", {}, (links.menuLinks || []).map((l) =>
-      el("a", { href: "#", onclick: (ev) => { ev.preventDefault(); frame.src = `${l.link}?ns=${nsSel.value}`; } },
-         l.text)),
-      el("a", { href: "#", onclick: (ev) => { ev.preventDefault(); manage(); } }, "Manage contributors"));
-    const main = el("div", {}, frame);
-    root.append(el("header", {}, el("h1", {}, "Kubeflow on MI355X"), nsSel, el("span", {}, env.user || "")),
-                el("div", { class: "dash" }, nav, main));
-    if (!exists.hasWorkgroup && exists.registrationFlowAllowed && exists.hasAuth) {
-      const inp = el("input", { value: exists.user });
-      main.replaceChildren(el("div", { class: "card" }, el("h2", {}, "Create your namespace"), inp,
-        el("button", { onclick: () => fetch(new URL("api/workgroup/create", base), {
-          method: "POST", headers: { "Content-Type": "application/json" },
-          body: JSON.stringify({ namespace: inp.value }) }).then(() => location.reload()) }, "Finish")));
-      return;
-    }
-    async function manage() {
-      const ns = nsSel.value;
-      const users = await j(`api/workgroup/get-contributors/${ns}`).catch(() => []);
-      const who = el("input", { placeholder: "user@example.com" });
-      const call = (m) => fetch(new URL(`api/workgroup/${m === "POST" ? "add" : "remove"}-contributor/${ns}`, base),
-        { method: m, headers: { "Content-Type": "application/json" }, body: JSON.stringify({ contributor: who.value }) })
-        .then(async (r) => { if (!r.ok) snack((await r.json()).error, true); manage(); });
-      main.replaceChildren(el("div", { class: "card" }, el("h2", {}, `Contributors of ${ns}`),
-        el("ul", {}, users.map((u) => el("li", {}, u))), who,
-        el("button", { onclick: () => call("POST") }, "Add"), el("button", { onclick: () => call("DELETE") }, "Remove")));
     }
   }
 
-  ({ jupyter, volumes, tensorboards, dashboard }[APP] || dashboard)().catch((e) => snack(e.message, true));
+  // ==================================================================== Central dashboard (T2/T3)
+  function dashboard() {
+    var j = function (p) { return fetch(new URL(p, KF.base)).then(function (r) { return r.json(); }); };
+    Promise.all([j("api/workgroup/env-info"), j("api/workgroup/exists"),
+                 j("api/dashboard-links").catch(function () { return { menuLinks: [] }; })]).then(function (r) {
+      var env = r[0], exists = r[1], links = r[2];
+      var nsSel = el("select", {}, (env.namespaces || []).map(function (b) {
+        return el("option", { value: b.namespace }, b.namespace + " (" + b.role + ")");
+      }));
+      var frame = el("iframe", { name: "content" });
+      var post = function () {
+        if (frame.contentWindow) frame.contentWindow.postMessage({ type: "namespace-selected", value: nsSel.value }, "*");
+      };
+      nsSel.addEventListener("change", function () { post(); home(); });
+      frame.addEventListener("load", post);
+      window.addEventListener("message", function (ev) {          // library.js protocol
+        if (ev.data && ev.data.type === "iframe-connected") post();
+      });
+      var main = el("div");
+      var nav = el("nav", {}, el("a", { href: "#", onclick: function (ev) { ev.preventDefault(); home(); } }, "Home"),
+        (links.menuLinks || []).map(function (l) {
+          return el("a", { href: "#", onclick: function (ev) {
+            ev.preventDefault(); frame.src = l.link + "?ns=" + nsSel.value; main.replaceChildren(frame);
+          } }, l.text);
+        }),
+        el("a", { href: "#", onclick: function (ev) { ev.preventDefault(); manage(); } }, "Manage contributors"));
+      root.append(header("Kubeflow on MI355X", [nsSel, el("span", {}, env.user || "")]), el("div", { class: "dash" }, nav, main));
+      if (!exists.hasWorkgroup && exists.registrationFlowAllowed && exists.hasAuth) {
+        var inp = el("input", { value: exists.user });
+        main.replaceChildren(el("div", { class: "card" }, el("h2", {}, "Create your namespace"), inp,
+          el("button", { onclick: function () {
+            fetch(new URL("api/workgroup/create", KF.base), { method: "POST", headers: { "Content-Type": "application/json" },
+                                                              body: JSON.stringify({ namespace: inp.value }) })
+              .then(function () { location.reload(); });
+          } }, "Finish")));
+        return;
+      }
+      function home() {
+        var ns = nsSel.value;
+        Promise.all([j("api/activities/" + ns).catch(function () { return []; }),
+                     j("api/metrics/node?interval=Last15m").catch(function () { return []; })]).then(function (r2) {
+          var acts = r2[0] || [], pts = Array.isArray(r2[1]) ? r2[1] : [];
+          main.replaceChildren(el("div", { style: "padding:16px" }, el("h2", {}, "Recent activity in " + ns),
+            KF.table([["Time", function (e) { return e.lastTimestamp || e.eventTime || ""; }], ["Type", function (e) { return e.type; }],
+                      ["Object", function (e) { return (e.involvedObject || {}).kind + "/" + (e.involvedObject || {}).name; }],
+                      ["Message", function (e) { return e.message; }]], acts.slice(0, 20), { empty: "No recent activity." }),
+            el("h2", {}, "Node CPU utilisation (15 min)"),
+            KF.table([["Time", function (p) { return new Date(p.timestamp * 1000).toLocaleTimeString(); }],
+                      ["Node", function (p) { return p.label; }], ["Value", function (p) { return (100 * p.value).toFixed(1) + " %"; }]],
+                     pts.slice(-20), { empty: "No metrics service configured." })));
+        });
+      }
+      function manage() {
+        var ns = nsSel.value;
+        j("api/workgroup/get-contributors/" + ns).catch(function () { return []; }).then(function (users) {
+          var who = el("input", { placeholder: "user@example.com" });
+          var call = function (m) {
+            return fetch(new URL("api/workgroup/" + (m === "POST" ? "add" : "remove") + "-contributor/" + ns, KF.base),
+                         { method: m, headers: { "Content-Type": "application/json" }, body: JSON.stringify({ contributor: who.value }) })
+              .then(function (r) { return r.ok ? null : r.json().then(function (b) { snack(b.error, true); }); }).then(manage);
+          };
+          main.replaceChildren(el("div", { class: "card" }, el("h2", {}, "Contributors of " + ns),
+            el("ul", {}, users.map(function (u) { return el("li", {}, u); })), who,
+            el("button", { onclick: function () { call("POST"); } }, "Add"),
+            el("button", { onclick: function () { call("DELETE"); } }, "Remove")));
+        });
+      }
+      home();
+    });
+  }
+
+  var apps = { jupyter: jupyter, volumes: volumes, tensorboards: tensorboards, dashboard: dashboard };
+  try { (apps[APP] || dashboard)(); } catch (e) { snack(e.message, true); }
 })();

@@ -1,0 +1,118 @@
+"""Web UI (T2-T7): the JavaScript sources parse (node --check), the common-lib logic
+(static/lib/kf-logic.js) behaves as the reference kubeflow-common-lib / JWA / VWA frontends do
+(run under node), and the JWA create body the UI generates is accepted by the real JWA backend."""
+import json
+import os
+import shutil
+import subprocess
+
+import pytest
+import yaml
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+STATIC = os.path.join(ROOT, "service_account_auth_improvements_amd", "webapps", "static")
+pytestmark = pytest.mark.skipif(shutil.which("node") is None, reason="node not available")
+
+
+@pytest.fixture(scope="module")
+def out():
+    r = subprocess.run(["node", os.path.join(ROOT, "tests", "js", "kf_logic_cases.js")], capture_output=True,
+                       text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    return json.loads(r.stdout)
+
+
+@pytest.mark.parametrize("f", ["kfamd-ui.js", "lib/kf-common.js", "lib/kf-logic.js"])
+def test_js_sources_parse(f):
+    r = subprocess.run(["node", "--check", os.path.join(STATIC, f)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+
+
+def test_every_app_page_loads_the_shared_libs():
+    for app in ("jupyter", "volumes", "tensorboards", "dashboard"):
+        html = open(os.path.join(STATIC, app, "index.html")).read()
+        i, j, k = (html.index(s) for s in ("lib/kf-logic.js", "lib/kf-common.js", "kfamd-ui.js\""))
+        assert i < j < k and f'data-app="{app}"' in html
+
+
+def test_poller_and_backoff(out):
+    assert out["poll"] == [1000, 2000, 4000, 8000, 8000, 1000, 2000]     # PollerService.exponential
+    assert out["backoff"] == [1000, 2000, 4000, 8000, 16000, 16000] and out["backoffReset"] == 1000
+
+
+def test_validators_and_env(out):
+    assert out["names"][0] == "" and out["names"][5] == ""
+    assert all(out["names"][i] for i in (1, 2, 3, 4))
+    assert [bool(x) for x in out["quantities"]] == [False, False, False, True, False]
+    assert out["env"] == {"A": "1", "B": " two=2"} and "not KEY=VALUE" in out["envErr"]
+    assert out["route"] == [{"page": "details", "args": ["ns1", "nb 1"]}, {"page": "index", "args": []},
+                            {"page": "new", "args": []}]
+
+
+def test_form_body_shape(out):
+    b = out["body"]
+    assert "shm" not in b                       # readOnly in the spawner config: never sent
+    assert b["gpus"] == {"num": "1", "vendor": "amd.com/gpu"} and b["environment"] == {"HIP_VISIBLE_DEVICES": "0"}
+    assert b["workspace"]["newPvc"]["metadata"]["name"] == "nb1-workspace"
+    assert b["datavols"][0] == {"mount": "/data", "existingSource": {"persistentVolumeClaim": {"claimName": "data"}}}
+    assert b["datavols"][1]["newPvc"]["spec"]["resources"]["requests"]["storage"] == "20Gi"
+    assert out["formErrors"] == []
+    errs = " | ".join(out["badFormErrors"])
+    for want in ("lower case", "CPU limit must be greater", "memory: Invalid quantity", "mount path used twice",
+                 "needs a name"):
+        assert want in errs, errs
+    cb = out["customBody"]
+    assert cb["customImage"] == "rocm/pytorch:latest" and "image" not in cb and cb["gpus"] == {"num": "none"}
+    assert "workspace" not in cb
+
+
+def test_ui_generated_bodies_are_accepted_by_the_jwa_backend(out):
+    from test_webapps import USER, _csrf, cluster  # noqa: F401
+    from service_account_auth_improvements_amd.controlplane.apiserver import APIServer
+    from service_account_auth_improvements_amd.controlplane.client import InMemoryClient
+    from service_account_auth_improvements_amd.controlplane.profile import default_cluster_roles
+    from service_account_auth_improvements_amd.webapps import jupyter
+    c = InMemoryClient(APIServer())
+    for cr in default_cluster_roles():
+        c.create(cr)
+    c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "alice"}})
+    c.create({"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "RoleBinding",
+              "metadata": {"name": "namespaceAdmin", "namespace": "alice"},
+              "roleRef": {"apiGroup": "rbac.authorization.k8s.io", "kind": "ClusterRole", "name": "kubeflow-admin"},
+              "subjects": [{"apiGroup": "rbac.authorization.k8s.io", "kind": "User", "name": "alice@example.com"}]})
+    c.create({"apiVersion": "v1", "kind": "PersistentVolumeClaim", "metadata": {"name": "data", "namespace": "alice"},
+              "spec": {"accessModes": ["ReadWriteOnce"], "resources": {"requests": {"storage": "1Gi"}}}})
+    tc = jupyter.create_app(c, settings_env={"APP_SECURE_COOKIES": "false"}).test_client()
+    h = dict(USER, **_csrf(tc))
+    body = dict(out["body"])
+    body["shm"] = True         # the dev spawner config is not readOnly for shm: the form sends it there
+    r = tc.post("/api/namespaces/alice/notebooks", json=body, headers=h)
+    assert r.status_code == 200, r.json
+    nb = c.get("kubeflow.org/v1beta1", "Notebook", "nb1", "alice")
+    ctr = nb["spec"]["template"]["spec"]["containers"][0]
+    assert ctr["resources"]["limits"]["amd.com/gpu"] == "1"
+    assert {"name": "HIP_VISIBLE_DEVICES", "value": "0"} in ctr["env"]
+    assert {m["mountPath"] for m in ctr["volumeMounts"]} == {"/dev/shm", "/data", "/scratch", "/home/jovyan"}
+    assert c.get("v1", "PersistentVolumeClaim", "scratch", "alice")
+    r = tc.post("/api/namespaces/alice/notebooks", json=out["customBody"], headers=h)
+    assert r.status_code == 200, r.json
+    assert c.get("kubeflow.org/v1beta1", "Notebook", "nb2", "alice")["spec"]["template"]["spec"]["containers"][0][
+        "image"] == "rocm/pytorch:latest"
+
+
+def test_volume_details_groups_pods_by_owner(out):
+    assert out["groups"] == [
+        {"name": "Notebooks", "links": [{"name": "nb1", "url": "https://kf.example.com/jupyter/notebook/details/alice/nb1/"}]},
+        {"name": "InferenceService", "links": [
+            {"name": "llm (predictor)", "url": "https://kf.example.com/models/details/alice/llm/"},
+            {"name": "old (transformer)", "url": "https://kf.example.com/models/details/alice/old/"}]}]
+
+
+def test_details_overview_conditions_and_yaml(out):
+    o = out["overview"]
+    assert o["gpus"] == ["1 x amd.com/gpu"] and o["configurations"] == ["add-gpu-env"]
+    assert o["cpu"] == "2" and o["cpuLimit"] == "2.4" and o["creator"] == "alice@example.com"
+    assert {"name": "dshm", "source": "emptyDir (Memory)", "mount": "/dev/shm"} in o["volumes"]
+    assert out["conditions"][0]["lastTransitionTime"] == "2024-01-01T00:00:00Z"
+    assert yaml.safe_load(out["yaml"]) == out["yamlInput"]          # the YAML tab round-trips
+    assert out["age"] == ["30s", "2d"]
