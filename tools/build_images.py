@@ -17,17 +17,44 @@ sys.path.insert(0, ROOT)
 
 # image -> (context dir, Dockerfile, build args, depends-on)
 IMAGES = {
+    # notebook servers (I1), in the reference's build order (example-notebook-servers/Makefile:1-17),
+    # the CUDA flavours replaced by ROCm / MI355X ones
     "base": ("images/base", "images/base/Dockerfile", {}, []),
+    "codeserver": ("images/codeserver", "images/codeserver/Dockerfile", {"BASE_IMG": "{r}/base:{t}"}, ["base"]),
+    "codeserver-python": ("images/codeserver-python", "images/codeserver-python/Dockerfile",
+                          {"BASE_IMG": "{r}/codeserver:{t}"}, ["codeserver"]),
     "jupyter": ("images/jupyter", "images/jupyter/Dockerfile", {"BASE_IMG": "{r}/base:{t}"}, ["base"]),
-    "jupyter-pytorch-rocm": (".", "images/jupyter-pytorch-rocm/Dockerfile", {}, []),
+    "jupyter-scipy": ("images/jupyter-scipy", "images/jupyter-scipy/Dockerfile", {"BASE_IMG": "{r}/jupyter:{t}"},
+                      ["jupyter"]),
+    "jupyter-pytorch": ("images/jupyter-pytorch", "images/jupyter-pytorch/Dockerfile", {"BASE_IMG": "{r}/jupyter:{t}"},
+                        ["jupyter"]),
+    "jupyter-pytorch-full": ("images/jupyter-pytorch-full", "images/jupyter-pytorch-full/Dockerfile",
+                             {"BASE_IMG": "{r}/jupyter-pytorch:{t}"}, ["jupyter-pytorch"]),
+    "jupyter-pytorch-rocm": (".", "images/jupyter-pytorch-rocm/Dockerfile", {"KF_BASE": "{r}/base:{t}"}, ["base"]),
+    "jupyter-pytorch-rocm-full": ("images/jupyter-pytorch-rocm-full", "images/jupyter-pytorch-rocm-full/Dockerfile",
+                                  {"BASE_IMG": "{r}/jupyter-pytorch-rocm:{t}"}, ["jupyter-pytorch-rocm"]),
+    "jupyter-tensorflow": ("images/jupyter-tensorflow", "images/jupyter-tensorflow/Dockerfile",
+                           {"BASE_IMG": "{r}/jupyter:{t}"}, ["jupyter"]),
+    "jupyter-tensorflow-full": ("images/jupyter-tensorflow-full", "images/jupyter-tensorflow-full/Dockerfile",
+                                {"BASE_IMG": "{r}/jupyter-tensorflow:{t}"}, ["jupyter-tensorflow"]),
+    "jupyter-tensorflow-rocm": ("images/jupyter-tensorflow-rocm", "images/jupyter-tensorflow-rocm/Dockerfile",
+                                {"KF_BASE": "{r}/base:{t}"}, ["base"]),
+    "jupyter-tensorflow-rocm-full": ("images/jupyter-tensorflow-rocm-full",
+                                     "images/jupyter-tensorflow-rocm-full/Dockerfile",
+                                     {"BASE_IMG": "{r}/jupyter-tensorflow-rocm:{t}"}, ["jupyter-tensorflow-rocm"]),
+    "rstudio": ("images/rstudio", "images/rstudio/Dockerfile", {"BASE_IMG": "{r}/base:{t}"}, ["base"]),
+    "rstudio-tidyverse": ("images/rstudio-tidyverse", "images/rstudio-tidyverse/Dockerfile",
+                          {"BASE_IMG": "{r}/rstudio:{t}"}, ["rstudio"]),
     "codeserver-python-rocm": ("images/codeserver-python-rocm", "images/codeserver-python-rocm/Dockerfile",
                                {"BASE_IMG": "{r}/jupyter-pytorch-rocm:{t}"}, ["jupyter-pytorch-rocm"]),
+    # data plane + platform
     "trainer-rocm": (".", "images/trainer-rocm/Dockerfile", {}, []),
     "predictor-rocm": ("images/predictor-rocm", "images/predictor-rocm/Dockerfile",
                        {"TRAINER_IMG": "{r}/trainer-rocm:{t}"}, ["trainer-rocm"]),
     "platform": (".", "images/platform/Dockerfile", {}, []),
     "tensorboard": ("images/tensorboard", "images/tensorboard/Dockerfile", {}, []),
 }
+NOTEBOOK_IMAGES = [n for n in IMAGES if n not in ("trainer-rocm", "predictor-rocm", "platform", "tensorboard")]
 
 
 def platform_aliases():
