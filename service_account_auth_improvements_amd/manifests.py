@@ -293,12 +293,30 @@ def _rule(groups, resources, verbs=("get", "list", "watch", "create", "update", 
     return {"apiGroups": list(groups), "resources": list(resources), "verbs": list(verbs)}
 
 
-def _vs(name, prefix, host, port=80, rewrite="/"):
+def _vs(name, prefix, host, port=80, rewrite="/", forwarded_prefix=None, namespace="kubeflow",
+        cluster_domain="cluster.local"):
+    http = {"match": [{"uri": {"prefix": prefix}}], "rewrite": {"uri": rewrite},
+            "route": [{"destination": {"host": f"{host}.{namespace}.svc.{cluster_domain}", "port": {"number": port}}}]}
+    if forwarded_prefix:
+        http = dict({"headers": {"request": {"add": {"x-forwarded-prefix": forwarded_prefix}}}}, **http)
     return {"apiVersion": "networking.istio.io/v1alpha3", "kind": "VirtualService", "metadata": {"name": name},
-            "spec": {"gateways": ["kubeflow-gateway"], "hosts": ["*"],
-                     "http": [{"match": [{"uri": {"prefix": prefix}}], "rewrite": {"uri": rewrite},
-                               "route": [{"destination": {"host": f"{host}.$(namespace).svc.$(clusterDomain)",
-                                                          "port": {"number": port}}}]}]}}
+            "spec": {"gateways": ["kubeflow-gateway"], "hosts": ["*"], "http": [http]}}
+
+
+INGRESS_GATEWAY_PRINCIPAL = "cluster.local/ns/istio-system/sa/istio-ingressgateway-service-account"
+
+
+def _authz_ingress_only(name, app):
+    """AuthorizationPolicy: only the Istio ingress gateway may call the app (reference
+    crud-web-apps/*/manifests/overlays/istio/authorization-policy.yaml)."""
+    return {"apiVersion": "security.istio.io/v1beta1", "kind": "AuthorizationPolicy", "metadata": {"name": name},
+            "spec": {"action": "ALLOW", "rules": [{"from": [{"source": {"principals": [INGRESS_GATEWAY_PRINCIPAL]}}]}],
+                     "selector": {"matchLabels": {"app": app}}}}
+
+
+def _destination_rule(name, host, namespace="kubeflow"):
+    return {"apiVersion": "networking.istio.io/v1alpha3", "kind": "DestinationRule", "metadata": {"name": name},
+            "spec": {"host": f"{host}.{namespace}.svc.cluster.local", "trafficPolicy": {"tls": {"mode": "ISTIO_MUTUAL"}}}}
 
 
 def _env(**kv):
@@ -435,7 +453,6 @@ def components() -> Dict[str, Dict[str, List[dict]]]:
         docs = {"deployment.yaml": [_deployment(f"{app}-deployment", app, [app, f"--port={port}"], {"http": port},
                                                 env=env)],
                 "service.yaml": [_service(f"{app}-service", app, [("http", 80, port)])],
-                "virtual-service.yaml": [_vs(app, prefix, f"{app}-service")],
                 "rbac.yaml": [_sa(app)] + _rbac(app, [
                     _rule(["authorization.k8s.io"], ["subjectaccessreviews"], ("create",)),
                     _rule([""], ["namespaces", "nodes"], ("get", "list")),
@@ -460,7 +477,6 @@ def components() -> Dict[str, Dict[str, List[dict]]]:
                                                  REGISTRATION_FLOW="true", DASHBOARD_CONFIGMAP="centraldashboard-config",
                                                  LOGOUT_URL="/oauth2/sign_out"))],
         "service.yaml": [_service("centraldashboard", "centraldashboard", [("http", 80, 8082)])],
-        "virtual-service.yaml": [_vs("centraldashboard", "/", "centraldashboard")],
         "configmap.yaml": [_dashboard_configmap()],
         "rbac.yaml": [_sa("centraldashboard")] + _rbac("centraldashboard", [
             _rule([""], ["namespaces", "events", "nodes", "configmaps"], ("get", "list", "watch")),
@@ -474,28 +490,87 @@ def _kubeflow_roles():
     return default_cluster_roles()
 
 
-def _dashboard_configmap():
+def _dashboard_configmap(kserve: bool = False):
+    """``kserve``: the kserve overlay's variant, adding the "KServe Endpoints" menu item
+    (reference centraldashboard/manifests/overlays/kserve/patches/configmap.yaml)."""
     import json
     links = {"menuLinks": [
         {"type": "item", "link": "/jupyter/", "text": "Notebooks", "icon": "book"},
         {"type": "item", "link": "/tensorboards/", "text": "TensorBoards", "icon": "assessment"},
         {"type": "item", "link": "/volumes/", "text": "Volumes", "icon": "device:storage"},
-        {"type": "item", "link": "/kserve-endpoints/", "text": "Endpoints", "icon": "kubeflow:models"},
         {"type": "item", "link": "/training/", "text": "Training Jobs (MI355X)", "icon": "kubeflow:katib"}],
         "externalLinks": [], "quickLinks": [
             {"text": "Create a new Notebook server", "desc": "Notebook Servers", "link": "/jupyter/new"},
             {"text": "Serve Llama-3 on MI355X", "desc": "InferenceService", "link": "/kserve-endpoints/"}],
         "documentationItems": []}
+    if kserve:
+        links["menuLinks"].insert(3, {"type": "item", "link": "/kserve-endpoints/", "text": "KServe Endpoints",
+                                      "icon": "kubeflow:models"})
     settings = {"DASHBOARD_FORCE_IFRAME": True}
     return {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "centraldashboard-config"},
             "data": {"links": json.dumps(links, indent=2), "settings": json.dumps(settings)}}
 
 
+WEB_APPS = (("jupyter-web-app", "/jupyter/", "/jupyter"), ("volumes-web-app", "/volumes/", "/volumes"),
+            ("tensorboards-web-app", "/tensorboards/", "/tensorboards"))
+
+
+def component_overlays() -> Dict[str, dict]:
+    """Per-component overlays (reference ``components/*/manifests/overlays/{istio,cert-manager,kserve}``):
+    ``<component>/overlays/<name>`` -> {"kustomization": ..., "files": {file: [docs]}}."""
+    out = {}
+    for app, prefix, fwd in WEB_APPS:
+        out[f"{app}/overlays/istio"] = {
+            "kustomization": {"resources": ["../..", "virtual-service.yaml", "authorization-policy.yaml",
+                                            "destination-rule.yaml"], "namespace": "kubeflow"},
+            "files": {"virtual-service.yaml": [_vs(f"{app}-{app}", prefix, f"{app}-service", forwarded_prefix=fwd)],
+                      "authorization-policy.yaml": [_authz_ingress_only(app, app)],
+                      "destination-rule.yaml": [_destination_rule(app, f"{app}-service")]}}
+    out["centraldashboard/overlays/istio"] = {
+        "kustomization": {"resources": ["../..", "virtual-service.yaml", "authorizationpolicy.yaml"],
+                          "namespace": "kubeflow"},
+        "files": {"virtual-service.yaml": [_vs("centraldashboard", "/", "centraldashboard")],
+                  "authorizationpolicy.yaml": [_authz_ingress_only("central-dashboard", "centraldashboard")]}}
+    out["centraldashboard/overlays/kserve"] = {
+        "kustomization": {"resources": ["../istio"], "patches": [{"path": "patches/configmap.yaml"}]},
+        "files": {"patches/configmap.yaml": [_dashboard_configmap(kserve=True)]}}
+    # cert-manager provisions the PodDefault webhook's serving certificate and injects its CA
+    # into the MutatingWebhookConfiguration (reference admission-webhook/manifests/overlays/cert-manager)
+    svc, ns = "admission-webhook-service", "kubeflow"
+    out["admission-webhook/overlays/cert-manager"] = {
+        "kustomization": {"resources": ["../..", "certificate.yaml"], "namespace": ns,
+                          "patchesStrategicMerge": ["mutating-webhook-configuration.yaml", "deployment.yaml"]},
+        "files": {
+            "certificate.yaml": [
+                {"apiVersion": "cert-manager.io/v1", "kind": "Certificate", "metadata": {"name": "admission-webhook-cert"},
+                 "spec": {"isCA": True, "commonName": f"{svc}.{ns}.svc",
+                          "dnsNames": [f"{svc}.{ns}.svc", f"{svc}.{ns}.svc.cluster.local"],
+                          "issuerRef": {"kind": "Issuer", "name": "admission-webhook-selfsigned-issuer"},
+                          "secretName": "webhook-certs"}},
+                {"apiVersion": "cert-manager.io/v1", "kind": "Issuer",
+                 "metadata": {"name": "admission-webhook-selfsigned-issuer"}, "spec": {"selfSigned": {}}}],
+            "mutating-webhook-configuration.yaml": [
+                {"apiVersion": "admissionregistration.k8s.io/v1", "kind": "MutatingWebhookConfiguration",
+                 "metadata": {"name": "admission-webhook-mutating-webhook-configuration",
+                              "annotations": {"cert-manager.io/inject-ca-from": f"{ns}/admission-webhook-cert"}}}],
+            "deployment.yaml": [
+                {"apiVersion": "apps/v1", "kind": "Deployment", "metadata": {"name": "admission-webhook-deployment"},
+                 "spec": {"template": {"spec": {"containers": [
+                     {"name": "admission-webhook",
+                      "args": ["admission-webhook", "--port=4443", "--tls-cert-file=/etc/webhook/certs/tls.crt",
+                               "--tls-key-file=/etc/webhook/certs/tls.key"]}]}}}}]}}
+    return out
+
+
 def overlays() -> Dict[str, dict]:
     """overlay dir -> kustomization (relative to manifests/)."""
     comps = sorted(components())
+    via = {app: f"../../{app}/overlays/istio" for app, _, _ in WEB_APPS}
+    via["centraldashboard"] = "../../centraldashboard/overlays/kserve"
+    via["admission-webhook"] = "../../admission-webhook/overlays/cert-manager"
     return {
-        "overlays/kubeflow": {"namespace": "kubeflow", "resources": ["../../crds"] + [f"../../{c}" for c in comps],
+        "overlays/kubeflow": {"namespace": "kubeflow",
+                              "resources": ["../../crds"] + [via.get(c, f"../../{c}") for c in comps],
                               "commonLabels": {"app.kubernetes.io/part-of": "kubeflow"}},
         "overlays/standalone": {"namespace": "kubeflow-standalone",
                                 "resources": ["../../crds", "../../notebook-controller", "../../training-operator",
@@ -519,6 +594,13 @@ def generate(out_dir: str):
               [{"apiVersion": "kustomize.config.k8s.io/v1beta1", "kind": "Kustomization",
                 "resources": sorted(files),
                 "images": [{"name": f"{IMAGE_PREFIX}/{comp}", "newName": f"{IMAGE_PREFIX}/{comp}", "newTag": TAG}]}])
+    for rel, ov in component_overlays().items():
+        d = os.path.join(out_dir, rel)
+        for fn, docs in ov["files"].items():
+            os.makedirs(os.path.dirname(os.path.join(d, fn)), exist_ok=True)
+            _dump(os.path.join(d, fn), docs)
+        _dump(os.path.join(d, "kustomization.yaml"),
+              [dict({"apiVersion": "kustomize.config.k8s.io/v1beta1", "kind": "Kustomization"}, **ov["kustomization"])])
     for rel, k in overlays().items():
         d = os.path.join(out_dir, rel)
         os.makedirs(d, exist_ok=True)

@@ -89,3 +89,62 @@ def test_sample_jobs_reconcile_on_local_cluster():
                                                          "kubeflow-user"), 20)
     finally:
         cl.stop()
+
+
+# ------------------------------------------------------------------ component overlays (M1)
+def _by(docs, kind, name=None):
+    return [d for d in docs if d["kind"] == kind and (name is None or d["metadata"]["name"] == name)]
+
+
+@pytest.mark.parametrize("app,prefix", [("jupyter-web-app", "/jupyter"), ("volumes-web-app", "/volumes"),
+                                        ("tensorboards-web-app", "/tensorboards")])
+def test_istio_overlay_renders(app, prefix):
+    """reference crud-web-apps/*/manifests/overlays/istio/{virtual-service,authorization-policy,destination-rule}.yaml"""
+    docs = manifests.build(os.path.join(MAN, app, "overlays", "istio"))
+    (vs,) = _by(docs, "VirtualService")
+    http = vs["spec"]["http"][0]
+    assert http["match"] == [{"uri": {"prefix": prefix + "/"}}] and http["rewrite"] == {"uri": "/"}
+    assert http["headers"]["request"]["add"]["x-forwarded-prefix"] == prefix
+    assert http["route"][0]["destination"]["host"] == f"{app}-service.kubeflow.svc.cluster.local"
+    (ap,) = _by(docs, "AuthorizationPolicy")
+    assert ap["spec"]["rules"][0]["from"][0]["source"]["principals"] == [manifests.INGRESS_GATEWAY_PRINCIPAL]
+    assert ap["spec"]["selector"]["matchLabels"] == {"app": app}
+    (dr,) = _by(docs, "DestinationRule")
+    assert dr["spec"]["trafficPolicy"]["tls"]["mode"] == "ISTIO_MUTUAL"
+    assert _by(docs, "Deployment") and all(d["metadata"]["namespace"] == "kubeflow" for d in docs
+                                           if d["kind"] not in ("ClusterRole", "ClusterRoleBinding"))
+
+
+def test_cert_manager_overlay_renders():
+    docs = manifests.build(os.path.join(MAN, "admission-webhook", "overlays", "cert-manager"))
+    (cert,) = _by(docs, "Certificate")
+    assert cert["spec"]["dnsNames"] == ["admission-webhook-service.kubeflow.svc",
+                                        "admission-webhook-service.kubeflow.svc.cluster.local"]
+    assert cert["spec"]["secretName"] == "webhook-certs" and _by(docs, "Issuer", cert["spec"]["issuerRef"]["name"])
+    (mw,) = _by(docs, "MutatingWebhookConfiguration")
+    assert mw["metadata"]["annotations"]["cert-manager.io/inject-ca-from"] == "kubeflow/admission-webhook-cert"
+    assert mw["webhooks"][0]["clientConfig"]["service"]["path"] == "/apply-poddefault"     # base kept
+    (dep,) = _by(docs, "Deployment")
+    ctr = dep["spec"]["template"]["spec"]["containers"][0]
+    assert "--tls-cert-file=/etc/webhook/certs/tls.crt" in ctr["args"]
+    assert any(v.get("secret", {}).get("secretName") == "webhook-certs" for v in dep["spec"]["template"]["spec"]["volumes"])
+
+
+def test_kserve_overlay_adds_the_endpoints_link():
+    import json
+    base = json.loads(_by(manifests.build(os.path.join(MAN, "centraldashboard")), "ConfigMap",
+                          "centraldashboard-config")[0]["data"]["links"])
+    docs = manifests.build(os.path.join(MAN, "centraldashboard", "overlays", "kserve"))
+    links = json.loads(_by(docs, "ConfigMap", "centraldashboard-config")[0]["data"]["links"])
+    texts = [m["text"] for m in links["menuLinks"]]
+    assert "KServe Endpoints" in texts and "KServe Endpoints" not in [m["text"] for m in base["menuLinks"]]
+    assert set(m["text"] for m in base["menuLinks"]) <= set(texts)
+    assert _by(docs, "VirtualService") and _by(docs, "AuthorizationPolicy")       # built on the istio overlay
+
+
+def test_kubeflow_overlay_composes_the_component_overlays():
+    docs = manifests.build(os.path.join(MAN, "overlays", "kubeflow"))
+    assert len(_by(docs, "VirtualService")) == 4 and len(_by(docs, "DestinationRule")) == 3
+    assert _by(docs, "Certificate") and _by(docs, "Issuer")
+    names = [d["metadata"]["name"] for d in docs]
+    assert len(names) == len(set((d["kind"], d["metadata"]["name"]) for d in docs)), "duplicate objects"
