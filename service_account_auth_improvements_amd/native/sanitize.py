@@ -90,6 +90,8 @@ def build_ops_check(force: bool = False, jobs: int | None = None) -> Path:
     import torch
     import torch.utils.cpp_extension as ce
 
+    from ..ops._build import FILE_FLAGS
+
     inc = ce.include_paths(device_type="cuda")
     lib = os.path.join(os.path.dirname(torch.__file__), "lib")
     abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
@@ -110,7 +112,8 @@ def build_ops_check(force: bool = False, jobs: int | None = None) -> Path:
     hips = sorted(CSRC.glob("*.hip"))
     cpps = [CSRC / "bindings.cpp", HERE / "sanitize" / "ops_host_check.cpp"]
     exe = OUT / "ops_host_check"
-    dg = _digest(hips + cpps + sorted(CSRC.glob("*.h")), hip_flags + cpp_flags + link)
+    dg = _digest(hips + cpps + sorted(CSRC.glob("*.h")),
+                 hip_flags + cpp_flags + link + [f"{k}:{v}" for k, v in sorted(FILE_FLAGS.items())])
     if _fresh(exe, dg, force):
         return exe
     TMP.mkdir(parents=True, exist_ok=True)
@@ -118,7 +121,7 @@ def build_ops_check(force: bool = False, jobs: int | None = None) -> Path:
     for s in hips:
         o = TMP / (s.stem + ".o")
         objs.append(o)
-        cmds.append([HIPCC, *hip_flags, "-c", str(s), "-o", str(o)])
+        cmds.append([HIPCC, *hip_flags, *FILE_FLAGS.get(s.name, []), "-c", str(s), "-o", str(o)])
     for s in cpps:
         o = TMP / (s.stem + ".o")
         objs.append(o)

@@ -53,6 +53,11 @@ def _flags():
     return kernel, binding, link
 
 
+# per-source extra flags: flash_attn.hip's dK/dV kernel pins its 256 accumulators to AGPRs
+# (inline asm) and needs the builtin MFMA chains in the VGPR form to fit the other 256
+FILE_FLAGS = {"flash_attn.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+
+
 def _sources():
     hips = sorted(CSRC.glob("*.hip"))
     return hips, CSRC / "bindings.cpp"
@@ -79,7 +84,7 @@ def _run(cmd):
 def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -> Path:
     kernel, binding, link = _flags()
     hips, bind = _sources()
-    digest = _digest(hips + [bind], kernel + binding + link)
+    digest = _digest(hips + [bind], kernel + binding + link + [f"{k}:{v}" for k, v in sorted(FILE_FLAGS.items())])
     stamp = HERE / (LIB_NAME + ".stamp")
     if not force and LIB_PATH.exists() and stamp.exists() and stamp.read_text().strip() == digest:
         return LIB_PATH
@@ -89,7 +94,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
     for src in hips:
         obj = BUILD / (src.stem + ".o")
         objs.append(obj)
-        cmds.append([HIPCC, *kernel, "-c", str(src), "-o", str(obj)])
+        cmds.append([HIPCC, *kernel, *FILE_FLAGS.get(src.name, []), "-c", str(src), "-o", str(obj)])
     bobj = BUILD / "bindings.o"
     objs.append(bobj)
     cmds.append([HIPCC, *binding, "-x", "c++", "-c", str(bind), "-o", str(bobj)])

@@ -547,7 +547,7 @@ constexpr int OFF_DO = OFF_Q + 16384;          // [2][32 x 256 B]
 constexpr int OFF_LD = OFF_DO + 16384;         // [2][lse 32 f32 | delta 32 f32]
 constexpr int SMEM = OFF_LD + 512;             // 66048 B -> 2 workgroups per CU
 
-__device__ __forceinline__ int n_chunks(int kb, int S, bool causal) {
+__host__ __device__ inline int n_chunks(int kb, int S, bool causal) {
   const int q0 = causal ? kb * BKV : 0;
   return (S - q0 + QCH - 1) / QCH;
 }
@@ -698,6 +698,263 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
   flush(dV, 1.f, dv_acc);
 }
 
+// ---- 64 keys per wave, one wave per SIMD (512-register budget) -------------------------
+// The 32-key kernel above is LDS-read bound: per 32-query iteration each wave reads 40 KB
+// (Q and dO row fragments, the K fragments again, Q^T and dO^T transposed fragments) for 32
+// MFMAs, so the CU's 8 waves need ~2560 LDS cycles against ~2048 MFMA cycles per SIMD, and
+// its 256 VGPRs spill.  Here each wave owns 64 keys as two 32-key groups: every Q/dO/Q^T/dO^T
+// fragment read feeds BOTH groups' MFMAs (48 KB for 64 MFMAs; ~1536 LDS cycles per 2048 MFMA
+// cycles on the CU), V stays in registers, and the 256 dK^T/dV^T accumulator registers go
+// to the AGPR half of the unified 512-entry file (1 workgroup of 4 waves per CU).
+namespace fb2 {
+constexpr int BKV2 = 256;                       // keys per workgroup (4 waves x 64)
+constexpr int OFF_K = 0;                       // [256 keys x 256 B] = 64 KB
+constexpr int OFF_Q = 65536;                   // [2][32 x 256 B]
+constexpr int OFF_DO = OFF_Q + 16384;          // [2][32 x 256 B]
+constexpr int OFF_LD = OFF_DO + 16384;         // [2][lse 32 f32 | delta 32 f32]
+constexpr int SMEM = 131072;                   // the flush transposes [256 keys][128 d] fp32
+
+__host__ __device__ inline int n_chunks(int kb, int S, bool causal) {
+  const int q0 = causal ? kb * BKV2 : 0;
+  return (S - q0 + QCH - 1) / QCH;
+}
+}  // namespace fb2
+
+// acc += a.b with the accumulator pinned to AGPRs: left to itself, hipcc picks the VGPR form
+// of the MFMA and parks the 256 accumulators in AGPRs between uses (~1200 v_accvgpr moves
+// per iteration)
+// (flash_attn.hip is built with -mllvm -amdgpu-mfma-vgpr-form so that the builtin S/dP chains
+// keep their accumulators in VGPRs).  The hazard recognizer does not look inside inline asm,
+// so the waits it would insert are explicit: two wait states before every MFMA (a VALU op may
+// just have written its B operand; the pad fills an MFMA issue gap) and drain_mfma() before
+// the accumulators are read back.
+__device__ __forceinline__ void mfma32_agpr(f32x16& acc, bf16x8 a, bf16x8 b) {
+  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ bf16x8 ds_b128(u32 addr) {
+  u32x4 v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr) : "memory");
+  return as_bf16x8(v);
+}
+__device__ __forceinline__ float ds_f32(u32 addr) {
+  float v;
+  asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"(addr) : "memory");
+  return v;
+}
+template <int N>
+__device__ __forceinline__ void lgkm_tie1(bf16x8& f) {
+  asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(f) : "i"(N) : "memory");
+}
+__device__ __forceinline__ void drain_mfma() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory"); }
+
+template <bool CAUSAL>
+__global__ __launch_bounds__(256, 1) void flash_bwd_dkdv64_kernel(
+    const bf16_t* __restrict__ qkv, long ld, const bf16_t* __restrict__ dout, long lddo,
+    const float* __restrict__ lse, const float* __restrict__ delta, float* __restrict__ dk_acc,
+    float* __restrict__ dv_acc, int B, int S, int Hq, int Hkv, float scale, int items_per_head) {
+  using namespace fb2;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  const int G = Hq / Hkv;
+  const int lid = xcd_remap(blockIdx.x, B * Hkv * items_per_head);
+  int item = lid % items_per_head;
+  const int bh = lid / items_per_head;
+  const int hkv = bh % Hkv, b = bh / Hkv;
+  const int nkb = S / BKV2;
+  int kb = 0;
+  for (; kb < nkb; ++kb) {
+    const int n = n_chunks(kb, S, CAUSAL);
+    if (item < n) break;
+    item -= n;
+  }
+  const int kv0 = kb * BKV2;
+  const int qs = (CAUSAL ? kv0 : 0) + item * QCH;
+  const int qe = min(S, qs + QCH);
+  const int ntq = (qe - qs) / QT;
+  const int niter = ntq * G;
+
+  const int tid = threadIdx.x, l = tid & 63, lr = l & 31, hh = l >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kw0 = kv0 + 64 * w;
+  const float c = scale * LOG2E, inv_scale = 1.f / scale;
+  const long rowB = (long)b * S;
+  const bf16_t* kp = qkv + rowB * ld + (long)(Hq + hkv) * D;
+  const bf16_t* vp = qkv + rowB * ld + (long)(Hq + Hkv + hkv) * D;
+
+  stage_rows(kp + (long)kv0 * ld, ld, smem + OFF_K, BKV2, w, 4, l);
+  bf16x8 vf[2][8];  // B operand of dP = dO V^T: V[key][16ks + 8hh .. +8], both key groups
+#pragma unroll
+  for (int kg = 0; kg < 2; ++kg)
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks)
+      vf[kg][ks] = as_bf16x8(ld16(vp + (long)(kw0 + 32 * kg + lr) * ld + 16 * ks + 8 * hh));
+
+  auto stage = [&](int it, int buf) {
+    const int hq = it / ntq, qt = it - hq * ntq;
+    const int h = hkv * G + hq;
+    const int q0 = qs + qt * QT;
+    stage_rows(qkv + (rowB + q0) * ld + (long)h * D, ld, smem + OFF_Q + buf * 8192, QT, w, 4, l);
+    stage_rows(dout + (rowB + q0) * lddo + (long)h * D, lddo, smem + OFF_DO + buf * 8192, QT, w, 4, l);
+    if (w == 0) {
+      const float* src = (l < 32 ? lse : delta) + ((long)b * Hq + h) * S + q0 + (l & 31);
+      glds4(src, smem + OFF_LD + buf * 256);
+    }
+  };
+
+  f32x16 dK[2][4], dV[2][4];
+#pragma unroll
+  for (int kg = 0; kg < 2; ++kg)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) { dK[kg][t] = f32x16{}; dV[kg][t] = f32x16{}; }
+  const int vrow = 4 * hh + ((l & 15) >> 2);
+  const int vcol = 16 * ((l >> 4) & 1) + 4 * (l & 3);
+
+  if (niter > 0) stage(0, 0);
+  wait_dma_barrier();
+  const bf16x8 ones = fold_ones(hh);
+  // Every LDS read in the loop is inline asm with counted lgkmcnt waits: hipcc orders a
+  // compiler-visible LDS read behind every LDS-DMA in flight (s_waitcnt vmcnt(0)), which would
+  // make each iteration wait for the NEXT tile's staging right after issuing it.
+  const u32 k_lds = lds_addr(smem + OFF_K);
+  for (int it = 0; it < niter; ++it) {
+    const int cur = it & 1;
+    const int qt = it % ntq;
+    const int q0 = qs + qt * QT;
+    if (it + 1 < niter) stage(it + 1, cur ^ 1);
+    const u32 q_lds = lds_addr(smem + OFF_Q + cur * 8192), do_lds = lds_addr(smem + OFF_DO + cur * 8192);
+    const u32 l_lds = lds_addr(smem + OFF_LD + cur * 256);
+    {
+      // No causal skip: a wave whose keys all lie above the tile's queries runs fully masked
+      // (diagonal tiles only, ~1.6 % of the work); a skip branch would make the loop-carried
+      // accumulators flow through a join, which hipcc resolves by copying all 256 of them
+      // AGPR -> VGPR -> AGPR every iteration.
+      float lse_s = ds_f32(l_lds + 4 * lr), dl = ds_f32(l_lds + 128 + 4 * lr);
+      // operand fragments one k-step ahead (4 reads per step)
+      bf16x8 fr[2][4];
+      auto rd = [&](int ks, int bf) {
+        fr[bf][0] = ds_b128(q_lds + swz(lr, 2 * ks + hh));
+        fr[bf][1] = ds_b128(do_lds + swz(lr, 2 * ks + hh));
+        fr[bf][2] = ds_b128(k_lds + swz(64 * w + lr, 2 * ks + hh));
+        fr[bf][3] = ds_b128(k_lds + swz(64 * w + 32 + lr, 2 * ks + hh));
+      };
+      rd(0, 0);
+      asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(lse_s), "+v"(dl) :: "memory");
+      // row constants -lse/scale and -delta of query row lr, folded once and shared by both groups
+      const f32x16 s_init = mfma32(fold_const(lse_s * inv_scale, hh), ones, f32x16{});
+      const f32x16 dp_init = mfma32(fold_const(dl, hh), ones, f32x16{});
+      f32x16 s[2] = {s_init, s_init}, dp[2] = {dp_init, dp_init};
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        const int bf = ks & 1;
+        if (ks < 7) {
+          rd(ks + 1, bf ^ 1);
+          lgkm_wait_tie<4>(fr[bf]);
+        } else {
+          lgkm_wait_tie<0>(fr[bf]);
+        }
+#pragma unroll
+        for (int kg = 0; kg < 2; ++kg) {
+          s[kg] = mfma32(fr[bf][0], fr[bf][2 + kg], s[kg]);
+          dp[kg] = mfma32(fr[bf][1], vf[kg][ks], dp[kg]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // causal mask without a branch (a masked/unmasked split doubles the live code and
+      // spills): element r of this lane is masked iff key - q0 - 4hh > (r & 3) + 8 (r >> 2)
+#pragma unroll
+      for (int kg = 0; kg < 2; ++kg) {
+        const int lim = kw0 + 32 * kg + lr - q0 - 4 * hh;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = __builtin_amdgcn_exp2f(s[kg][r] * c);
+          s[kg][r] = (CAUSAL && lim > (r & 3) + 8 * (r >> 2)) ? 0.f : p;
+        }
+      }
+      bf16x8 pf[2][2];
+#pragma unroll
+      for (int kg = 0; kg < 2; ++kg)
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          u32x4 u;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) u[i] = pack2(s[kg][8 * ss + 2 * i], s[kg][8 * ss + 2 * i + 1]);
+          pf[kg][ss] = as_bf16x8(u);
+        }
+      // dV^T += dO^T P and dK^T += Q^T dS: one transposed A fragment feeds both key groups,
+      // read one step ahead of its two MFMAs
+      auto tr = [&](u32 base, int st) {
+        const int row = 16 * (st & 1) + vrow, col = 32 * (st >> 1) + vcol;
+        return tr_pair_asm(base + swz8(row, col), base + swz8(row + 8, col));
+      };
+      bf16x8 ta[2];
+      ta[0] = tr(do_lds, 0);
+#pragma unroll
+      for (int st = 0; st < 8; ++st) {
+        const int t = st >> 1, ss = st & 1, bf = st & 1;
+        if (st < 7) {
+          ta[bf ^ 1] = tr(do_lds, st + 1);
+          lgkm_tie1<2>(ta[bf]);
+        } else {
+          lgkm_tie1<0>(ta[bf]);
+        }
+        mfma32_agpr(dV[0][t], ta[bf], pf[0][ss]);
+        mfma32_agpr(dV[1][t], ta[bf], pf[1][ss]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      bf16x8 sf[2][2];
+#pragma unroll
+      for (int kg = 0; kg < 2; ++kg)
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          u32x4 u;
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            u[i] = pack2(s[kg][8 * ss + 2 * i] * dp[kg][8 * ss + 2 * i],
+                         s[kg][8 * ss + 2 * i + 1] * dp[kg][8 * ss + 2 * i + 1]);
+          sf[kg][ss] = as_bf16x8(u);
+        }
+      ta[0] = tr(q_lds, 0);
+#pragma unroll
+      for (int st = 0; st < 8; ++st) {
+        const int t = st >> 1, ss = st & 1, bf = st & 1;
+        if (st < 7) {
+          ta[bf ^ 1] = tr(q_lds, st + 1);
+          lgkm_tie1<2>(ta[bf]);
+        } else {
+          lgkm_tie1<0>(ta[bf]);
+        }
+        mfma32_agpr(dK[0][t], ta[bf], sf[0][ss]);
+        mfma32_agpr(dK[1][t], ta[bf], sf[1][ss]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    wait_dma_barrier();
+  }
+  // ---- chunk partial sums: transpose [d][key] accumulators through LDS, row-contiguous adds
+  drain_mfma();
+  float* T = reinterpret_cast<float*>(smem);   // [256 keys][128 d] fp32 = 128 KB
+  auto flush = [&](const f32x16(&acc)[2][4], float mul, float* dst_base) {
+#pragma unroll
+    for (int kg = 0; kg < 2; ++kg)
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int d = 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          const int key = 64 * w + 32 * kg + lr;
+          T[key * 128 + (d ^ ((key & 31) << 2))] = acc[kg][t][r] * mul;
+        }
+    __syncthreads();
+    float* dst = dst_base + (rowB + kv0) * (long)(Hkv * D) + (long)hkv * D;
+    for (int e = tid; e < BKV2 * 128; e += 256) {
+      const int key = e >> 7, d = e & 127;
+      atomicAdd(dst + (long)key * Hkv * D + d, T[key * 128 + (d ^ ((key & 31) << 2))]);
+    }
+    __syncthreads();
+  };
+  flush(dK, scale, dk_acc);
+  flush(dV, 1.f, dv_acc);
+}
+
 // fp32 dK/dV accumulators -> bf16 k/v columns of the fused dqkv [T, (Hq + 2Hkv) * 128]
 __global__ __launch_bounds__(256) void flash_bwd_post_kernel(const float* __restrict__ dk,
                                                              const float* __restrict__ dv,
@@ -752,6 +1009,14 @@ bool bwd_fork_enabled() {
   }();
   return on;
 }
+// KFAMD_FA_DKDV=32 selects the 32-keys-per-wave dK/dV kernel (A/B against the 64-key default)
+bool dkdv64_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("KFAMD_FA_DKDV");
+    return !(e && std::atoi(e) == 32);
+  }();
+  return on;
+}
 BwdFork* bwd_fork() {
   static BwdFork per_dev[64];
   int dev = 0;
@@ -800,17 +1065,31 @@ int kf_flash_bwd(const void* qkv, long ld, const void* o, long ldo, const void* 
   if (skv != st &&
       (hipEventRecord(fk->pre, st) != hipSuccess || hipStreamWaitEvent(skv, fk->pre, 0) != hipSuccess))
     return fail(2);
+  const bool kv64 = dkdv64_enabled() && S % fb2::BKV2 == 0;
   int items = 0;
-  for (int kb = 0; kb < S / BKV; ++kb) items += (S - (causal ? kb * BKV : 0) + QCH - 1) / QCH;
+  if (kv64)
+    for (int kb = 0; kb < S / fb2::BKV2; ++kb) items += fb2::n_chunks(kb, S, causal);
+  else
+    for (int kb = 0; kb < S / BKV; ++kb) items += n_chunks(kb, S, causal);
   const int g_kv = B * Hkv * items, g_q = B * Hq * ((S + BQ8 - 1) / BQ8);
   const float sl2 = scale * LOG2E;
+  if (kv64) {
+    if (causal)
+      flash_bwd_dkdv64_kernel<true><<<g_kv, 256, 0, skv>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo, lse,
+                                                           delta, dk_acc, dv_acc, B, S, Hq, Hkv, scale, items);
+    else
+      flash_bwd_dkdv64_kernel<false><<<g_kv, 256, 0, skv>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo, lse,
+                                                            delta, dk_acc, dv_acc, B, S, Hq, Hkv, scale, items);
+  }
   if (causal) {
-    flash_bwd_dkdv_kernel<true><<<g_kv, 256, 0, skv>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo,
-                                                       lse, delta, dk_acc, dv_acc, B, S, Hq, Hkv, scale, items);
+    if (!kv64)
+      flash_bwd_dkdv_kernel<true><<<g_kv, 256, 0, skv>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo,
+                                                         lse, delta, dk_acc, dv_acc, B, S, Hq, Hkv, scale, items);
     flash_bwd_dq_kernel<true><<<g_q, 512, 0, st>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo, lse,
                                                    delta, (bf16_t*)dqkv, lddqkv, B, S, Hq, Hkv, sl2, scale);
   } else {
-    flash_bwd_dkdv_kernel<false><<<g_kv, 256, 0, skv>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo,
+    if (!kv64)
+      flash_bwd_dkdv_kernel<false><<<g_kv, 256, 0, skv>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo,
                                                         lse, delta, dk_acc, dv_acc, B, S, Hq, Hkv, scale, items);
     flash_bwd_dq_kernel<false><<<g_q, 512, 0, st>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo, lse,
                                                     delta, (bf16_t*)dqkv, lddqkv, B, S, Hq, Hkv, sl2, scale);

@@ -55,9 +55,19 @@ int main(int argc, char** argv) {
   init_bf16<<<4096, 256>>>(dout, (long)T * ldo, 0x9876u, 1.0f);
   CK(hipDeviceSynchronize());
 
-  int items = 0;
-  for (int kb = 0; kb < S / BKV; ++kb) items += (S - kb * BKV + QCH - 1) / QCH;
-  const int g_kv = B * Hkv * items, g_q = B * Hq * ((S + BQ8 - 1) / BQ8), g_f = B * Hq * ((S + BQ8 - 1) / BQ8);
+  int items = 0, items64 = 0;
+  const int g_q = B * Hq * ((S + BQ8 - 1) / BQ8), g_f = B * Hq * ((S + BQ8 - 1) / BQ8);
+  for (int kb = 0; kb < S / BKV; ++kb) items += fb::n_chunks(kb, S, true);
+  for (int kb = 0; kb < S / fb2::BKV2; ++kb) items64 += fb2::n_chunks(kb, S, true);
+  const int g_kv64 = B * Hkv * items64, g_kv = B * Hkv * items;
+  const char* dkv_env = getenv("KFAMD_FA_DKDV");
+  const bool use64 = !(dkv_env && atoi(dkv_env) == 32);
+  auto dkdv_run = [&] {
+    if (use64)
+      flash_bwd_dkdv64_kernel<true><<<g_kv64, 256>>>(qkv, ldq, dout, ldo, lse, delta, dk, dv, B, S, Hq, Hkv, scale, items64);
+    else
+      flash_bwd_dkdv_kernel<true><<<g_kv, 256>>>(qkv, ldq, dout, ldo, lse, delta, dk, dv, B, S, Hq, Hkv, scale, items);
+  };
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
@@ -105,16 +115,14 @@ int main(int argc, char** argv) {
   CK(hipGetLastError());
   double bwd = 0;
   bwd += timeit("pre", 0, [&] { flash_bwd_pre_kernel<<<(T * Hq + 15) / 16, 256>>>(o, ldo, dout, ldo, delta, B, S, Hq); });
-  bwd += timeit("dkdv", 4 * mm, [&] {
-    flash_bwd_dkdv_kernel<true><<<g_kv, 256>>>(qkv, ldq, dout, ldo, lse, delta, dk, dv, B, S, Hq, Hkv, scale, items);
-  });
+  bwd += timeit(use64 ? "dkdv64" : "dkdv", 4 * mm, dkdv_run);
   bwd += timeit("dq", 3 * mm, [&] {
     flash_bwd_dq_kernel<true><<<g_q, 512>>>(qkv, ldq, dout, ldo, lse, delta, dqkv, ldq, B, S, Hq, Hkv, sl2, scale);
   });
   bwd += timeit("post", 0, post);
   // one clean pass for the checks (the timing loops accumulated dK/dV repeatedly)
   zero();
-  flash_bwd_dkdv_kernel<true><<<g_kv, 256>>>(qkv, ldq, dout, ldo, lse, delta, dk, dv, B, S, Hq, Hkv, scale, items);
+  dkdv_run();
   flash_bwd_dq_kernel<true><<<g_q, 512>>>(qkv, ldq, dout, ldo, lse, delta, dqkv, ldq, B, S, Hq, Hkv, sl2, scale);
   post();
   CK(hipDeviceSynchronize());
