@@ -699,13 +699,14 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
 }
 
 // ---- 64 keys per wave, one wave per SIMD (512-register budget) -------------------------
-// The 32-key kernel above is LDS-read bound: per 32-query iteration each wave reads 40 KB
-// (Q and dO row fragments, the K fragments again, Q^T and dO^T transposed fragments) for 32
-// MFMAs, so the CU's 8 waves need ~2560 LDS cycles against ~2048 MFMA cycles per SIMD, and
-// its 256 VGPRs spill.  Here each wave owns 64 keys as two 32-key groups: every Q/dO/Q^T/dO^T
-// fragment read feeds BOTH groups' MFMAs (48 KB for 64 MFMAs; ~1536 LDS cycles per 2048 MFMA
-// cycles on the CU), V stays in registers, and the 256 dK^T/dV^T accumulator registers go
-// to the AGPR half of the unified 512-entry file (1 workgroup of 4 waves per CU).
+// The 32-key kernel above reads 40 KB of LDS per wave and 32-query iteration (Q and dO row
+// fragments, the K fragments again, Q^T and dO^T transposed fragments) for 32 MFMAs, and its
+// 256 VGPRs spill.  Here each wave owns 64 keys as two 32-key groups: every Q/dO/Q^T/dO^T
+// fragment read feeds BOTH groups' MFMAs (48 KB for 64 MFMAs), V stays in registers, and the
+// 256 dK^T/dV^T accumulator registers go to the AGPR half of the unified 512-entry file
+// (1 workgroup of 4 waves per CU).  Measured (profiles/attention_microbench.txt): no spill
+// and the same speed as the 32-key kernel; phase stamps put both MFMA phases at ~2x their
+// MFMA floor, waiting on LDS-read latency at one wave per SIMD.
 namespace fb2 {
 constexpr int BKV2 = 256;                       // keys per workgroup (4 waves x 64)
 constexpr int OFF_K = 0;                       // [256 keys x 256 B] = 64 KB
