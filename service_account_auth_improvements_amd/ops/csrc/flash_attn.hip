@@ -1010,13 +1010,12 @@ bool bwd_fork_enabled() {
   }();
   return on;
 }
-// KFAMD_FA_DKDV=32 selects the 32-keys-per-wave dK/dV kernel (A/B against the 64-key default)
+// dK/dV kernel choice, read per call: the 32-keys-per-wave kernel is the default (in-step
+// 1-GPU Llama-3-8B A/B with the dQ fork: 21.89k vs 21.76k tok/s, profiles/attention_microbench.txt);
+// KFAMD_FA_DKDV=64 selects the 64-key, one-wave-per-SIMD kernel.
 bool dkdv64_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("KFAMD_FA_DKDV");
-    return !(e && std::atoi(e) == 32);
-  }();
-  return on;
+  const char* e = getenv("KFAMD_FA_DKDV");
+  return e && std::atoi(e) == 64;
 }
 BwdFork* bwd_fork() {
   static BwdFork per_dev[64];

@@ -44,10 +44,14 @@ def test_flash_fwd_spiky_scores():
     assert torch.allclose(lse, lse_ref, atol=2e-2, rtol=1e-3)
 
 
+@pytest.mark.parametrize("dkdv", ["32", "64"])
 @pytest.mark.parametrize("B,S,Hq,Hkv,causal", [
     (1, 256, 2, 1, True), (2, 512, 8, 2, True), (1, 1024, 32, 8, True),
     (1, 512, 4, 4, False), (1, 768, 8, 1, True)])
-def test_flash_bwd(B, S, Hq, Hkv, causal):
+def test_flash_bwd(B, S, Hq, Hkv, causal, dkdv, monkeypatch):
+    """Both dK/dV kernels (32 keys per wave, the default, and 64 keys per wave, which needs
+    S % 256 == 0 and otherwise falls back to the 32-key kernel) against fp32 autograd."""
+    monkeypatch.setenv("KFAMD_FA_DKDV", dkdv)
     qkv = _qkv(B, S, Hq, Hkv, seed=S + 3 * Hq)
     sc = 1 / math.sqrt(128)
     o, lse = torch.ops.kfamd.flash_fwd(qkv, B, S, Hq, Hkv, 128, sc, causal)
@@ -92,12 +96,13 @@ def test_flash_bwd_stream_fork_ordering():
         assert err < 1e-2, err
 
 
-@pytest.mark.parametrize("b,g", [(0, 0), (1, 5)])
-def test_flash_fwd_bwd_at_bench_shape(b, g):
+@pytest.mark.parametrize("b,g,dkdv", [(0, 0, "32"), (1, 5, "64")])
+def test_flash_fwd_bwd_at_bench_shape(b, g, dkdv, monkeypatch):
     """The bench's exact launch: B=2, S=8192, Hq=32, Hkv=8, causal (64 heavy-first q-blocks, the
     XCD remap and the dK/dV work-item split as in the training step), checked on one (batch,
     kv-head) GQA group -- its 4 query heads' O / lse / dQ and the group's dK / dV -- against an
-    fp32 autograd reference of that slice."""
+    fp32 autograd reference of that slice; once per dK/dV kernel."""
+    monkeypatch.setenv("KFAMD_FA_DKDV", dkdv)
     B, S, Hq, Hkv, D = 2, 8192, 32, 8, 128
     G = Hq // Hkv
     sc = 1 / math.sqrt(D)

@@ -61,7 +61,7 @@ int main(int argc, char** argv) {
   for (int kb = 0; kb < S / fb2::BKV2; ++kb) items64 += fb2::n_chunks(kb, S, true);
   const int g_kv64 = B * Hkv * items64, g_kv = B * Hkv * items;
   const char* dkv_env = getenv("KFAMD_FA_DKDV");
-  const bool use64 = !(dkv_env && atoi(dkv_env) == 32);
+  const bool use64 = dkv_env && atoi(dkv_env) == 64;
   auto dkdv_run = [&] {
     if (use64)
       flash_bwd_dkdv64_kernel<true><<<g_kv64, 256>>>(qkv, ldq, dout, ldo, lse, delta, dk, dv, B, S, Hq, Hkv, scale, items64);
