@@ -755,6 +755,25 @@ class APIServer:
                 raise NotFound(f'{t.plural} "{meta.get("name")}" not found')
             return self._write(t, cur, copy.deepcopy(obj), t.status_subresource, False, "system:admin")
 
+    def bind_pod(self, namespace: str, name: str, node: str, user: str = "system:kube-scheduler") -> dict:
+        """The ``pods/binding`` subresource (what kube-scheduler POSTs): sets ``spec.nodeName``
+        of an unbound pod; binding a pod that is already bound (to any node) is a 409."""
+        t = self.type_for("v1", "Pod")
+        with self._lock:
+            cur = self._bucket(t).get(self._key(t, namespace, name))
+            if cur is None:
+                raise NotFound(f'pods "{name}" not found')
+            if cur["metadata"].get("deletionTimestamp"):
+                raise Conflict(f'pod {name} is being deleted, cannot be assigned to a host')
+            bound = (cur.get("spec") or {}).get("nodeName")
+            if bound:
+                raise Conflict(f'Operation cannot be fulfilled on pods/binding "{name}": pod {name} is already '
+                               f'assigned to node "{bound}"')
+            new = copy.deepcopy(cur)
+            new["spec"]["nodeName"] = node
+            self._write(t, cur, new, False, False, user)
+        return {"kind": "Status", "apiVersion": "v1", "status": "Success", "code": 201}
+
     def patch(self, api_version: str, kind: str, name: str, namespace: Optional[str], patch,
               patch_type: str = "merge", subresource: Optional[str] = None, dry_run: bool = False,
               user: str = "system:admin") -> dict:

@@ -88,6 +88,9 @@ class InMemoryClient(Client):
     def delete(self, api_version, kind, name, namespace=None, propagation="Background"):
         return self.server.delete(api_version, kind, name, namespace, propagation)
 
+    def bind(self, namespace, name, node):
+        return self.server.bind_pod(namespace, name, node)
+
     def list_with_rv(self, api_version, kind, namespace=None, label_selector=None, field_selector=None):
         return self.server.list_with_rv(api_version, kind, namespace, label_selector, field_selector)
 
@@ -207,6 +210,12 @@ class RestClient(Client):
     def delete(self, api_version, kind, name, namespace=None, propagation="Background"):
         return self._req("DELETE", self._path(api_version, kind, namespace, name),
                          {"kind": "DeleteOptions", "apiVersion": "v1", "propagationPolicy": propagation})
+
+    def bind(self, namespace, name, node):
+        """POST pods/{name}/binding (a Binding to node ``node``)."""
+        body = {"apiVersion": "v1", "kind": "Binding", "metadata": {"name": name, "namespace": namespace},
+                "target": {"apiVersion": "v1", "kind": "Node", "name": node}}
+        return self._req("POST", self._path("v1", "Pod", namespace, name, "binding"), body)
 
     WATCH_TIMEOUT = 300        # seconds per watch request before it is re-opened from the last RV
 

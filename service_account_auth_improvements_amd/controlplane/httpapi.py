@@ -83,6 +83,9 @@ def make_handler(server: APIServer):
                     items, rv = server.list_with_rv(av, t.kind, ns, q.get("labelSelector"), q.get("fieldSelector"))
                     return self._send(200, {"apiVersion": av, "kind": f"{t.kind}List", "items": items,
                                             "metadata": {"resourceVersion": rv}})
+                if method == "POST" and sub == "binding" and t.kind == "Pod":
+                    body = self._body() or {}
+                    return self._send(201, server.bind_pod(ns, name, (body.get("target") or {}).get("name", "")))
                 if method == "POST":
                     body = self._body()
                     body.setdefault("apiVersion", av)

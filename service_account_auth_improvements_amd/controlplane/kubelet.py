@@ -126,8 +126,8 @@ class DeploymentController(Controller):
 class DevicePlugin:
     """amd.com/gpu allocator for one node: hands out concrete GPU indices."""
 
-    def __init__(self, n_gpus: int):
-        self.free = list(range(n_gpus))
+    def __init__(self, n_gpus: int, base: int = 0):
+        self.free = list(range(base, base + n_gpus))
         self.owner: Dict[str, List[int]] = {}
 
     def allocate(self, pod_uid: str, n: int) -> Optional[List[int]]:
@@ -159,10 +159,15 @@ class Kubelet(Controller):
     name = "kubelet"
 
     def __init__(self, client: Client, node_name: str = "node-0", n_gpus: int = 8, exec_pods: bool = False,
-                 extra_env: Optional[dict] = None, workdir: Optional[str] = None, log_dir: Optional[str] = None):
+                 extra_env: Optional[dict] = None, workdir: Optional[str] = None, log_dir: Optional[str] = None,
+                 self_schedule: bool = True, gpu_base: int = 0):
         super().__init__(client)
         self.node = node_name
-        self.dp = DevicePlugin(n_gpus)
+        self.name = "kubelet" if node_name == "node-0" else f"kubelet-{node_name}"
+        # self_schedule: the single-node cluster's kubelet claims every unbound pod; with a
+        # scheduler (multi-node clusters) it runs only the pods bound to its node
+        self.self_schedule = self_schedule
+        self.dp = DevicePlugin(n_gpus, gpu_base)
         self.exec_pods = exec_pods
         self.extra_env = extra_env or {}
         self.workdir = workdir
@@ -218,9 +223,14 @@ class Kubelet(Controller):
         if phase in ("Succeeded", "Failed"):
             self.dp.release(uid)
             return Result()
-        if not pod["spec"].get("nodeName"):
+        bound = pod["spec"].get("nodeName")
+        if not bound:
+            if not self.self_schedule:
+                return Result()
             pod["spec"]["nodeName"] = self.node
             pod = c.update(pod)
+        elif bound != self.node:
+            return Result()
         if phase in (None, "", "Pending"):
             ngpu = pod_gpu_request(pod)
             ids = self.dp.allocate(uid, ngpu) if ngpu else []

@@ -11,6 +11,9 @@ loads / hipBLASLt heuristics).  Prints one JSON line with p50/p90 and the breakd
 
   python tools/bench_crd_to_step.py --jobs 5 --model llama3-8b --gpus 1
   python tools/bench_crd_to_step.py --jobs 3 --model mnist --gpus 0 --nodes 2   # configs[0]
+  python tools/bench_crd_to_step.py --processes ...   # apiserver / controller-manager /
+      # kubelet(s) as separate processes over HTTP (cluster.ProcessCluster): the job CR, its
+      # pods and their status travel through the REST API and watches as on a real cluster
 """
 import argparse
 import json
@@ -35,18 +38,25 @@ def main():
     ap.add_argument("--layers", type=int, default=None)
     ap.add_argument("--timeout", type=float, default=300)
     ap.add_argument("--gap", type=float, default=0.0, help="idle seconds between jobs (GPU memory settle)")
+    ap.add_argument("--processes", action="store_true",
+                    help="control plane and node agents as separate processes over HTTP (one kubelet per node)")
     a = ap.parse_args()
 
-    from service_account_auth_improvements_amd.cluster import LocalCluster
+    from service_account_auth_improvements_amd.cluster import LocalCluster, ProcessCluster
     from service_account_auth_improvements_amd.controlplane import training
     from service_account_auth_improvements_amd.native import build_native
     build_native()
     tmp = tempfile.mkdtemp(prefix="crd2step-")
     events = os.path.join(tmp, "events.jsonl")
-    n_gpus = a.gpus * a.nodes
-    cl = LocalCluster(n_gpus=n_gpus, exec_pods=True, api_port=None, log_dir=tmp,
-                      extra_env={"KFAMD_EVENTS_FILE": events, "OMP_NUM_THREADS": "4"}).start()
-    cl.server.ensure_namespace("bench")
+    env = {"KFAMD_EVENTS_FILE": events, "OMP_NUM_THREADS": "4"}
+    if a.processes:
+        cl = ProcessCluster(nodes=a.nodes, gpus_per_node=a.gpus, exec_pods=True, log_dir=tmp, extra_env=env).start()
+        client, pod_log = cl.client, cl.pod_log
+        client.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "bench"}})
+    else:
+        cl = LocalCluster(n_gpus=a.gpus * a.nodes, exec_pods=True, api_port=None, log_dir=tmp, extra_env=env).start()
+        client, pod_log = cl.client, cl.kubelet.pod_log
+        cl.server.ensure_namespace("bench")
     dev = "cuda" if a.gpus else "cpu"
     cmd = [sys.executable, "-m", "service_account_auth_improvements_amd", "train", "--model", a.model,
            "--steps", "1", "--device", dev]
@@ -68,13 +78,13 @@ def main():
             if not a.gpus:
                 job["spec"]["nprocPerNode"] = "1"
             t0 = time.time()
-            cl.client.create(job)
+            client.create(job)
             t_running = None
             first = None
             deadline = t0 + a.timeout
             while time.time() < deadline:
                 if t_running is None:
-                    p = cl.client.get_or_none("v1", "Pod", f"{name}-master-0", "bench")
+                    p = client.get_or_none("v1", "Pod", f"{name}-master-0", "bench")
                     if p and (p.get("status") or {}).get("phase") == "Running":
                         t_running = time.time()
                 evs = [json.loads(x) for x in open(events).read().splitlines() if x.strip()]
@@ -84,7 +94,7 @@ def main():
                     break
                 time.sleep(0.01)
             if first is None:
-                log = cl.kubelet.pod_log("bench", f"{name}-master-0")
+                log = pod_log("bench", f"{name}-master-0")
                 raise SystemExit(f"{name}: no first_step within {a.timeout}s\n{log[-3000:]}")
             r0 = [e for e in evs if e.get("rank") == 0]
             ps = next(e["ts"] for e in r0 if e["event"] == "process_start")
@@ -101,7 +111,7 @@ def main():
             print(json.dumps({"job": name, **{k: round(v, 3) for k, v in rows[-1].items()}}), flush=True)
             # wait for the job to finish so the GPUs are free for the next one
             while time.time() < deadline:
-                jb = cl.client.get(training.PT_API, "PyTorchJob", name, "bench")
+                jb = client.get(training.PT_API, "PyTorchJob", name, "bench")
                 if any(c["type"] in ("Succeeded", "Failed") and c["status"] == "True"
                        for c in (jb.get("status") or {}).get("conditions", [])):
                     break
@@ -110,6 +120,7 @@ def main():
         cl.stop()
     tot = sorted(r["total"] for r in rows)
     out = {"metric": "CRD-to-first-step", "model": a.model, "gpus_per_node": a.gpus, "nodes": a.nodes,
+           "control_plane": "processes over HTTP" if a.processes else "in-process",
            "gap_s": a.gap,
            "jobs": len(rows), "p50_s": round(statistics.median(tot), 3),
            "p90_s": round(tot[min(len(tot) - 1, int(0.9 * len(tot)))], 3), "min_s": round(tot[0], 3),
