@@ -79,9 +79,11 @@ class Scheduler(Controller):
         seen_bound = set()
         for p in pods:
             node = (p.get("spec") or {}).get("nodeName")
-            if not node or (p.get("status") or {}).get("phase") in ("Succeeded", "Failed"):
+            if not node:
                 continue
-            seen_bound.add(p["metadata"].get("uid"))
+            seen_bound.add(p["metadata"].get("uid"))      # the view has the binding: drop the assumption
+            if (p.get("status") or {}).get("phase") in ("Succeeded", "Failed"):
+                continue
             used[node] = used.get(node, 0) + pod_gpu_request(p)
             count[node] = count.get(node, 0) + 1
         live = {p["metadata"].get("uid") for p in pods}

@@ -137,3 +137,20 @@ def test_two_node_pytorchjob_across_processes(tmp_path):
         assert {e["rank"] for e in firsts} == {0, 1}
     finally:
         pc.stop()
+
+
+def test_finished_pod_frees_its_gpus_for_the_next_binding():
+    """The assume cache must let go of a binding once the view shows the pod bound -- also when
+    the pod has already finished by then (short jobs on a 1-GPU node, back to back)."""
+    cl = LocalCluster(n_gpus=1, nodes=2, api_port=None)
+    c, m = cl.client, cl.manager
+    cl.server.ensure_namespace("team")
+    for i in range(4):
+        c.create(_pod(f"p{i}", 1))
+        m.run_until_idle()
+        node = _node_of(c, f"p{i}")
+        assert node is not None, i
+        p = c.get("v1", "Pod", f"p{i}", "team")
+        p["status"] = dict(p.get("status") or {}, phase="Succeeded")
+        c.update_status(p)
+        m.run_until_idle()
