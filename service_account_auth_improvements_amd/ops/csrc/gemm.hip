@@ -23,7 +23,7 @@
 //    hoisted above the wait for its operands.
 //  * Products are computed as C^T tiles (operands swapped): each lane holds 4 consecutive
 //    output columns -> 8-byte stores (and loads when accumulating).
-//  * XCD-aware bijective block remap + grouped (8 M-tiles) raster: the workgroups of one
+//  * XCD-aware bijective block remap + grouped (4 M-tiles) raster: the workgroups of one
 //    XCD share A and B panels in its L2.
 //  * s_setprio(1/0) around each MFMA group measured null (tools/kbench/gemm_bench: 1276 vs
 //    1279 TF over the step's dW shapes), so the schedule is left to the counted waits.
@@ -41,7 +41,12 @@ namespace gm {
 constexpr int BM = 256, BN = 256, BK = 32, NBUF = 4;
 constexpr int IMG = BK * 256;               // one [32][128] bf16 image: 8 KB
 constexpr int SMEM = 4 * NBUF * IMG;        // images laid out [image][buffer]: 128 KB
-constexpr int GROUP_M = 8;
+// M-tiles per raster group: 4 measured 1.0-1.3 % faster than 8 over the step's dW shapes on
+// two boxes (16 / 32: -3 % / -6 %; tools/gpu_r2_gemm.sh); -DKF_GEMM_GROUP_M overrides
+#ifndef KF_GEMM_GROUP_M
+#define KF_GEMM_GROUP_M 4
+#endif
+constexpr int GROUP_M = KF_GEMM_GROUP_M;
 
 __device__ __forceinline__ int blk_x(int row) { return (row & 3) | ((row >> 1) & 4); }
 
