@@ -25,6 +25,9 @@
 //    output columns -> 8-byte stores (and loads when accumulating).
 //  * XCD-aware bijective block remap + grouped (4 M-tiles) raster: the workgroups of one
 //    XCD share A and B panels in its L2.
+//  * The four DMA pieces of a stage go out as one burst: one piece per MFMA group measured
+//    0.5 % slower, and additionally staggering the two waves of a SIMD 4 % slower
+//    (profiles/gemm_dw_raster_group.txt).
 //  * s_setprio(1/0) around each MFMA group measured null (tools/kbench/gemm_bench: 1276 vs
 //    1279 TF over the step's dW shapes), so the schedule is left to the counted waits.
 //  * A 4-wave variant (2 x 2 waves of 128 x 128, 256 accumulators pinned to AGPRs with

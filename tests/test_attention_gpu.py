@@ -134,3 +134,59 @@ def test_flash_fwd_bwd_at_bench_shape(b, g, dkdv, monkeypatch):
     assert rel(dq_s, dq_r) < 3e-2
     assert rel(dqkv[rows, (Hq + g) * D:(Hq + g + 1) * D].float(), dk_r) < 3e-2
     assert rel(dqkv[rows, (Hq + Hkv + g) * D:(Hq + Hkv + g + 1) * D].float(), dv_r) < 3e-2
+
+
+@pytest.mark.parametrize("dkdv", ["32", "64"])
+def test_flash_long_context_32k(dkdv, monkeypatch):
+    """Long context: S = 32768, causal GQA 8/2, B = 1.  The forward's O / lse and
+    the backward's dQ are checked on the LAST 256 query rows of one head (they attend to every
+    key), dK / dV on the first 256 keys of one kv-head (every query attends to them), against
+    fp32 references over the full key / query range of that slice."""
+    assert _ext.load()
+    monkeypatch.setenv("KFAMD_FA_DKDV", dkdv)
+    B, S, Hq, Hkv, D = 1, 32768, 8, 2, 128
+    G = Hq // Hkv
+    sc = 1 / math.sqrt(D)
+    qkv = _qkv(B, S, Hq, Hkv, seed=5)
+    o, lse = torch.ops.kfamd.flash_fwd(qkv, B, S, Hq, Hkv, D, sc, True)
+    do = torch.randn(o.shape, generator=torch.Generator(device="cpu").manual_seed(21)).to(DEV, torch.bfloat16)
+    dqkv = torch.ops.kfamd.flash_bwd(qkv, o, lse, do, B, S, Hq, Hkv, D, sc, True)
+    torch.cuda.synchronize()
+    h, g = 5, 5 // G
+    k = qkv[:, (Hq + g) * D:(Hq + g + 1) * D].float()
+    v = qkv[:, (Hq + Hkv + g) * D:(Hq + Hkv + g + 1) * D].float()
+
+    def rel(a, r):
+        return ((a - r).abs().max() / r.abs().max()).item()
+    # last 256 query rows of head h: O, lse, dQ
+    rows = slice(S - 256, S)
+    q = qkv[rows, h * D:(h + 1) * D].float().requires_grad_(True)
+    s = (q @ k.t()) * sc
+    qi = torch.arange(S - 256, S, device=DEV)[:, None]
+    s = s.masked_fill(torch.arange(S, device=DEV)[None, :] > qi, float("-inf"))
+    o_ref = torch.softmax(s, -1) @ v
+    assert (o[rows, h * D:(h + 1) * D].float() - o_ref).abs().max().item() < 2e-2
+    assert torch.allclose(lse[0, h, rows], torch.logsumexp(s, -1), atol=2e-3, rtol=1e-4)
+    (dq_r,) = torch.autograd.grad(o_ref, q, do[rows, h * D:(h + 1) * D].float())
+    assert rel(dqkv[rows, h * D:(h + 1) * D].float(), dq_r) < 3e-2
+    # first 256 keys of kv-head g: dK / dV summed over the group's query heads and all queries
+    dk_r = torch.zeros(256, D, device=DEV)
+    dv_r = torch.zeros(256, D, device=DEV)
+    for hq in range(g * G, (g + 1) * G):
+        for c0 in range(0, S, 4096):            # query chunks bound the fp32 score memory
+            qc = qkv[c0:c0 + 4096, hq * D:(hq + 1) * D].float()
+            # probabilities need the full causal row: keys 0 .. c0 + 4095
+            kf = k[:c0 + 4096]
+            sf = (qc @ kf.t()) * sc
+            sf = sf.masked_fill(torch.arange(c0 + 4096, device=DEV)[None, :] >
+                                torch.arange(c0, c0 + 4096, device=DEV)[:, None], float("-inf"))
+            lse_c = torch.logsumexp(sf, -1, keepdim=True)
+            p = torch.exp(sf[:, :256] - lse_c)                 # probabilities on the 256 keys
+            dO = do[c0:c0 + 4096, hq * D:(hq + 1) * D].float()
+            dP = dO @ v[:c0 + 4096].t()
+            delta = (dO * (torch.exp(sf - lse_c) @ v[:c0 + 4096])).sum(-1, keepdim=True)
+            ds = p * (dP[:, :256] - delta)
+            dv_r += p.t() @ dO
+            dk_r += (ds.t() @ qc) * sc
+    assert rel(dqkv[:256, (Hq + g) * D:(Hq + g + 1) * D].float(), dk_r) < 3e-2
+    assert rel(dqkv[:256, (Hq + Hkv + g) * D:(Hq + Hkv + g + 1) * D].float(), dv_r) < 3e-2
