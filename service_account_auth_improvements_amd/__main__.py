@@ -19,6 +19,7 @@ Components (reference flags kept where they exist):
 * ``centraldashboard``      --port (env: PROFILES_KFAM_SERVICE_HOST/PORT, PROMETHEUS_URL...)
 * ``predictor``             the InferenceService model server (serving/server.py)
 * ``train``                 the PyTorchJob worker entry (runtime/train_entry.py)
+* ``mpi-wait``              the MPIJob launcher for mpirun-style jobs (controlplane/mpi.py)
 * ``cluster``               the single-process local cluster (cluster.py)
 """
 from __future__ import annotations
@@ -79,6 +80,9 @@ def main(argv=None):
         return m(rest)
     if comp == "cluster":
         from .cluster import main as m
+        return m(rest)
+    if comp == "mpi-wait":
+        from .controlplane.mpi import main as m
         return m(rest)
 
     ap = argparse.ArgumentParser(prog=f"kfamd {comp}")

@@ -109,6 +109,8 @@ class LocalCluster:
             self.client.create(cr)
         self.server.ensure_namespace("kubeflow")
         env = {"PYTHONPATH": REPO}
+        if self.http is not None:     # pods that talk to the API server (e.g. the MPIJob launcher)
+            env["KUBE_API_URL"] = self.http.url
         env.update(extra_env or {})
         # nodes > 1: n_gpus GPUs per node, distinct device indices, pods placed by the scheduler
         self.kubelets = [Kubelet(self.client, node_name=f"node-{i}", n_gpus=n_gpus, exec_pods=exec_pods,
@@ -251,7 +253,7 @@ class ProcessCluster:
                     "--gpu-base", str(i * self.gpus), "--log-dir", self.log_dir, "--workdir", self.workdir]
             if self.exec_pods:
                 args.append("--exec-pods")
-            for k, v in self.extra_env.items():
+            for k, v in dict({"KUBE_API_URL": self.url}, **self.extra_env).items():
                 args += ["--env", f"{k}={v}"]
             self._spawn(f"kubelet-{i}", args)
         # ready when every node has registered and the controller manager answers

@@ -11,7 +11,8 @@
 //    agent its global rank offset, the world size and a round id.  A restart starts a new
 //    round, so all nodes restart their workers together.
 // 2. Spawn: P workers per node, each with RANK, LOCAL_RANK, WORLD_SIZE,
-//    LOCAL_WORLD_SIZE, GROUP_RANK, NODE_RANK, MASTER_ADDR, MASTER_PORT, the ROCm IPC
+//    LOCAL_WORLD_SIZE, GROUP_RANK, NODE_RANK, MASTER_ADDR, MASTER_PORT (and the OpenMPI
+//    OMPI_COMM_WORLD_{RANK,SIZE,LOCAL_RANK,LOCAL_SIZE} names), the ROCm IPC
 //    setting HSA_ENABLE_IPC_MODE_LEGACY=0 (dmabuf IPC for RCCL / tensor sharing) and
 //    TORCH_NCCL_ASYNC_ERROR_HANDLING=1 (RCCL async error -> abort, so a hung/failed
 //    collective surfaces as a process exit).  With --isolate-devices each worker gets
@@ -280,6 +281,11 @@ pid_t spawn(const Args& a, const Assignment& as, int lr, const std::string& hb) 
   set("MASTER_ADDR", a.master_addr);
   set("MASTER_PORT", std::to_string(a.master_port));
   set("KFAMD_RDZV_ROUND", std::to_string(as.round));
+  // the OpenMPI names too, for programs written against mpirun's environment (MPIJob workers)
+  set("OMPI_COMM_WORLD_RANK", std::to_string(as.rank_offset + lr));
+  set("OMPI_COMM_WORLD_SIZE", std::to_string(as.world));
+  set("OMPI_COMM_WORLD_LOCAL_RANK", std::to_string(lr));
+  set("OMPI_COMM_WORLD_LOCAL_SIZE", std::to_string(a.nproc));
   set("HSA_ENABLE_IPC_MODE_LEGACY", "0");
   set("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1");
   if (!hb.empty()) set("KFAMD_HEARTBEAT_FILE", hb);
