@@ -42,8 +42,9 @@ COMPONENTS = {
     "pvcviewer_controller": ("PVCViewer Controller", [f"{PKG}/controlplane/pvcviewer.py"],
                              "tests/test_controllers.py -k pvcviewer", "platform", "pvcviewer-controller"),
     "training_operator": ("Training Operator (PyTorchJob / MPIJob)",
-                          [f"{PKG}/controlplane/training.py", f"{PKG}/native/**"],
-                          "tests/test_training_operator.py tests/test_native_sanitize.py", "platform",
+                          [f"{PKG}/controlplane/training.py", f"{PKG}/controlplane/mpi.py", f"{PKG}/native/**"],
+                          "tests/test_training_operator.py tests/test_mpijob.py tests/test_native_sanitize.py",
+                          "platform",
                           "training-operator"),
     "jwa": ("Jupyter Web App", [f"{PKG}/webapps/jupyter.py", f"{PKG}/webapps/crud_backend.py",
                                 f"{PKG}/webapps/config/**"],
