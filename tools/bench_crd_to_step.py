@@ -27,6 +27,24 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def mpijob_manifest(name, ns, program, workers, gpus, port):
+    """Upstream-shaped MPIJob: Launcher ``mpirun -np workers*gpus program``, Workers run sshd
+    (the training operator translates it, controlplane/mpi.py)."""
+    from service_account_auth_improvements_amd.controlplane import training
+    slots = max(gpus, 1)
+    wc = {"name": "worker", "image": "local", "command": ["/usr/sbin/sshd", "-De"]}
+    if gpus:
+        wc["resources"] = {"limits": {"amd.com/gpu": str(gpus)}}
+    lc = {"name": "launcher", "image": "local",
+          "command": ["mpirun", "--allow-run-as-root", "-np", str(workers * slots)] + list(program)}
+    return {"apiVersion": training.MPI_API, "kind": "MPIJob",
+            "metadata": {"name": name, "namespace": ns, "annotations": {"kfamd.io/master-port": str(port)}},
+            "spec": {"slotsPerWorker": slots, "runPolicy": {"cleanPodPolicy": "None"},
+                     "mpiReplicaSpecs": {"Launcher": {"replicas": 1, "template": {"spec": {"containers": [lc]}}},
+                                         "Worker": {"replicas": workers,
+                                                    "template": {"spec": {"containers": [wc]}}}}}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--jobs", type=int, default=5)
@@ -38,6 +56,8 @@ def main():
     ap.add_argument("--layers", type=int, default=None)
     ap.add_argument("--timeout", type=float, default=300)
     ap.add_argument("--gap", type=float, default=0.0, help="idle seconds between jobs (GPU memory settle)")
+    ap.add_argument("--kind", choices=["pytorchjob", "mpijob"], default="pytorchjob",
+                    help="mpijob: an upstream-style MPIJob (Launcher mpirun -np G, Worker with G GPUs)")
     ap.add_argument("--processes", action="store_true",
                     help="control plane and node agents as separate processes over HTTP (one kubelet per node)")
     a = ap.parse_args()
@@ -73,10 +93,15 @@ def main():
                 time.sleep(a.gap)
             name = f"job{j}"
             open(events, "w").close()
-            job = training.pytorchjob_manifest(name, "bench", "local", cmd, n_nodes=a.nodes, gpus_per_node=a.gpus,
-                                               master_port=29700 + 7 * j)
-            if not a.gpus:
-                job["spec"]["nprocPerNode"] = "1"
+            if a.kind == "mpijob":
+                job = mpijob_manifest(name, "bench", cmd, a.nodes, a.gpus, 29700 + 7 * j)
+                rank0_pod = f"{name}-worker-0"
+            else:
+                job = training.pytorchjob_manifest(name, "bench", "local", cmd, n_nodes=a.nodes,
+                                                   gpus_per_node=a.gpus, master_port=29700 + 7 * j)
+                if not a.gpus:
+                    job["spec"]["nprocPerNode"] = "1"
+                rank0_pod = f"{name}-master-0"
             t0 = time.time()
             client.create(job)
             t_running = None
@@ -84,7 +109,7 @@ def main():
             deadline = t0 + a.timeout
             while time.time() < deadline:
                 if t_running is None:
-                    p = client.get_or_none("v1", "Pod", f"{name}-master-0", "bench")
+                    p = client.get_or_none("v1", "Pod", rank0_pod, "bench")
                     if p and (p.get("status") or {}).get("phase") == "Running":
                         t_running = time.time()
                 evs = [json.loads(x) for x in open(events).read().splitlines() if x.strip()]
@@ -94,7 +119,7 @@ def main():
                     break
                 time.sleep(0.01)
             if first is None:
-                log = pod_log("bench", f"{name}-master-0")
+                log = pod_log("bench", rank0_pod)
                 raise SystemExit(f"{name}: no first_step within {a.timeout}s\n{log[-3000:]}")
             r0 = [e for e in evs if e.get("rank") == 0]
             ps = next(e["ts"] for e in r0 if e["event"] == "process_start")
@@ -111,7 +136,7 @@ def main():
             print(json.dumps({"job": name, **{k: round(v, 3) for k, v in rows[-1].items()}}), flush=True)
             # wait for the job to finish so the GPUs are free for the next one
             while time.time() < deadline:
-                jb = client.get(training.PT_API, "PyTorchJob", name, "bench")
+                jb = client.get(job["apiVersion"], job["kind"], name, "bench")
                 if any(c["type"] in ("Succeeded", "Failed") and c["status"] == "True"
                        for c in (jb.get("status") or {}).get("conditions", [])):
                     break
@@ -119,7 +144,8 @@ def main():
     finally:
         cl.stop()
     tot = sorted(r["total"] for r in rows)
-    out = {"metric": "CRD-to-first-step", "model": a.model, "gpus_per_node": a.gpus, "nodes": a.nodes,
+    out = {"metric": "CRD-to-first-step", "kind": a.kind, "model": a.model, "gpus_per_node": a.gpus,
+           "nodes": a.nodes,
            "control_plane": "processes over HTTP" if a.processes else "in-process",
            "gap_s": a.gap,
            "jobs": len(rows), "p50_s": round(statistics.median(tot), 3),
