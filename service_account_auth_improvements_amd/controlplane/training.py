@@ -432,3 +432,23 @@ def pytorchjob_manifest(name: str, namespace: str, image: str, command: List[str
             "spec": {"nprocPerNode": str(gpus_per_node) if gpus_per_node else "1",
                      "runPolicy": {"backoffLimit": backoff_limit, "cleanPodPolicy": "None"},
                      "pytorchReplicaSpecs": specs}}
+
+
+def mpijob_manifest(name: str, namespace: str, image: str, program: List[str], workers: int = 1,
+                    gpus_per_worker: int = 8, master_port: Optional[int] = None) -> dict:
+    """An MPIJob in the upstream mpi-operator shape: the Launcher runs ``mpirun -np N program``
+    over the hostfile, the Workers run sshd (N = workers x slots).  The operator translates it
+    (see MPIJobReconciler / controlplane/mpi.py)."""
+    slots = max(gpus_per_worker, 1)
+    wc = {"name": "worker", "image": image, "command": ["/usr/sbin/sshd", "-De"]}
+    if gpus_per_worker:
+        wc["resources"] = {"limits": {GPU: str(gpus_per_worker)}}
+    lc = {"name": "launcher", "image": image,
+          "command": ["mpirun", "--allow-run-as-root", "-np", str(workers * slots)] + list(program)}
+    ann = {"kfamd.io/master-port": str(master_port)} if master_port else {}
+    return {"apiVersion": MPI_API, "kind": "MPIJob",
+            "metadata": {"name": name, "namespace": namespace, "annotations": ann},
+            "spec": {"slotsPerWorker": slots, "runPolicy": {"cleanPodPolicy": "None"},
+                     "mpiReplicaSpecs": {"Launcher": {"replicas": 1, "template": {"spec": {"containers": [lc]}}},
+                                         "Worker": {"replicas": workers,
+                                                    "template": {"spec": {"containers": [wc]}}}}}}

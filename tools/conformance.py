@@ -6,8 +6,9 @@ Against a cluster's Kubernetes REST API (``--kube-api``) or an in-process LocalC
 
 1. create Profile ``kf-conformance`` (owner, quota cpu 4 / memory 4Gi / storage 5Gi) and wait
    for its namespace, service accounts, role bindings and quota;
-2. run the training conformance job -- a 2-replica MNIST PyTorchJob over gloo through the
-   operator and the kfamd-launch launcher -- and wait for ``Succeeded``;
+2. run the training conformance jobs -- a 2-replica MNIST PyTorchJob over gloo through the
+   operator and the kfamd-launch launcher, and the same MNIST run as an upstream-shaped MPIJob
+   (Launcher ``mpirun -np 2``, 2 Workers running sshd) -- and wait for ``Succeeded``;
 3. (optional ``--gpu``) a 1-GPU Llama PyTorchJob step on MI355X;
 4. write a JSON report (one record per check) and exit non-zero on any failure.
 
@@ -39,8 +40,8 @@ def wait(fn, timeout):
     return None
 
 
-def job_done(c, name):
-    j = c.get("kubeflow.org/v1", "PyTorchJob", name, NS)
+def job_done(c, name, api="kubeflow.org/v1", kind="PyTorchJob"):
+    j = c.get(api, kind, name, NS)
     for cd in (j.get("status") or {}).get("conditions") or []:
         if cd["type"] in ("Succeeded", "Failed") and cd["status"] == "True":
             return cd["type"]
@@ -63,7 +64,8 @@ def main(argv=None):
     else:
         from service_account_auth_improvements_amd.cluster import LocalCluster
         build_native()
-        cl = LocalCluster(n_gpus=1 if a.gpu else 0, exec_pods=True, api_port=None,
+        # the REST facade is up so the MPIJob launcher (mpi-wait) can follow its workers
+        cl = LocalCluster(n_gpus=1 if a.gpu else 0, exec_pods=True, api_port=0,
                           extra_env={"OMP_NUM_THREADS": "2"}).start()
         c = cl.client
     results = []
@@ -91,6 +93,11 @@ def main(argv=None):
         c.create(job)
         res = wait(lambda: job_done(c, "mnist-conformance"), a.timeout)
         check("training: PyTorchJob 2-replica MNIST (gloo)", res == "Succeeded", f"result={res}")
+        mj = training.mpijob_manifest("mnist-mpi-conformance", NS, "kfamd/trainer-rocm:latest", cmd, workers=2,
+                                      gpus_per_worker=0, master_port=29821)
+        c.create(mj)
+        res = wait(lambda: job_done(c, "mnist-mpi-conformance", training.MPI_API, "MPIJob"), a.timeout)
+        check("training: MPIJob mpirun -np 2 MNIST (gloo)", res == "Succeeded", f"result={res}")
         if a.gpu:
             cmd = [sys.executable, "-m", "service_account_auth_improvements_amd", "train", "--model", "llama3-8b",
                    "--seq-len", "2048", "--steps", "2", "--device", "cuda"]
