@@ -49,6 +49,26 @@ def _free_port() -> int:
     return port
 
 
+def _auto_micro_batch(dp: int, zero1: bool, grad_reduce: str, collectives: bool, grad_accum: int = 1,
+                      budget_gib: float = 268.0) -> int:
+    """Largest micro-batch (<= 4) of Llama-3-8B at 8k whose peak fits a 288 GB MI355X with ~20 GiB
+    left for RCCL and transients.  Measured at dp1 (profiles/dp_path_rehearsal.md): 190.1 GiB at
+    micro-batch 2, +34.3 GiB per sequence; the fp32 DP reduction adds the fp32 gradient (30 GiB,
+    1/dp of it as ZeRO-1 shards, and a full fp32 accumulator with grad_accum > 1); ZeRO-1 removes (1 - 1/dp) of the 89.7 GiB fp32 master + AdamW
+    moments."""
+    extra = 0.0
+    if collectives and grad_reduce == "fp32":
+        extra += 30.0 / dp if zero1 else 30.0
+    if grad_reduce == "fp32" and grad_accum > 1 and not (collectives and not zero1):
+        extra += 30.0
+    if zero1:
+        extra -= 89.7 * (1.0 - 1.0 / dp)
+    for mb in (4, 3, 2):
+        if 190.1 + 34.3 * (mb - 2) + extra <= budget_gib:
+            return mb
+    return 1
+
+
 def _launch_ranks(n: int) -> int:
     """Run this script as N ranks under torch.distributed.run (a child process; this process
     has not initialised the GPU and never does)."""
@@ -67,8 +87,9 @@ def main():
     ap.add_argument("--model", default="llama3-8b")
     ap.add_argument("--seq-len", type=int, default=8192)
     ap.add_argument("--micro-batch", type=int, default=0,
-                    help="sequences per micro-batch; 0 = auto: 4 on a 288 GB MI355X for Llama-3-8B at 8k "
-                         "(chunked LM head, ~260 GiB peak: profiles/chunked_head_microbatch.md), else 2")
+                    help="sequences per micro-batch; 0 = auto: the largest <= 4 that fits a 288 GB MI355X for "
+                         "Llama-3-8B at 8k under the run's DP memory plan (_auto_micro_batch; 4 at dp1 and "
+                         "for ZeRO-1 at any N), else 2")
     ap.add_argument("--grad-accum", type=int, default=1)
     ap.add_argument("--zero1", dest="zero1", action="store_true", default=None,
                     help="ZeRO-1: reduce-scatter grads, 1/N-sharded AdamW, parameter all-gather hidden "
@@ -84,6 +105,9 @@ def main():
                     help="per-layer activation recomputation (memory plans that need it, e.g. 70B at long S)")
     ap.add_argument("--head-chunk", type=int, default=4096,
                     help="LM head + cross-entropy row chunk in tokens (0 = materialise all logits)")
+    ap.add_argument("--force-collectives", action="store_true",
+                    help="REHEARSAL: run the DP collectives (ZeRO-1 / fp32 reduction) on a one-rank RCCL "
+                         "group, to check the N > 1 path's memory and call sequence at full size on one GPU")
     ap.add_argument("--layers", type=int, default=None, help="DEBUG ONLY: invalid for reporting")
     ap.add_argument("--json-out", default=None)
     a = ap.parse_args()
@@ -95,21 +119,34 @@ def main():
         print(f"bench: --gpus {a.gpus} but WORLD_SIZE={env_world}: refusing to report a "
               "different GPU count", file=sys.stderr)
         sys.exit(2)
+    if a.force_collectives:
+        if a.gpus != 1:
+            sys.exit("bench: --force-collectives is a one-GPU rehearsal")
+        for k, v in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", str(_free_port())), ("RANK", "0"),
+                     ("LOCAL_RANK", "0"), ("WORLD_SIZE", "1")):
+            os.environ.setdefault(k, v)
+        if torch.cuda.is_available():
+            torch.cuda.set_device(0)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+        else:
+            dist.init_process_group("gloo")
     st = init_distributed(tp=a.tp, pp=a.pp)
     world = st.world_size
+    if a.zero1 is None:
+        a.zero1 = (st.dp > 1 or a.force_collectives) and a.pp == 1
     if a.micro_batch <= 0:
         big = (st.device.type == "cuda" and torch.cuda.get_device_properties(st.device).total_memory >= 280e9
                and a.model == "llama3-8b" and a.seq_len <= 8192 and a.tp == 1 and a.pp == 1)
-        a.micro_batch = 4 if big else 2
+        a.micro_batch = _auto_micro_batch(st.dp, a.zero1, a.grad_reduce, st.dp > 1 or a.force_collectives,
+                                           a.grad_accum) if big else 2
     backend = dist.get_backend() if dist.is_initialized() else "none"
     world_seen = dist.get_world_size() if dist.is_initialized() else 1
     assert world_seen == a.gpus, (world_seen, a.gpus)
-    if a.zero1 is None:
-        a.zero1 = st.dp > 1 and a.pp == 1
     tcfg = TrainConfig(model=a.model, seq_len=a.seq_len, micro_batch=a.micro_batch,
                        grad_accum=a.grad_accum, zero1=a.zero1, bucket_mb=a.bucket_mb,
                        grad_reduce=a.grad_reduce,
-                       n_layers=a.layers, recompute=a.recompute, head_chunk=a.head_chunk)
+                       n_layers=a.layers, recompute=a.recompute, head_chunk=a.head_chunk,
+                       force_collectives=a.force_collectives)
     t0 = time.time()
     if a.pp > 1:
         from service_account_auth_improvements_amd.parallel.pipeline import PipelineTrainer
@@ -195,6 +232,8 @@ def main():
         }
         if a.layers is not None:
             out["INVALID"] = "reduced layer count (debug run)"
+        if a.force_collectives:
+            out["rehearsal"] = "DP collectives forced on a one-rank group"
         line = json.dumps(out)
         print(line, flush=True)
         if a.json_out:

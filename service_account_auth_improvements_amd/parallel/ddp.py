@@ -240,6 +240,9 @@ class GradReducer:
         if not self.enabled or self.mode != "reduce_scatter":
             return
         r = dist.get_rank(self.dp_group) if self.dp_group is not None else dist.get_rank()
+        # RCCL gathers in place (input = output + rank * n, the NCCL in-place contract): no
+        # staging copy of the shard and no transient 1/dp-of-the-model buffer; gloo needs one
+        in_place = dist.get_backend(self.dp_group) == "nccl"
         # small groups (norm weights) first: every layer reads one of them, and the gathers
         # complete in launch order on the communicator's stream
         for name, bl in sorted(self.buckets.items(), key=lambda kv: kv[1][-1].hi if kv[1] else 0):
@@ -247,8 +250,9 @@ class GradReducer:
                 b = bl[idx]
                 x = b.group.params[b.lo:b.hi]
                 n = (b.hi - b.lo) // self.dp
+                mine = x[r * n:(r + 1) * n]
                 self._gathers[(name, idx)] = dist.all_gather_into_tensor(
-                    x, x[r * n:(r + 1) * n].clone(), group=self.dp_group, async_op=True)
+                    x, mine if in_place else mine.clone(), group=self.dp_group, async_op=True)
         if not overlap:
             self.wait_all_params()
 

@@ -74,3 +74,30 @@ def test_bench_refuses_world_size_mismatch():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", *ARGS],
                        capture_output=True, text=True, timeout=300, env=env, cwd="/tmp")
     assert r.returncode != 0 and not _json_lines(r.stdout)
+
+
+def test_bench_rehearsal_flag_marks_the_record():
+    """``--force-collectives`` runs the ZeRO-1 / fp32-reduction path on a one-rank group and says so."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--force-collectives", *ARGS],
+                       capture_output=True, text=True, timeout=300, env=env, cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-2000:]
+    recs = _json_lines(r.stdout)
+    assert len(recs) == 1
+    _check(recs[0], 1)
+    assert recs[0]["rehearsal"] and recs[0]["config"]["optimizer_sharding"] == "zero1"
+    assert recs[0]["backend"] == "gloo"
+
+
+def test_auto_micro_batch_memory_plan():
+    """Micro-batch 4 at dp1 and for ZeRO-1 at every N; 3 when a full fp32 gradient buffer is added."""
+    sys.path.insert(0, ROOT)
+    import bench
+    for dp in (1, 2, 4, 8):
+        assert bench._auto_micro_batch(dp, dp > 1, "fp32", dp > 1) == 4
+        assert bench._auto_micro_batch(dp, dp > 1, "bf16", dp > 1) == 4
+    for dp in (2, 4, 8):
+        assert bench._auto_micro_batch(dp, False, "fp32", True) == 3      # fp32 all-reduce staging
+    assert bench._auto_micro_batch(1, True, "fp32", True) == 3            # one-rank rehearsal
+    assert bench._auto_micro_batch(1, False, "fp32", False, grad_accum=4) == 3

@@ -51,11 +51,13 @@ def _rccl_body(rank, world):
     y = torch.empty_like(x)
     w = dist.all_gather_into_tensor(y, x.clone(), async_op=True)
     w.wait()
+    z = x.clone()
+    dist.all_gather_into_tensor(z, z[0:4096], async_op=True).wait()   # in place: input = output + rank*n
     dist.broadcast(x, src=0)
     r = torch.empty_like(x)
     dist.all_to_all_single(r, x, async_op=True).wait()
     torch.cuda.synchronize()
-    out["raw_ok"] = bool(torch.equal(x, ref) and torch.equal(y, ref) and torch.equal(r, ref))
+    out["raw_ok"] = bool(torch.equal(x, ref) and torch.equal(y, ref) and torch.equal(r, ref) and torch.equal(z, ref))
 
     for zero1, mode in CASES:
         with_pg = _train(st, zero1, mode, force=True)
