@@ -101,6 +101,9 @@ def main():
                          "fp32 micro-batch accumulation) or bf16 (RCCL bf16 reduce-scatter / all-reduce)")
     ap.add_argument("--tp", type=int, default=1, help="tensor parallel degree (configs[4]: 70B TP=8)")
     ap.add_argument("--pp", type=int, default=1, help="pipeline parallel degree (1F1B)")
+    ap.add_argument("--sp", action="store_true",
+                    help="Megatron sequence parallelism on top of --tp: norms / residual on 1/tp of the token "
+                         "rows, reduce-scatter + all-gather in place of the TP all-reduces")
     ap.add_argument("--recompute", action="store_true",
                     help="per-layer activation recomputation (memory plans that need it, e.g. 70B at long S)")
     ap.add_argument("--head-chunk", type=int, default=4096,
@@ -146,7 +149,7 @@ def main():
                        grad_accum=a.grad_accum, zero1=a.zero1, bucket_mb=a.bucket_mb,
                        grad_reduce=a.grad_reduce,
                        n_layers=a.layers, recompute=a.recompute, head_chunk=a.head_chunk,
-                       force_collectives=a.force_collectives)
+                       force_collectives=a.force_collectives, sequence_parallel=a.sp)
     t0 = time.time()
     if a.pp > 1:
         from service_account_auth_improvements_amd.parallel.pipeline import PipelineTrainer
@@ -218,6 +221,7 @@ def main():
                 "n_layers": tr.mcfg.n_layers,
                 "attention": "hip",
                 "activation_recompute": a.recompute,
+                "sequence_parallel": bool(a.sp and a.tp > 1),
                 "head_chunk": a.head_chunk,
             },
             "backend": backend,

@@ -34,7 +34,8 @@ import torch.nn.functional as F
 
 from .. import ops
 from ..ops.attention import attention_bwd, attention_fwd
-from ..parallel.state import ParallelState, get_state, tp_all_reduce
+from ..parallel.state import (ParallelState, get_state, tp_all_gather_rows, tp_all_reduce,
+                              tp_reduce_scatter_rows)
 
 # KFAMD_DX_T=0 runs the activation-gradient GEMMs on the untransposed weights (A/B switch)
 _DX_T = os.environ.get("KFAMD_DX_T", "1") != "0"
@@ -146,6 +147,12 @@ class Llama:
         # K5: LM head + cross-entropy in row chunks of this many tokens (0 = one chunk): the
         # [T, vocab] logits are never materialised -- only one [chunk, vocab] slab at a time
         self.head_chunk = 4096
+        # Megatron sequence parallelism (tp > 1): the residual stream, the RMSNorms and their
+        # saved activations hold only this rank's 1/tp block of token rows; an all-gather feeds
+        # each column-parallel GEMM and a reduce-scatter (instead of the all-reduce) ends each
+        # row-parallel one -- the same bytes per layer, 1/tp of the norm/residual activations
+        self.sequence_parallel = False
+        self._sp_norm_parts: list = []
         cos, sin = ops.rope_tables(cfg.max_seq, D, cfg.rope_theta)
         self.cos = cos.to(self.device)
         self.sin = sin.to(self.device)
@@ -239,14 +246,50 @@ class Llama:
         self._mm_into(o0, a0, b0, accumulate)
         self._mm_into(o1, a1, b1, accumulate)
 
+    # ------------------------------------------------------------------ TP / SP collectives
+    @property
+    def _sp(self) -> bool:
+        return self.sequence_parallel and self.tp > 1
+
+    def _gather(self, x):
+        """SP: this rank's token rows -> all rows (identity without SP)."""
+        return tp_all_gather_rows(x, self.st) if self._sp else x
+
+    def _reduce_out(self, x):
+        """Partial sums of a row-parallel product: SP -> this rank's rows (reduce-scatter),
+        else all rows (all-reduce; a no-op at tp 1)."""
+        return tp_reduce_scatter_rows(x, self.st) if self._sp else tp_all_reduce(x, self.st)
+
+    def _norm_bwd(self, dy, h, rstd, name: str, accumulate: bool, dres=None):
+        """K1 backward.  Under SP each rank sees 1/tp of the rows, so the norm weight gradient
+        is a partial sum: it goes to a scratch row and is all-reduced (fp32) over the TP group
+        at the end of the stage's backward (:meth:`_sp_finish_norms`)."""
+        if not self._sp:
+            return ops.rmsnorm_bwd(dy, h, rstd, self.P(name), self.G(name), accumulate, dres=dres)
+        part = torch.empty_like(self.G(name))
+        dh = ops.rmsnorm_bwd(dy, h, rstd, self.P(name), part, False, dres=dres)
+        self._sp_norm_parts.append((name, part, accumulate))
+        return dh
+
+    def _sp_finish_norms(self):
+        if not self._sp_norm_parts:
+            return
+        parts, self._sp_norm_parts = self._sp_norm_parts, []
+        tot = torch.stack([p.float() for _, p, _ in parts])
+        dist.all_reduce(tot, group=self.st.tp_group)
+        for k, (name, _, acc) in enumerate(parts):
+            G = self.G(name)
+            G.copy_(tot[k] + G.float() if acc else tot[k])
+
     # ------------------------------------------------------------------ embedding
     def embed_fwd(self, tokens: torch.Tensor) -> torch.Tensor:
         """K7 gather (vocab-parallel: rows outside this rank's shard are zero, then summed)."""
         x = ops.embed_fwd(tokens, self.P("embed"), self.vstart if self.tp > 1 else 0)
-        return tp_all_reduce(x, self.st) if self.tp > 1 else x
+        return self._reduce_out(x) if self.tp > 1 else x
 
     def embed_bwd(self, tokens: torch.Tensor, g: torch.Tensor, accumulate: bool):
         """K7 scatter-add straight into the flat gradient buffer's embedding slice."""
+        g = self._gather(g)
         ops.embed_bwd_(tokens, g, self.G("embed"), self.vstart if self.tp > 1 else 0, accumulate)
         self._ready(self.mats, "embed")
 
@@ -255,15 +298,15 @@ class Llama:
         cfg = self.cfg
         c = _LayerCtx()
         a, h1, rstd1 = ops.rmsnorm_fwd(r, self.P(f"l{i}.norm1"), cfg.norm_eps, residual=d)
-        qkv = torch.mm(a, self.P(f"l{i}.wqkv").t())
+        qkv = torch.mm(self._gather(a), self.P(f"l{i}.wqkv").t())
         ops.rope_(qkv, self.hq + self.hkv, cfg.head_dim, self.cos, self.sin, seq_len=S)
         o, lse = attention_fwd(qkv, B, S, self.hq, self.hkv, cfg.head_dim)
-        da = tp_all_reduce(torch.mm(o, self.P(f"l{i}.wo").t()), self.st)
+        da = self._reduce_out(torch.mm(o, self.P(f"l{i}.wo").t()))
         m, h2, rstd2 = ops.rmsnorm_fwd(h1, self.P(f"l{i}.norm2"), cfg.norm_eps, residual=da)
         del da
-        gu = torch.mm(m, self.P(f"l{i}.wgu").t())
+        gu = torch.mm(self._gather(m), self.P(f"l{i}.wgu").t())
         s = ops.swiglu_fwd(gu)
-        dm = tp_all_reduce(torch.mm(s, self.P(f"l{i}.wd").t()), self.st)
+        dm = self._reduce_out(torch.mm(s, self.P(f"l{i}.wd").t()))
         c.h1, c.rstd1, c.a, c.qkv, c.o, c.lse = h1, rstd1, a, qkv, o, lse
         c.h2, c.rstd2, c.m, c.gu, c.s = h2, rstd2, m, gu, s
         return h2, dm, c
@@ -274,28 +317,34 @@ class Llama:
         # The four weight gradients run as two grouped dW launches whose tile counts fill whole
         # waves of the 256 CUs: {wgu, wo} (7 + 1 waves at Llama-3-8B) as soon as dh2 exists,
         # {wd, wqkv} (3.5 + 1.5) at the end -- separately, wd and wqkv each end on a half wave.
+        # Under SP, g / dh2 / the saved norm outputs a, m are this rank's token rows: the GEMMs
+        # read their all-gathered forms (the backward of a reduce-scatter is an all-gather) and
+        # the input gradients of the column-parallel GEMMs are reduce-scattered.
         # MLP
-        gs = self._mm_dx(g, Wd)
+        gf = self._gather(g)
+        gs = self._mm_dx(gf, Wd)
         dgu = ops.swiglu_bwd(c.gu, gs)
         del gs
         c.gu = None
-        dmm = tp_all_reduce(self._mm_dx(dgu, Wgu), self.st)
-        dh2 = ops.rmsnorm_bwd(dmm, c.h2, c.rstd2, self.P(f"l{i}.norm2"), self.G(f"l{i}.norm2"),
-                              accumulate, dres=g)
+        dmm = self._reduce_out(self._mm_dx(dgu, Wgu))
+        dh2 = self._norm_bwd(dmm, c.h2, c.rstd2, f"l{i}.norm2", accumulate, dres=g)
         del dmm
-        self._mm_into2((self.G(f"l{i}.wgu"), dgu.t(), c.m), (self.G(f"l{i}.wo"), dh2.t(), c.o), accumulate)
+        dh2f = self._gather(dh2)
+        self._mm_into2((self.G(f"l{i}.wgu"), dgu.t(), self._gather(c.m)), (self.G(f"l{i}.wo"), dh2f.t(), c.o),
+                       accumulate)
         del dgu
         # attention
-        do = self._mm_dx(dh2, Wo)
+        do = self._mm_dx(dh2f, Wo)
+        del dh2f
         dqkv = attention_bwd(c.qkv, c.o, c.lse, do, B, S, self.hq, self.hkv, cfg.head_dim)
         del do
         ops.rope_(dqkv, self.hq + self.hkv, cfg.head_dim, self.cos, self.sin, seq_len=S, inverse=True)
-        da = tp_all_reduce(self._mm_dx(dqkv, Wqkv), self.st)
-        self._mm_into2((self.G(f"l{i}.wd"), g.t(), c.s), (self.G(f"l{i}.wqkv"), dqkv.t(), c.a), accumulate)
+        da = self._reduce_out(self._mm_dx(dqkv, Wqkv))
+        self._mm_into2((self.G(f"l{i}.wd"), gf.t(), c.s), (self.G(f"l{i}.wqkv"), dqkv.t(), self._gather(c.a)),
+                       accumulate)
         c.s = None
-        del dqkv
-        dh1 = ops.rmsnorm_bwd(da, c.h1, c.rstd1, self.P(f"l{i}.norm1"), self.G(f"l{i}.norm1"),
-                              accumulate, dres=dh2)
+        del dqkv, gf
+        dh1 = self._norm_bwd(da, c.h1, c.rstd1, f"l{i}.norm1", accumulate, dres=dh2)
         self._ready(self.mats, f"l{i}.wqkv")
         return dh1
 
@@ -333,6 +382,7 @@ class Llama:
         the dy products (forward operand layout, see _mm_dx).  dW_head is accumulated across
         chunks by the dW kernel (bf16 output, fp32 inside each chunk)."""
         h, rstd, y, labels, scale, loss = ctx
+        y = self._gather(y)
         W = self.P("lm_head")
         T = y.shape[0]
         tc = self.head_chunk if self.head_chunk and self.head_chunk < T else T
@@ -353,9 +403,9 @@ class Llama:
             del logits, rows
         loss.add_(tot * scale)
         del Wt
-        dy = tp_all_reduce(dy, self.st)
+        dy = self._reduce_out(dy)
         self._ready(self.mats, "lm_head")
-        dh = ops.rmsnorm_bwd(dy, h, rstd, self.P("final_norm"), self.G("final_norm"), accumulate)
+        dh = self._norm_bwd(dy, h, rstd, "final_norm", accumulate)
         return dh
 
     # ------------------------------------------------------------------ stage-level API
@@ -392,6 +442,8 @@ class Llama:
         """inp: tokens [B*S] (first stage) or activation [B*S, H].  Returns (out, ctx) where
         out is the loss (last stage) or the activation handed to the next stage."""
         ctx = {"layers": []}
+        if self._sp:
+            assert (B * S) % self.tp == 0, f"sequence parallelism needs B*S divisible by tp ({B}x{S}, tp {self.tp})"
         if self.first:
             ctx["tokens"] = inp
             self._wait("embed", "embed")
@@ -434,7 +486,8 @@ class Llama:
             del c
         if self.first:
             self.embed_bwd(ctx["tokens"], g, accumulate)
-            return None
+            g = None
+        self._sp_finish_norms()
         return g
 
     def forward_backward(self, tokens: torch.Tensor, labels: torch.Tensor, accumulate: bool = False,
@@ -455,4 +508,4 @@ class Llama:
         for i in self.layers:
             r, d, _ = self.layer_fwd(i, r, d, B, S)
         y, _, _ = ops.rmsnorm_fwd(r, self.P("final_norm"), self.cfg.norm_eps, residual=d)
-        return torch.mm(y, self.P("lm_head").t()).view(B, S, -1)
+        return torch.mm(self._gather(y), self.P("lm_head").t()).view(B, S, -1)

@@ -181,6 +181,7 @@ class PipelineTrainer:
         self.model = Llama(mcfg, st, layer_range=lr, seed=tcfg.seed, full_init=full_init)
         self.model.recompute = tcfg.recompute
         self.model.head_chunk = getattr(tcfg, "head_chunk", self.model.head_chunk)
+        self.model.sequence_parallel = getattr(tcfg, "sequence_parallel", False)
         self.model.allocate()
         self.reducer = GradReducer(self.model.groups, st.dp_group, st.dp,
                                    bucket_bytes=tcfg.bucket_mb << 20,
@@ -193,6 +194,8 @@ class PipelineTrainer:
                              tp_sharded={"matrices": st.tp_group} if st.tp > 1 else None,
                              grad_view=self.reducer.grad_view)
         T = tcfg.micro_batch * tcfg.seq_len
+        if self.model.sequence_parallel and st.tp > 1:
+            T //= st.tp                     # stages exchange this rank's block of token rows
         self.p2p = P2P(st, (T, mcfg.hidden), torch.bfloat16, st.device)
 
     def _hook(self, on: bool):

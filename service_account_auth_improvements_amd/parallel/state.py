@@ -127,6 +127,28 @@ def tp_all_reduce(x: torch.Tensor, st: Optional[ParallelState] = None) -> torch.
     return x
 
 
+def tp_all_gather_rows(x: torch.Tensor, st: Optional[ParallelState] = None) -> torch.Tensor:
+    """Sequence parallelism: this rank's contiguous block of token rows -> all rows (rank order)."""
+    st = st or get_state()
+    if st.tp == 1:
+        return x
+    out = torch.empty((x.shape[0] * st.tp,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    dist.all_gather_into_tensor(out, x.contiguous(), group=st.tp_group)
+    return out
+
+
+def tp_reduce_scatter_rows(x: torch.Tensor, st: Optional[ParallelState] = None) -> torch.Tensor:
+    """Sequence parallelism: partial sums over all token rows -> this rank's block of summed rows
+    (replaces the all-reduce after a row-parallel GEMM: same result rows, half the bytes)."""
+    st = st or get_state()
+    if st.tp == 1:
+        return x
+    assert x.shape[0] % st.tp == 0, (x.shape, st.tp)
+    out = torch.empty((x.shape[0] // st.tp,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    dist.reduce_scatter_tensor(out, x.contiguous(), group=st.tp_group)
+    return out
+
+
 def barrier():
     if dist.is_initialized():
         dist.barrier()

@@ -42,6 +42,10 @@ def main(argv=None):
     ap.add_argument("--tp", type=int, default=1)
     ap.add_argument("--pp", type=int, default=1)
     ap.add_argument("--zero1", action="store_true")
+    ap.add_argument("--sp", action="store_true", help="sequence parallelism on top of --tp (Megatron SP)")
+    ap.add_argument("--recompute", action="store_true", help="per-layer activation recomputation")
+    ap.add_argument("--grad-reduce", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--head-chunk", type=int, default=4096)
     ap.add_argument("--layers", type=int, default=None)
     ap.add_argument("--device", default="auto", choices=["auto", "cpu", "cuda"])
     ap.add_argument("--save", default=None, help="checkpoint directory written at the end")
@@ -71,7 +75,8 @@ def main(argv=None):
             tr.step_idx = int(load_checkpoint(a.resume, tr, data=data)["step"])
         return _loop(a, tr, data, st, t_start)
     tcfg = TrainConfig(model=a.model, seq_len=a.seq_len, micro_batch=a.micro_batch, grad_accum=a.grad_accum,
-                       zero1=a.zero1, n_layers=a.layers)
+                       zero1=a.zero1, n_layers=a.layers, sequence_parallel=a.sp, recompute=a.recompute,
+                       grad_reduce=a.grad_reduce, head_chunk=a.head_chunk)
     if a.pp > 1:
         from ..parallel.pipeline import PipelineTrainer
         tr = PipelineTrainer(tcfg, st)

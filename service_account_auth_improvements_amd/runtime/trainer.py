@@ -45,6 +45,7 @@ class TrainConfig:
     n_layers: Optional[int] = None   # override (tests only; benches must use the full model)
     recompute: bool = False          # per-layer activation recomputation (memory for compute)
     head_chunk: int = 4096           # K5: LM head + CE row chunk (tokens); 0 = whole micro-batch
+    sequence_parallel: bool = False  # Megatron SP on top of TP (token-row-sharded norms / residual)
 
 
 class Trainer:
@@ -63,6 +64,7 @@ class Trainer:
         self.model = Llama(mcfg, self.st, seed=tcfg.seed, full_init=full_init)
         self.model.recompute = tcfg.recompute
         self.model.head_chunk = tcfg.head_chunk
+        self.model.sequence_parallel = tcfg.sequence_parallel
         self.model.allocate(pad_to=self.st.dp * 64 if tcfg.zero1 else 1)
         self._sync()
         self.init_times = {"params_alloc_init_s": time.time() - t0}

@@ -1,4 +1,5 @@
 """Multi-process (gloo, world 2) correctness of DP (all-reduce and ZeRO-1) and TP."""
+import pytest
 import torch
 
 from dist_util import run_ranks
@@ -67,25 +68,30 @@ def test_zero1_matches_allreduce():
     assert torch.equal(zb[0][1], z[0][1]) and zb[0][0] == z[0][0]
 
 
-def _tp_body(rank, world):
+def _tp_body(rank, world, sp=False):
     from service_account_auth_improvements_amd.models.llama import Llama, LlamaConfig
     from service_account_auth_improvements_amd.parallel.state import init_distributed
     st = init_distributed(tp=world, pp=1, device="cpu")
     cfg = LlamaConfig.preset("tiny")
     m = Llama(cfg, st, device="cpu", seed=9, full_init=True).allocate()
+    m.sequence_parallel = sp
+    assert m._sp == sp
     tok, lab = _tiny_batches(cfg.vocab_size, 1, seed=3)[0]
     loss = m.forward_backward(tok, lab)
     return float(loss), {s.name: m.G(s.name).float().clone() for g in m.groups for s in g.specs}
 
 
-def test_tensor_parallel_matches_tp1():
+@pytest.mark.parametrize("sp", [False, True], ids=["tp", "tp+sp"])
+def test_tensor_parallel_matches_tp1(sp):
+    """TP=2 (and TP=2 with Megatron sequence parallelism: row-sharded norms / residual, all-gather
+    before and reduce-scatter after the TP GEMMs, TP-summed norm gradients) == TP=1 gradients."""
     from service_account_auth_improvements_amd.models.llama import Llama, LlamaConfig
     from service_account_auth_improvements_amd.parallel.state import ParallelState
     cfg = LlamaConfig.preset("tiny")
     ref = Llama(cfg, ParallelState(), device="cpu", seed=9, full_init=True).allocate()
     tok, lab = _tiny_batches(cfg.vocab_size, 1, seed=3)[0]
     ref_loss = float(ref.forward_backward(tok, lab))
-    res = run_ranks(_tp_body, world=2)
+    res = run_ranks(_tp_body, world=2, args=(sp,))
     for rank, (loss, grads) in enumerate(res):
         assert abs(loss - ref_loss) < 1e-2 * ref_loss, (loss, ref_loss)
         # shard the reference grads exactly like the TP model shards its weights

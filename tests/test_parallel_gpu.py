@@ -67,7 +67,7 @@ def test_ddp_two_ranks_one_gpu_matches_single_process(zero1):
         assert bool((~torch.isnan(g0) | ~torch.isnan(g1)).all())
 
 
-def _tp_body(rank, world, clip):
+def _tp_body(rank, world, clip, sp=False):
     import os
 
     os.environ["KFAMD_DIST_BACKEND"] = "gloo"
@@ -75,22 +75,25 @@ def _tp_body(rank, world, clip):
     from service_account_auth_improvements_amd.runtime.trainer import TrainConfig, Trainer
 
     st = init_distributed(tp=world, pp=1, device="cuda")
-    tr = Trainer(TrainConfig(model="small", seq_len=256, micro_batch=2, n_layers=2, lr=1e-3, max_grad_norm=clip), st,
-                 full_init=True)
+    tr = Trainer(TrainConfig(model="small", seq_len=256, micro_batch=2, n_layers=2, lr=1e-3, max_grad_norm=clip,
+                             sequence_parallel=sp), st, full_init=True)
+    assert tr.model._sp == sp
     losses = [float(tr.train_step([(x.to(st.device), y.to(st.device))]))
               for x, y in _batches(tr.mcfg.vocab_size, 2, seed=11)]
     torch.cuda.synchronize()
     return losses, tr.model.norms.params.float().cpu()
 
 
-def test_tensor_parallel_two_ranks_one_gpu_matches_tp1():
+@pytest.mark.parametrize("sp", [False, True], ids=["tp", "tp+sp"])
+def test_tensor_parallel_two_ranks_one_gpu_matches_tp1(sp):
     """Megatron TP=2 on the GPU kernels (sharded GEMMs and transposes, vocab-parallel CE,
-    TP-aware clipping) == TP=1, two full AdamW steps with clipping active."""
+    TP-aware clipping) == TP=1, two full AdamW steps with clipping active; and the same with
+    sequence parallelism (row-sharded RMSNorm kernels, TP-summed norm gradients)."""
     from service_account_auth_improvements_amd.parallel.state import ParallelState
     from service_account_auth_improvements_amd.runtime.trainer import TrainConfig, Trainer
 
     clip = 0.05
-    res = run_ranks(_tp_body, world=2, args=(clip,), timeout=300)
+    res = run_ranks(_tp_body, world=2, args=(clip, sp), timeout=300)
     st = ParallelState(device=torch.device("cuda", 0))
     tr = Trainer(TrainConfig(model="small", seq_len=256, micro_batch=2, n_layers=2, lr=1e-3, max_grad_norm=clip), st,
                  full_init=True)

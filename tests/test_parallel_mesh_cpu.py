@@ -19,13 +19,13 @@ def _batches(vocab, n, B=2, S=32, seed=0):
             for _ in range(n)]
 
 
-def _mesh_body(rank, world, tp, pp, n_micro, grad_reduce):
+def _mesh_body(rank, world, tp, pp, n_micro, grad_reduce, sp=False):
     from service_account_auth_improvements_amd.parallel.pipeline import PipelineTrainer
     from service_account_auth_improvements_amd.parallel.state import init_distributed
     from service_account_auth_improvements_amd.runtime.trainer import TrainConfig, Trainer
     st = init_distributed(tp=tp, pp=pp, device="cpu")
     tcfg = TrainConfig(model="tiny", seq_len=32, micro_batch=2, grad_accum=n_micro, n_layers=4, lr=LR,
-                       zero1=st.dp > 1 and pp == 1, bucket_mb=1, grad_reduce=grad_reduce)
+                       zero1=st.dp > 1 and pp == 1, bucket_mb=1, grad_reduce=grad_reduce, sequence_parallel=sp)
     tr = PipelineTrainer(tcfg, st, full_init=True) if pp > 1 else Trainer(tcfg, st, full_init=True)
     losses = []
     for step in range(STEPS):
@@ -50,14 +50,15 @@ def _reference(n_batches_per_step, n_layers=4):
     return tr, losses
 
 
-@pytest.mark.parametrize("tp,pp", [(2, 1), (1, 2), (2, 2)], ids=["dp2xtp2", "dp2xpp2", "tp2xpp2"])
-def test_2d_mesh_training_matches_single_process(tp, pp):
+@pytest.mark.parametrize("tp,pp,sp", [(2, 1, False), (1, 2, False), (2, 2, False), (2, 1, True), (2, 2, True)],
+                         ids=["dp2xtp2", "dp2xpp2", "tp2xpp2", "dp2xtp2+sp", "tp2xpp2+sp"])
+def test_2d_mesh_training_matches_single_process(tp, pp, sp):
     from service_account_auth_improvements_amd.models.llama import Llama
     from service_account_auth_improvements_amd.parallel.state import ParallelState
     world = 4
     dp = world // (tp * pp)
     n_micro = 2
-    res = run_ranks(_mesh_body, world=world, args=(tp, pp, n_micro, "fp32"), timeout=600)
+    res = run_ranks(_mesh_body, world=world, args=(tp, pp, n_micro, "fp32", sp), timeout=600)
     ref, ref_losses = _reference(dp * n_micro)
     # every (dp, tp, pp) coordinate appears exactly once
     assert sorted(r["coords"] for r in res) == sorted((d, t, p) for d in range(dp) for t in range(tp)
