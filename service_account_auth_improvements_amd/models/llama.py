@@ -34,6 +34,7 @@ import torch.nn.functional as F
 
 from .. import ops
 from ..ops.attention import attention_bwd, attention_fwd
+from ..parallel import context as cpx
 from ..parallel.state import (ParallelState, get_state, tp_all_gather_rows, tp_all_reduce,
                               tp_reduce_scatter_rows)
 
@@ -92,7 +93,7 @@ class LlamaConfig:
 
 
 class _LayerCtx:
-    __slots__ = ("h1", "rstd1", "a", "qkv", "o", "lse", "h2", "rstd2", "m", "gu", "s")
+    __slots__ = ("h1", "rstd1", "a", "qkv", "o", "o_tok", "lse", "h2", "rstd2", "m", "gu", "s")
 
 
 class Llama:
@@ -153,6 +154,9 @@ class Llama:
         # row-parallel one -- the same bytes per layer, 1/tp of the norm/residual activations
         self.sequence_parallel = False
         self._sp_norm_parts: list = []
+        # context parallelism (parallel/context.py): this rank holds 1/cp of every sequence's
+        # tokens; attention runs on all tokens for 1/cp of the heads between two all-to-alls
+        self.cp, self.cp_rank, self.cp_group = 1, 0, None
         cos, sin = ops.rope_tables(cfg.max_seq, D, cfg.rope_theta)
         self.cos = cos.to(self.device)
         self.sin = sin.to(self.device)
@@ -246,6 +250,11 @@ class Llama:
         self._mm_into(o0, a0, b0, accumulate)
         self._mm_into(o1, a1, b1, accumulate)
 
+    def set_context_parallel(self, group, size: int, rank: int):
+        assert self.hq % size == 0 and self.hkv % size == 0, \
+            f"context parallelism needs the (per-TP-rank) heads {self.hq}/{self.hkv} divisible by cp={size}"
+        self.cp, self.cp_rank, self.cp_group = size, rank, group
+
     # ------------------------------------------------------------------ TP / SP collectives
     @property
     def _sp(self) -> bool:
@@ -299,15 +308,20 @@ class Llama:
         c = _LayerCtx()
         a, h1, rstd1 = ops.rmsnorm_fwd(r, self.P(f"l{i}.norm1"), cfg.norm_eps, residual=d)
         qkv = torch.mm(self._gather(a), self.P(f"l{i}.wqkv").t())
-        ops.rope_(qkv, self.hq + self.hkv, cfg.head_dim, self.cos, self.sin, seq_len=S)
-        o, lse = attention_fwd(qkv, B, S, self.hq, self.hkv, cfg.head_dim)
-        da = self._reduce_out(torch.mm(o, self.P(f"l{i}.wo").t()))
+        D, cp = cfg.head_dim, self.cp
+        hq, hkv, Sa = self.hq // cp, self.hkv // cp, S * cp
+        if cp > 1:   # own tokens x all heads -> all tokens x own head group
+            qkv = cpx.to_heads(qkv, B, S, [self.hq * D, self.hkv * D, self.hkv * D], cp, self.cp_group)
+        ops.rope_(qkv, hq + hkv, D, self.cos, self.sin, seq_len=Sa)
+        o, lse = attention_fwd(qkv, B, Sa, hq, hkv, D)
+        o_tok = cpx.to_tokens(o, B, S, [hq * D], cp, self.cp_group) if cp > 1 else o
+        da = self._reduce_out(torch.mm(o_tok, self.P(f"l{i}.wo").t()))
         m, h2, rstd2 = ops.rmsnorm_fwd(h1, self.P(f"l{i}.norm2"), cfg.norm_eps, residual=da)
         del da
         gu = torch.mm(self._gather(m), self.P(f"l{i}.wgu").t())
         s = ops.swiglu_fwd(gu)
         dm = self._reduce_out(torch.mm(s, self.P(f"l{i}.wd").t()))
-        c.h1, c.rstd1, c.a, c.qkv, c.o, c.lse = h1, rstd1, a, qkv, o, lse
+        c.h1, c.rstd1, c.a, c.qkv, c.o, c.o_tok, c.lse = h1, rstd1, a, qkv, o, o_tok, lse
         c.h2, c.rstd2, c.m, c.gu, c.s = h2, rstd2, m, gu, s
         return h2, dm, c
 
@@ -330,15 +344,21 @@ class Llama:
         dh2 = self._norm_bwd(dmm, c.h2, c.rstd2, f"l{i}.norm2", accumulate, dres=g)
         del dmm
         dh2f = self._gather(dh2)
-        self._mm_into2((self.G(f"l{i}.wgu"), dgu.t(), self._gather(c.m)), (self.G(f"l{i}.wo"), dh2f.t(), c.o),
+        self._mm_into2((self.G(f"l{i}.wgu"), dgu.t(), self._gather(c.m)), (self.G(f"l{i}.wo"), dh2f.t(), c.o_tok),
                        accumulate)
         del dgu
-        # attention
+        # attention (context parallel: the same all-to-alls as forward, in reverse roles)
+        D, cp = cfg.head_dim, self.cp
+        hq, hkv, Sa = self.hq // cp, self.hkv // cp, S * cp
         do = self._mm_dx(dh2f, Wo)
         del dh2f
-        dqkv = attention_bwd(c.qkv, c.o, c.lse, do, B, S, self.hq, self.hkv, cfg.head_dim)
+        if cp > 1:
+            do = cpx.to_heads(do, B, S, [self.hq * D], cp, self.cp_group)
+        dqkv = attention_bwd(c.qkv, c.o, c.lse, do, B, Sa, hq, hkv, D)
         del do
-        ops.rope_(dqkv, self.hq + self.hkv, cfg.head_dim, self.cos, self.sin, seq_len=S, inverse=True)
+        ops.rope_(dqkv, hq + hkv, D, self.cos, self.sin, seq_len=Sa, inverse=True)
+        if cp > 1:
+            dqkv = cpx.to_tokens(dqkv, B, S, [hq * D, hkv * D, hkv * D], cp, self.cp_group)
         da = self._reduce_out(self._mm_dx(dqkv, Wqkv))
         self._mm_into2((self.G(f"l{i}.wd"), gf.t(), c.s), (self.G(f"l{i}.wqkv"), dqkv.t(), self._gather(c.a)),
                        accumulate)

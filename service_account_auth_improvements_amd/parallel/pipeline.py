@@ -182,6 +182,7 @@ class PipelineTrainer:
         self.model.recompute = tcfg.recompute
         self.model.head_chunk = getattr(tcfg, "head_chunk", self.model.head_chunk)
         self.model.sequence_parallel = getattr(tcfg, "sequence_parallel", False)
+        assert not getattr(tcfg, "context_parallel", False), "context parallelism is not combined with PP"
         self.model.allocate()
         self.reducer = GradReducer(self.model.groups, st.dp_group, st.dp,
                                    bucket_bytes=tcfg.bucket_mb << 20,

@@ -46,6 +46,9 @@ class TrainConfig:
     recompute: bool = False          # per-layer activation recomputation (memory for compute)
     head_chunk: int = 4096           # K5: LM head + CE row chunk (tokens); 0 = whole micro-batch
     sequence_parallel: bool = False  # Megatron SP on top of TP (token-row-sharded norms / residual)
+    # context parallelism (parallel/context.py): the DP group becomes ONE context-parallel group --
+    # its ranks share the same sequences, each holding 1/dp of every sequence's tokens
+    context_parallel: bool = False
 
 
 class Trainer:
@@ -65,6 +68,9 @@ class Trainer:
         self.model.recompute = tcfg.recompute
         self.model.head_chunk = tcfg.head_chunk
         self.model.sequence_parallel = tcfg.sequence_parallel
+        self.cp = self.st.dp if tcfg.context_parallel else 1
+        if self.cp > 1:
+            self.model.set_context_parallel(self.st.dp_group, self.st.dp, self.st.dp_rank)
         self.model.allocate(pad_to=self.st.dp * 64 if tcfg.zero1 else 1)
         self._sync()
         self.init_times = {"params_alloc_init_s": time.time() - t0}
@@ -130,9 +136,16 @@ class Trainer:
     @property
     def tokens_per_step(self) -> int:
         """Tokens processed by THIS rank per step."""
-        return self.tcfg.micro_batch * self.tcfg.seq_len * self.tcfg.grad_accum
+        return self.tcfg.micro_batch * self.tcfg.seq_len * self.tcfg.grad_accum // self.cp
 
     def train_step(self, micro_batches: List[Tuple[torch.Tensor, torch.Tensor]]) -> torch.Tensor:
+        """``micro_batches``: [B, S] token / label pairs.  Under context parallelism every rank of
+        the group passes the SAME full sequences and trains on its own token block of them; the
+        returned loss is then the mean over this rank's tokens."""
+        if self.cp > 1:
+            from ..parallel.context import shard_tokens
+            micro_batches = [(shard_tokens(t, self.cp, self.st.dp_rank), shard_tokens(l, self.cp, self.st.dp_rank))
+                             for t, l in micro_batches]
         n = len(micro_batches)
         ntok = sum(t.numel() for t, _ in micro_batches)
         scale = 1.0 / ntok
