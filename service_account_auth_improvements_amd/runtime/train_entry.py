@@ -43,6 +43,8 @@ def main(argv=None):
     ap.add_argument("--pp", type=int, default=1)
     ap.add_argument("--zero1", action="store_true")
     ap.add_argument("--sp", action="store_true", help="sequence parallelism on top of --tp (Megatron SP)")
+    ap.add_argument("--cp", action="store_true",
+                    help="context parallelism: the data-parallel ranks share each sequence (long context)")
     ap.add_argument("--recompute", action="store_true", help="per-layer activation recomputation")
     ap.add_argument("--grad-reduce", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--head-chunk", type=int, default=4096)
@@ -75,14 +77,16 @@ def main(argv=None):
             tr.step_idx = int(load_checkpoint(a.resume, tr, data=data)["step"])
         return _loop(a, tr, data, st, t_start)
     tcfg = TrainConfig(model=a.model, seq_len=a.seq_len, micro_batch=a.micro_batch, grad_accum=a.grad_accum,
-                       zero1=a.zero1, n_layers=a.layers, sequence_parallel=a.sp, recompute=a.recompute,
+                       zero1=a.zero1, n_layers=a.layers, sequence_parallel=a.sp, context_parallel=a.cp,
+                       recompute=a.recompute,
                        grad_reduce=a.grad_reduce, head_chunk=a.head_chunk)
     if a.pp > 1:
         from ..parallel.pipeline import PipelineTrainer
         tr = PipelineTrainer(tcfg, st)
     else:
         tr = Trainer(tcfg, st)
-    data = SyntheticData(tr.mcfg.vocab_size, a.micro_batch, a.seq_len, st.device, seed=17, rank=st.dp_rank)
+    data = SyntheticData(tr.mcfg.vocab_size, a.micro_batch, a.seq_len, st.device, seed=17,
+                         rank=0 if a.cp else st.dp_rank)     # --cp: the group shares its sequences
     if a.resume:
         # weights, optimizer state, step, RNG and the data stream position: the resumed job
         # continues exactly where it stopped instead of replaying batches it already saw
