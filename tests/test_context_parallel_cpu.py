@@ -50,39 +50,48 @@ def _mcfg(kv):
     return LlamaConfig.preset("tiny").with_(n_heads=2 * kv, n_kv_heads=kv)
 
 
-def _cp_body(rank, world, zero1, n_layers, kv):
+def _cp_body(rank, world, zero1, n_layers, kv, tp=1):
     from service_account_auth_improvements_amd.parallel.state import init_distributed
     from service_account_auth_improvements_amd.runtime.trainer import TrainConfig, Trainer
-    st = init_distributed(device="cpu")
+    st = init_distributed(tp=tp, device="cpu")
     tr = Trainer(TrainConfig(model="tiny", seq_len=64, micro_batch=2, n_layers=n_layers, lr=LR, max_grad_norm=0.05,
                              zero1=zero1, bucket_mb=1, context_parallel=True), st, mcfg=_mcfg(kv), full_init=True)
-    assert tr.cp == world and tr.model.cp == world
+    assert tr.cp == world // tp and tr.model.cp == world // tp
     losses = []
     for step in range(STEPS):
         losses.append(float(tr.train_step(_batches(tr.mcfg.vocab_size, 1, seed=50 + step))))
     tr.sync_params()
-    return losses, {s.name: tr.model.P(s.name).float().clone() for g in tr.model.groups for s in g.specs}
+    return losses, {s.name: tr.model.P(s.name).float().clone() for g in tr.model.groups for s in g.specs}, st.tp_rank
 
 
-@pytest.mark.parametrize("world,zero1,kv", [(2, False, 2), (2, True, 2), (4, True, 4)],
-                         ids=["cp2", "cp2-zero1", "cp4-zero1"])
-def test_context_parallel_training_matches_single_process(world, zero1, kv):
+@pytest.mark.parametrize("world,zero1,kv,tp", [(2, False, 2, 1), (2, True, 2, 1), (4, True, 4, 1), (4, True, 4, 2)],
+                         ids=["cp2", "cp2-zero1", "cp4-zero1", "cp2xtp2-zero1"])
+def test_context_parallel_training_matches_single_process(world, zero1, kv, tp):
     from service_account_auth_improvements_amd.parallel.state import ParallelState
     from service_account_auth_improvements_amd.runtime.trainer import TrainConfig, Trainer
     n_layers = 2
-    res = run_ranks(_cp_body, world=world, args=(zero1, n_layers, kv), timeout=600)
+    from service_account_auth_improvements_amd.models.llama import Llama
+    res = run_ranks(_cp_body, world=world, args=(zero1, n_layers, kv, tp), timeout=600)
     ref = Trainer(TrainConfig(model="tiny", seq_len=64, micro_batch=2, n_layers=n_layers, lr=LR, max_grad_norm=0.05),
                   ParallelState(), mcfg=_mcfg(kv), full_init=True)
     ref_losses = [float(ref.train_step(_batches(ref.mcfg.vocab_size, 1, seed=50 + step))) for step in range(STEPS)]
+    cp = world // tp
     for step in range(STEPS):
-        got = sum(r[0][step] for r in res) / world        # equal token blocks: mean of means
+        got = sum(r[0][step] for r in res) / world        # equal token blocks: mean of means (TP ranks agree)
         assert abs(got - ref_losses[step]) < 1e-2 * ref_losses[step], (step, got, ref_losses[step])
-    for name, want in ((s.name, ref.model.P(s.name).float()) for g in ref.model.groups for s in g.specs):
-        for losses, params in res:
+    slicers = {}
+    for t in range(tp):
+        slicers[t] = Llama(ref.mcfg, ParallelState(tp=tp, tp_rank=t), device="cpu", seed=1234,
+                           full_init=True)._tp_slicers() if tp > 1 else {}
+    for name, full in ((s.name, ref.model.P(s.name).float()) for g in ref.model.groups for s in g.specs):
+        for losses, params, t in res:
+            want = slicers[t][name][1](full) if name in slicers[t] else full
             diff = (params[name] - want).abs()
             assert diff.max().item() <= 2 * LR * STEPS + 1e-3, (name, diff.max().item())
             assert (diff <= 2e-4 + 1e-2 * want.abs()).float().mean().item() > 0.98, name
-    # replicas of the weights stay identical across the group
+    # replicas of the weights stay identical across the context-parallel group
     for name in res[0][1]:
         for other in res[1:]:
-            assert torch.equal(res[0][1][name], other[1][name]), name
+            if other[2] == res[0][2]:
+                assert torch.equal(res[0][1][name], other[1][name]), name
+    assert cp * tp == world
