@@ -20,6 +20,8 @@ Components (reference flags kept where they exist):
 * ``predictor``             the InferenceService model server (serving/server.py)
 * ``train``                 the PyTorchJob worker entry (runtime/train_entry.py)
 * ``mpi-wait``              the MPIJob launcher for mpirun-style jobs (controlplane/mpi.py)
+* ``nb-server``             notebook server stand-in: read-only Jupyter REST subset + GPU probe
+  under NB_PREFIX (runtime/notebook_server.py)
 * ``cluster``               the single-process local cluster (cluster.py)
 """
 from __future__ import annotations
@@ -77,6 +79,9 @@ def main(argv=None):
         return m(rest)
     if comp == "train":
         from .runtime.train_entry import main as m
+        return m(rest)
+    if comp == "nb-server":
+        from .runtime.notebook_server import main as m
         return m(rest)
     if comp == "cluster":
         from .cluster import main as m

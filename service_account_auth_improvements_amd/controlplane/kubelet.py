@@ -173,6 +173,7 @@ class Kubelet(Controller):
         self.workdir = workdir
         self.log_dir = log_dir
         self.procs: Dict[str, subprocess.Popen] = {}
+        self.uids: Dict[str, str] = {}      # ns/name -> uid holding devices (released when the pod goes)
         self.logs: Dict[str, str] = {}
         self._lock = threading.Lock()
         self._register_node(n_gpus)
@@ -209,19 +210,21 @@ class Kubelet(Controller):
         c = self.client
         pod = c.get_or_none("v1", "Pod", req.name, req.namespace)
         key = f"{req.namespace}/{req.name}"
-        if pod is None:
+        if pod is None or pod["metadata"].get("deletionTimestamp"):
+            # the pod is gone (or going): stop its container and give its GPUs back
             with self._lock:
                 p = self.procs.pop(key, None)
             if p and p.poll() is None:
                 p.terminate()
+            uid = self.uids.pop(key, None) or (pod or {}).get("metadata", {}).get("uid")
+            if uid:
+                self.dp.release(uid)
             return Result()
         uid = pod["metadata"]["uid"]
-        if pod["metadata"].get("deletionTimestamp"):
-            self.dp.release(uid)
-            return Result()
         phase = (pod.get("status") or {}).get("phase")
         if phase in ("Succeeded", "Failed"):
             self.dp.release(uid)
+            self.uids.pop(key, None)
             return Result()
         bound = pod["spec"].get("nodeName")
         if not bound:
@@ -234,6 +237,8 @@ class Kubelet(Controller):
         if phase in (None, "", "Pending"):
             ngpu = pod_gpu_request(pod)
             ids = self.dp.allocate(uid, ngpu) if ngpu else []
+            if ngpu and ids is not None:
+                self.uids[key] = uid
             if ids is None:
                 st = self._status("Pending", False, {"waiting": {"reason": "Unschedulable"}},
                                   "Unschedulable", f"0/1 nodes are available: insufficient {GPU_RESOURCE}", pod)
@@ -294,8 +299,11 @@ class Kubelet(Controller):
             path = os.path.join(self.log_dir, key.replace("/", "_") + ".log")
             self.logs[key] = path
             out = open(path, "w")
-        p = subprocess.Popen(cmd, env=env, cwd=ctr.get("workingDir") or self.workdir, stdout=out,
-                             stderr=subprocess.STDOUT)
+        # the image's filesystem is not on this host: a workingDir that only exists inside the
+        # image (e.g. the notebook controller's /home/jovyan) falls back to the kubelet's workdir
+        wd = ctr.get("workingDir")
+        cwd = wd if wd and os.path.isdir(wd) else self.workdir
+        p = subprocess.Popen(cmd, env=env, cwd=cwd, stdout=out, stderr=subprocess.STDOUT)
         with self._lock:
             self.procs[key] = p
 
