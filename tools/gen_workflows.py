@@ -28,8 +28,10 @@ IMAGE = "rocm/pytorch:rocm7.0_ubuntu22.04_py3.10_pytorch_release_2.10.0"
 
 # id -> (workflow title, source paths, unit-test selection, image, tools/ci_integration.py component)
 COMPONENTS = {
-    "notebook_controller": ("Notebook Controller", [f"{PKG}/controlplane/notebook.py"],
-                            "tests/test_notebook_controller.py", "platform", "notebook-controller"),
+    "notebook_controller": ("Notebook Controller", [f"{PKG}/controlplane/notebook.py",
+                                                    f"{PKG}/runtime/notebook_server.py"],
+                            "tests/test_notebook_controller.py tests/test_notebook_server.py", "platform",
+                            "notebook-controller"),
     "profile_controller": ("Profile Controller + KFAM",
                            [f"{PKG}/controlplane/profile.py", f"{PKG}/controlplane/kfam.py",
                             f"{PKG}/controlplane/cloud_iam.py", f"{PKG}/controlplane/monitoring.py"],
