@@ -269,6 +269,25 @@ class Llama:
         else all rows (all-reduce; a no-op at tp 1)."""
         return tp_reduce_scatter_rows(x, self.st) if self._sp else tp_all_reduce(x, self.st)
 
+    def _reduce_out_async(self, x):
+        """:meth:`_reduce_out` launched asynchronously on the TP communicator's stream; returns
+        (result, handle) -- :meth:`_finish` makes the compute stream wait for it.  The backward
+        overlaps its input-gradient reductions with the weight-gradient GEMMs that do not need
+        them (at TP=8 over xGMI each all-reduce costs several times its producing GEMM)."""
+        if self.tp == 1:
+            return x, None
+        if self._sp:
+            out = torch.empty((x.shape[0] // self.tp,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+            return out, dist.reduce_scatter_tensor(out, x.contiguous(), group=self.st.tp_group, async_op=True)
+        return x, dist.all_reduce(x, group=self.st.tp_group, async_op=True)
+
+    @staticmethod
+    def _finish(pending):
+        y, work = pending
+        if work is not None:
+            work.wait()
+        return y
+
     def _norm_bwd(self, dy, h, rstd, name: str, accumulate: bool, dres=None):
         """K1 backward.  Under SP each rank sees 1/tp of the rows, so the norm weight gradient
         is a partial sum: it goes to a scratch row and is all-reduced (fp32) over the TP group
@@ -340,12 +359,24 @@ class Llama:
         dgu = ops.swiglu_bwd(c.gu, gs)
         del gs
         c.gu = None
-        dmm = self._reduce_out(self._mm_dx(dgu, Wgu))
-        dh2 = self._norm_bwd(dmm, c.h2, c.rstd2, f"l{i}.norm2", accumulate, dres=g)
-        del dmm
-        dh2f = self._gather(dh2)
-        self._mm_into2((self.G(f"l{i}.wgu"), dgu.t(), self._gather(c.m)), (self.G(f"l{i}.wo"), dh2f.t(), c.o_tok),
-                       accumulate)
+        if self.tp == 1:
+            dmm = self._mm_dx(dgu, Wgu)
+            dh2 = self._norm_bwd(dmm, c.h2, c.rstd2, f"l{i}.norm2", accumulate, dres=g)
+            del dmm
+            dh2f = dh2
+            self._mm_into2((self.G(f"l{i}.wgu"), dgu.t(), c.m), (self.G(f"l{i}.wo"), dh2f.t(), c.o_tok), accumulate)
+        else:
+            # TP: the dmm reduction runs while the wgu weight gradient (which does not need it)
+            # is computed; SP gathers m before the reduce-scatter goes out on the communicator
+            mf = self._gather(c.m)
+            pend = self._reduce_out_async(self._mm_dx(dgu, Wgu))
+            self._mm_into(self.G(f"l{i}.wgu"), dgu.t(), mf, accumulate)
+            del mf
+            dmm = self._finish(pend)
+            dh2 = self._norm_bwd(dmm, c.h2, c.rstd2, f"l{i}.norm2", accumulate, dres=g)
+            del dmm, pend
+            dh2f = self._gather(dh2)
+            self._mm_into(self.G(f"l{i}.wo"), dh2f.t(), c.o_tok, accumulate)
         del dgu
         # attention (context parallel: the same all-to-alls as forward, in reverse roles)
         D, cp = cfg.head_dim, self.cp
@@ -359,11 +390,12 @@ class Llama:
         ops.rope_(dqkv, hq + hkv, D, self.cos, self.sin, seq_len=Sa, inverse=True)
         if cp > 1:
             dqkv = cpx.to_tokens(dqkv, B, S, [hq * D, hkv * D, hkv * D], cp, self.cp_group)
-        da = self._reduce_out(self._mm_dx(dqkv, Wqkv))
-        self._mm_into2((self.G(f"l{i}.wd"), gf.t(), c.s), (self.G(f"l{i}.wqkv"), dqkv.t(), self._gather(c.a)),
-                       accumulate)
+        af = self._gather(c.a)
+        pend = self._reduce_out_async(self._mm_dx(dqkv, Wqkv))     # overlaps the two dW GEMMs below
+        self._mm_into2((self.G(f"l{i}.wd"), gf.t(), c.s), (self.G(f"l{i}.wqkv"), dqkv.t(), af), accumulate)
+        da = self._finish(pend)
         c.s = None
-        del dqkv, gf
+        del dqkv, gf, af, pend
         dh1 = self._norm_bwd(da, c.h1, c.rstd1, f"l{i}.norm1", accumulate, dres=dh2)
         self._ready(self.mats, f"l{i}.wqkv")
         return dh1
