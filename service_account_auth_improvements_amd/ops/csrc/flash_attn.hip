@@ -598,7 +598,11 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
     stage_rows(qkv + (rowB + q0) * ld + (long)h * D, ld, smem + OFF_Q + buf * 8192, QT, w, 4, l);
     stage_rows(dout + (rowB + q0) * lddo + (long)h * D, lddo, smem + OFF_DO + buf * 8192, QT, w, 4, l);
     if (w == 0) {
-      const float* src = (l < 32 ? lse : delta) + ((long)b * Hq + h) * S + q0 + (l & 31);
+      // lse/delta select from an opaque lane id: hoisted, the per-lane 64-bit pointer lived
+      // across the loop and was the kernel's only scratch spill
+      int lo = l;
+      asm volatile("" : "+v"(lo));
+      const float* src = (lo < 32 ? lse : delta) + ((long)b * Hq + h) * S + q0 + (lo & 31);
       glds4(src, smem + OFF_LD + buf * 256);
     }
   };
