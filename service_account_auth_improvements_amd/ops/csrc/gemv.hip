@@ -20,7 +20,18 @@
 //  * NORM prologue (decode layer norms fused in, as in skinny_gemm.hip): each workgroup
 //    forms h = bf16(x + res) and its sum of squares, stages y = bf16(h * rstd * w_norm) in
 //    LDS; workgroup 0 stores h.  The first W chunks are requested before the prologue.
+//  * K split inside the workgroup (KS = 4) for narrow, deep projections (wd: N = 4096,
+//    K = 14336): with one wave per R rows it launches 256 workgroups, one wave per SIMD, and
+//    each wave walks its K/512 chunk slots in a serial chain of 7 load -> wait -> dot rounds.
+//    With KS = 4 the four waves of a workgroup share its R rows and take a quarter of K each
+//    (4x the waves, a quarter of the chain); the partial sums meet in LDS.  Measured
+//    (tools/kbench/gemv_bench, profiles/serve_gemv_ksplit.txt): wd 24.1 -> 19.5 us at M = 1
+//    (6.0 TB/s), 29.2 -> 24.9 us at M = 4; at K = 4096 it is null at M = 1 and 10-15 % slower
+//    at M = 4, and with the norm prologue (every workgroup normalises X itself) 1.3-1.6x
+//    slower.  Hence: no prologue, K >= 8192 and < 4 workgroups per CU unsplit.
+//    KFAMD_GEMV_KSPLIT=1 / 4 forces it off / on.
 #include "common.h"
+#include <cstdlib>
 
 using namespace kf;
 
@@ -60,7 +71,7 @@ struct GvRope {
   int hq, hkv, lmax;
 };
 
-template <int M, int R, bool SWIGLU, bool NORM, bool ROPE = false>
+template <int M, int R, bool SWIGLU, bool NORM, bool ROPE = false, int KS = 1>
 __global__ __launch_bounds__(64 * GV_WAVES) void gemv_kernel(const bf16_t* __restrict__ x, long ldx,
                                                             const bf16_t* __restrict__ w, int N, int K,
                                                             bf16_t* __restrict__ y, long ldy, int up_off,
@@ -69,12 +80,17 @@ __global__ __launch_bounds__(64 * GV_WAVES) void gemv_kernel(const bf16_t* __res
   extern __shared__ __attribute__((aligned(16))) bf16_t xs[];   // NORM: M x K normalised rows
   __shared__ float ssq[GV_WAVES][M];
   constexpr int NR = SWIGLU ? 2 * R : R;
+  static_assert(KS == 1 || KS == GV_WAVES, "K split: 1 or all waves of the workgroup");
+  __shared__ float red[KS > 1 ? GV_WAVES : 1][NR][M];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int gw = blockIdx.x * GV_WAVES + wave;
+  const int gw = KS > 1 ? (int)blockIdx.x : (int)blockIdx.x * GV_WAVES + wave;   // owner of R rows
   // ROPE: wave gw owns rotation pairs (p, p + 64) and (p + 1, p + 65) of head gw / 32
   const int r0 = ROPE ? (gw >> 5) * 128 + (gw & 31) * 2 : gw * R;
   const int nch = K >> 3;                       // 16-byte chunks per row
   const int J = (nch + 63) >> 6;                // chunk slots per lane
+  const int Jw = (J + KS - 1) / KS;             // this wave's slots: [jb, je)
+  const int jb = KS > 1 ? wave * Jw : 0;
+  const int je = KS > 1 ? min(J, jb + Jw) : J;
 
   auto row_of = [&](int i) -> int {
     if constexpr (ROPE) return r0 + (i & 1) + (i >> 1) * 64;
@@ -93,12 +109,12 @@ __global__ __launch_bounds__(64 * GV_WAVES) void gemv_kernel(const bf16_t* __res
 #pragma unroll
       for (int u = 0; u < GV_U; ++u) {
         const int c = lane + 64 * (j0 + u);
-        wv[i][u] = (row_ok(i) && j0 + u < J && c < nch)
+        wv[i][u] = (row_ok(i) && j0 + u < je && c < nch)
                        ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(row_ptr(i) + 512 * (j0 + u)))
                        : u32x4{0, 0, 0, 0};
       }
   };
-  load_w(0);
+  load_w(jb);
 
   if constexpr (NORM) {
     float ss[M];
@@ -158,12 +174,12 @@ __global__ __launch_bounds__(64 * GV_WAVES) void gemv_kernel(const bf16_t* __res
 #pragma unroll
     for (int m = 0; m < M; ++m) acc[i][m] = 0.f;
 
-  for (int j0 = 0; j0 < J; j0 += GV_U) {
-    if (j0 > 0) load_w(j0);
+  for (int j0 = jb; j0 < je; j0 += GV_U) {
+    if (j0 > jb) load_w(j0);
 #pragma unroll
     for (int u = 0; u < GV_U; ++u) {
       const int c = lane + 64 * (j0 + u);
-      if (j0 + u >= J || c >= nch) continue;
+      if (j0 + u >= je || c >= nch) continue;
 #pragma unroll
       for (int m = 0; m < M; ++m) {
         const u32x4 xv = NORM ? *reinterpret_cast<const u32x4*>(xs + (long)m * K + 8 * c)
@@ -185,6 +201,21 @@ __global__ __launch_bounds__(64 * GV_WAVES) void gemv_kernel(const bf16_t* __res
   for (int i = 0; i < NR; ++i)
 #pragma unroll
     for (int m = 0; m < M; ++m) acc[i][m] = wave_sum(acc[i][m]);
+  if constexpr (KS > 1) {
+    // the workgroup's four K quarters meet in LDS; wave 0 runs the epilogue
+    if (lane == 0) {
+#pragma unroll
+      for (int i = 0; i < NR; ++i)
+#pragma unroll
+        for (int m = 0; m < M; ++m) red[wave][i][m] = acc[i][m];
+    }
+    __syncthreads();
+    if (wave != 0) return;
+#pragma unroll
+    for (int i = 0; i < NR; ++i)
+#pragma unroll
+      for (int m = 0; m < M; ++m) acc[i][m] = red[0][i][m] + red[1][i][m] + red[2][i][m] + red[3][i][m];
+  }
   if (lane < R * M) {
     const int i = lane / M, m = lane % M;
     float g = 0.f, u = 0.f;
@@ -222,14 +253,30 @@ __global__ __launch_bounds__(64 * GV_WAVES) void gemv_kernel(const bf16_t* __res
   }
 }
 
+// K split for deep K without the norm prologue when the unsplit grid leaves the 256 CUs
+// with < 4 workgroups each; KFAMD_GEMV_KSPLIT=1 / 4 forces it off / on (A/B)
+bool use_ksplit(int blocks_unsplit, int K, bool norm) {
+  static const int force = [] {
+    const char* e = getenv("KFAMD_GEMV_KSPLIT");
+    return e ? atoi(e) : 0;
+  }();
+  if (force == 1) return false;
+  if (force == GV_WAVES) return true;
+  return !norm && K >= 8192 && blocks_unsplit < 4 * 256;
+}
+
 template <int M, bool SWIGLU, bool NORM>
 int gv_launch(const bf16_t* x, long ldx, const bf16_t* w, int N, int K, bf16_t* y, long ldy, int up_off,
               GvNorm na, hipStream_t st) {
   constexpr int R = SWIGLU ? (GV_R_CFG > 1 ? GV_R_CFG / 2 : 1) : GV_R_CFG;
   const int blocks = (N + R * GV_WAVES - 1) / (R * GV_WAVES);
   const size_t dyn = NORM ? (size_t)M * K * 2 : 0;
-  hipLaunchKernelGGL((gemv_kernel<M, R, SWIGLU, NORM>), dim3(blocks), dim3(64 * GV_WAVES), dyn, st, x, ldx, w, N,
-                     K, y, ldy, up_off, na, GvRope{});
+  if (use_ksplit(blocks, K, NORM))
+    hipLaunchKernelGGL((gemv_kernel<M, R, SWIGLU, NORM, false, GV_WAVES>), dim3((N + R - 1) / R),
+                       dim3(64 * GV_WAVES), dyn, st, x, ldx, w, N, K, y, ldy, up_off, na, GvRope{});
+  else
+    hipLaunchKernelGGL((gemv_kernel<M, R, SWIGLU, NORM>), dim3(blocks), dim3(64 * GV_WAVES), dyn, st, x, ldx, w,
+                       N, K, y, ldy, up_off, na, GvRope{});
   KF_CHECK_LAUNCH();
   return 0;
 }
@@ -250,8 +297,12 @@ template <int M>
 int gv_rope_launch(const bf16_t* x, long ldx, const bf16_t* w, int N, int K, bf16_t* y, long ldy, GvNorm na,
                    GvRope ra, hipStream_t st) {
   const int blocks = N / (4 * GV_WAVES);
-  hipLaunchKernelGGL((gemv_kernel<M, 4, false, true, true>), dim3(blocks), dim3(64 * GV_WAVES), (size_t)M * K * 2,
-                     st, x, ldx, w, N, K, y, ldy, 0, na, ra);
+  if (use_ksplit(blocks, K, true))
+    hipLaunchKernelGGL((gemv_kernel<M, 4, false, true, true, GV_WAVES>), dim3(N / 4), dim3(64 * GV_WAVES),
+                       (size_t)M * K * 2, st, x, ldx, w, N, K, y, ldy, 0, na, ra);
+  else
+    hipLaunchKernelGGL((gemv_kernel<M, 4, false, true, true>), dim3(blocks), dim3(64 * GV_WAVES), (size_t)M * K * 2,
+                       st, x, ldx, w, N, K, y, ldy, 0, na, ra);
   KF_CHECK_LAUNCH();
   return 0;
 }

@@ -109,9 +109,11 @@ def test_skinny_gemm(M, N, K, swiglu):
 
 
 @pytest.mark.parametrize("M,N,K,swiglu", [(1, 1000, 1792, False), (2, 4104, 520, True), (3, 16032, 4096, False),
-                                         (4, 4096, 14336, False), (1, 128256, 4096, False)])
+                                         (4, 4096, 14336, False), (1, 4096, 14336, False), (2, 1000, 9000, False),
+                                         (1, 2052, 8192, True), (1, 128256, 4096, False)])
 def test_gemv_odd_shapes(M, N, K, swiglu):
-    """The VALU decode GEMV (M <= 4): TP-shard widths (K = 1792), ragged N, LM-head size."""
+    """The VALU decode GEMV (M <= 4): TP-shard widths (K = 1792), ragged N, LM-head size; the
+    in-workgroup K split (K >= 8192 on narrow N: wd, ragged K quarters, SwiGLU rows)."""
     from service_account_auth_improvements_amd import ops
     g = torch.Generator(device="cpu").manual_seed(M * 13 + N + K)
     x = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
