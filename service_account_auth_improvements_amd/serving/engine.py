@@ -27,6 +27,7 @@ MI355X-first design:
 from __future__ import annotations
 
 import math
+import os
 import queue
 import threading
 import time
@@ -42,9 +43,30 @@ from ..ops.attention import attention_fwd, decode_attention, kv_fill_, rope_appe
 from ..parallel.state import ParallelState, tp_all_reduce
 
 BUCKETS = (1, 2, 4, 8, 16, 32, 64, 128, 256)
-SKINNY_MAX_ROWS = 16          # decode batches up to this use the weight-streaming skinny GEMM
+# decode batches up to this use the weight-streaming skinny GEMM (KFAMD_SKINNY_MAX_ROWS: A/B, <= 64)
+SKINNY_MAX_ROWS = min(64, int(os.environ.get("KFAMD_SKINNY_MAX_ROWS", "16")))
 SKINNY_MAX_N = 32768          # beyond this (LM head) hipBLASLt streams faster than the MFMA skinny kernel
 GEMV_MAX_ROWS = 4             # ... but not than the VALU GEMV (ops/csrc/gemv.hip) the 1-4 row case takes
+# hipBLASLt/rocBLAS solutions for the decode GEMM shapes above SKINNY_MAX_ROWS where the library
+# heuristic picks a poor kernel (tools/tune_decode_gemm.py; only the shapes that measured >= 5 %
+# faster HBM-cold are kept, profiles/serve_large_batch.md).  Loaded into PyTorch TunableOp with
+# tuning off; KFAMD_DECODE_TUNED=0 disables it, =<file> uses another results file.
+TUNED_DECODE_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned", "decode_gemm_gfx950.csv")
+
+
+def _load_tuned_decode_gemms(dev, cfg, tp: int) -> bool:
+    path = os.environ.get("KFAMD_DECODE_TUNED", TUNED_DECODE_FILE)
+    if dev.type != "cuda" or path == "0" or not os.path.exists(path):
+        return False
+    if path == TUNED_DECODE_FILE and (cfg.hidden, cfg.ffn, cfg.vocab_size, tp) != (4096, 14336, 128256, 1):
+        return False                  # the shipped file holds Llama-3-8B TP=1 shapes only
+    if torch.cuda.get_device_properties(dev).gcnArchName.split(":")[0] != "gfx950":
+        return False
+    import torch.cuda.tunable as tn
+    tn.enable(True)
+    tn.tuning_enable(False)           # never tune inside a serving process
+    tn.read_file(path)
+    return True
 
 
 class Engine:
@@ -62,6 +84,7 @@ class Engine:
         self.kc = torch.zeros(shape, dtype=torch.bfloat16, device=self.dev)
         self.vc = torch.zeros(shape, dtype=torch.bfloat16, device=self.dev)
         self.use_graphs = (self.dev.type == "cuda") if use_graphs is None else use_graphs
+        self.tuned_gemms = _load_tuned_decode_gemms(self.dev, cfg, model.tp)
         # TP > 1 on GPUs: the decode step's small all-reduces go one-shot over peer-mapped
         # IPC buffers (parallel/custom_ar.py, C7) instead of an RCCL ring
         self.car = None
