@@ -47,6 +47,8 @@ BUCKETS = (1, 2, 4, 8, 16, 32, 64, 128, 256)
 SKINNY_MAX_ROWS = min(64, int(os.environ.get("KFAMD_SKINNY_MAX_ROWS", "16")))
 SKINNY_MAX_N = 32768          # beyond this (LM head) hipBLASLt streams faster than the MFMA skinny kernel
 GEMV_MAX_ROWS = 4             # ... but not than the VALU GEMV (ops/csrc/gemv.hip) the 1-4 row case takes
+# prompts admitted in one scheduler iteration are prefilled together up to this many tokens
+PREFILL_MAX_TOKENS = int(os.environ.get("KFAMD_PREFILL_MAX_TOKENS", "16384"))
 # hipBLASLt/rocBLAS solutions for the decode GEMM shapes above SKINNY_MAX_ROWS where the library
 # heuristic picks a poor kernel (tools/tune_decode_gemm.py; only the shapes that measured >= 5 %
 # faster HBM-cold are kept, profiles/serve_large_batch.md).  Loaded into PyTorch TunableOp with
@@ -139,6 +141,39 @@ class Engine:
         y, _, _ = ops.rmsnorm_fwd(r[S - 1:S].contiguous(), m.P("final_norm"), cfg.norm_eps,
                                   residual=d[S - 1:S].contiguous())
         return self._logits_full(y)[0]
+
+    @torch.no_grad()
+    def prefill_batch(self, slots: List[int], prompts: List[List[int]]) -> torch.Tensor:
+        """Several prompts in ONE pass: each is padded to the longest (rounded to the flash
+        kernel's 128-row tiles) and the batch runs as B sequences of that length, so every
+        projection is one GEMM over all B * Sp rows instead of B GEMMs over Sp rows (causal
+        attention: the pad rows after a prompt never reach its real rows).  Fills every slot's
+        KV; returns the last-position logits [B, V].  == ``prefill`` per prompt up to the
+        GEMMs' row-count-dependent rounding."""
+        m, cfg = self.m, self.cfg
+        n = len(prompts)
+        assert n == len(slots) and n > 0
+        lens = [len(t) for t in prompts]
+        assert 0 < min(lens) and max(lens) <= self.max_len
+        Sp = max(lens) if self.dev.type != "cuda" else ((max(lens) + 127) // 128) * 128
+        tok = torch.zeros(n, Sp, dtype=torch.long)
+        for b, t in enumerate(prompts):
+            tok[b, :len(t)] = torch.tensor(t, dtype=torch.long)
+        r = self._embed(tok.reshape(-1).to(self.dev))
+        d = None
+        for li, i in enumerate(m.layers):
+            a, h1, _ = ops.rmsnorm_fwd(r, m.P(f"l{i}.norm1"), cfg.norm_eps, residual=d)
+            qkv = torch.mm(a, m.P(f"l{i}.wqkv").t())
+            ops.rope_(qkv, m.hq + m.hkv, cfg.head_dim, m.cos, m.sin, seq_len=Sp)   # position = row % Sp
+            o, _ = attention_fwd(qkv, n, Sp, m.hq, m.hkv, cfg.head_dim)
+            for b in range(n):
+                kv_fill_(qkv[b * Sp:(b + 1) * Sp], lens[b], m.hq, slots[b], self.kc[li], self.vc[li])
+            da = tp_all_reduce(torch.mm(o, m.P(f"l{i}.wo").t()), m.st)
+            r, d = self._mlp(i, h1, da)
+        last = torch.tensor([b * Sp + lens[b] - 1 for b in range(n)], device=self.dev)
+        y, _, _ = ops.rmsnorm_fwd(r.index_select(0, last), m.P("final_norm"), cfg.norm_eps,
+                                  residual=d.index_select(0, last))
+        return self._logits_full(y)
 
     # ------------------------------------------------------------------ decode
     def _tp_ar(self, x):
@@ -314,23 +349,36 @@ class Scheduler:
         del self.active[slot]
         self.free.append(slot)
 
+    def _admit(self, batch: List[tuple]):
+        """Prefill newly admitted (slot, request) pairs together (Engine.prefill_batch) and
+        sample their first tokens."""
+        logits = self.e.prefill_batch([s for s, _ in batch], [r.prompt for _, r in batch])
+        for j, (slot, req) in enumerate(batch):
+            tok = int(sample(logits[j:j + 1], req.temperature, req.top_p)[0])
+            req.output.append(tok)
+            req.t_first = time.time()
+            self.active[slot] = req
+            if len(req.output) >= req.max_new_tokens or (req.stop and tok in req.stop):
+                self._finish(slot, req)
+
     def step(self) -> bool:
         """One scheduling iteration; returns False when idle."""
         admitted = False
-        while self.free and len(self.active) < self.max_batch:
+        batch: List[tuple] = []
+        ntok = 0
+        while self.free and len(self.active) + len(batch) < self.max_batch:
             try:
                 req = self.q.get_nowait()
             except queue.Empty:
                 break
-            slot = self.free.pop()
-            logits = self.e.prefill(slot, req.prompt)
-            tok = int(sample(logits[None], req.temperature, req.top_p)[0])
-            req.output.append(tok)
-            req.t_first = time.time()
-            self.active[slot] = req
+            if batch and ntok + len(req.prompt) > PREFILL_MAX_TOKENS:
+                self._admit(batch)
+                batch, ntok = [], 0
+            batch.append((self.free.pop(), req))
+            ntok += len(req.prompt)
             admitted = True
-            if len(req.output) >= req.max_new_tokens or (req.stop and tok in req.stop):
-                self._finish(slot, req)
+        if batch:
+            self._admit(batch)
         if not self.active:
             return admitted
         slots = sorted(self.active)

@@ -3,9 +3,9 @@
 The predictor pod runs ``kfamd-launch --nproc-per-node N --isolate-devices -- python -m
 ...serving.server --tp N`` (controlplane/inferenceservice.py), i.e. one process per GPU,
 each holding a 1/N Megatron shard of the model (serving/engine.py).  Only rank 0 serves HTTP
-and runs the :class:`~.engine.Scheduler`; every engine call it makes (prefill of one prompt,
-one joint decode step) is first broadcast to the follower ranks as a tiny command over a
-gloo control group, so all ranks issue the same sequence of collectives (RCCL for prefill /
+and runs the :class:`~.engine.Scheduler`; every engine call it makes (prefill of one prompt or
+of the prompts admitted together, one joint decode step) is first broadcast to the follower
+ranks as a tiny command over a gloo control group, so all ranks issue the same sequence of collectives (RCCL for prefill /
 logits, the one-shot IPC all-reduce for the decode step's per-layer reductions).  Sampling
 happens on rank 0 only: the next step's tokens arrive with its command.
 
@@ -38,6 +38,10 @@ class TPLeaderEngine:
         self._send(("prefill", int(slot), [int(t) for t in tokens]))
         return self.e.prefill(slot, tokens)
 
+    def prefill_batch(self, slots: List[int], prompts: List[List[int]]):
+        self._send(("prefill_batch", [int(s) for s in slots], [[int(t) for t in p] for p in prompts]))
+        return self.e.prefill_batch(slots, prompts)
+
     def decode(self, tokens: List[int], slots: List[int], pos: List[int]):
         self._send(("decode", [int(t) for t in tokens], [int(s) for s in slots], [int(p) for p in pos]))
         return self.e.decode(tokens, slots, pos)
@@ -58,6 +62,8 @@ def follower_loop(engine, group=None, max_commands: Optional[int] = None) -> int
             break
         if cmd[0] == "prefill":
             engine.prefill(cmd[1], cmd[2])
+        elif cmd[0] == "prefill_batch":
+            engine.prefill_batch(cmd[1], cmd[2])
         elif cmd[0] == "decode":
             engine.decode(cmd[1], cmd[2], cmd[3])
         else:

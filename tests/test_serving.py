@@ -37,6 +37,24 @@ def test_prefill_decode_match_full_forward(eng):
         assert torch.allclose(out, full[len(prompt) + j], atol=1e-2)
 
 
+def test_prefill_batch_matches_per_prompt_prefill(eng):
+    """Batched prefill of prompts of different lengths == one prefill per prompt: logits and
+    every slot's KV cache (positions below each prompt's length)."""
+    prompts = [[5, 17, 99, 3, 42, 7], [9, 8], [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11]]
+    slots = [0, 3, 1]
+    one = [eng.prefill(s, p).float() for s, p in zip(slots, prompts)]
+    kc1, vc1 = eng.kc.clone(), eng.vc.clone()
+    eng.kc.zero_()
+    eng.vc.zero_()
+    lg = eng.prefill_batch(slots, prompts).float()
+    assert lg.shape == (3, eng.cfg.vocab_size)
+    for j, (s, p) in enumerate(zip(slots, prompts)):
+        assert torch.allclose(lg[j], one[j], atol=1e-4), j
+        n = len(p)
+        assert torch.allclose(eng.kc[:, s, :, :n].float(), kc1[:, s, :, :n].float(), atol=1e-3)
+        assert torch.allclose(eng.vc[:, s, :, :n].float(), vc1[:, s, :, :n].float(), atol=1e-3)
+
+
 def test_continuous_batching_is_order_independent(eng):
     s = Scheduler(eng, max_batch=3)
     a = s.submit(Request(prompt=[1, 2, 3, 4], max_new_tokens=6))
@@ -202,9 +220,9 @@ def test_tp_predictor_leader_drives_followers():
 
     res = run_ranks(_tp_predictor_body, world=2, timeout=300)
     logits, outs = res[0]
-    # follower replayed: 1 prefill + 2 decodes, then the scheduler's 2 prefills (first tokens)
-    # and 3 joint decode steps (tokens 2..4 of both requests)
-    assert res[1] == 3 + 2 + 3
+    # follower replayed: 1 prefill + 2 decodes, then the scheduler's ONE batched prefill of
+    # both admitted prompts (first tokens) and 3 joint decode steps (tokens 2..4 of both)
+    assert res[1] == 3 + 1 + 3
     ref = build_engine("tiny", device="cpu", n_slots=4, max_len=128, full_init=True)
     exp = [ref.prefill(0, list(range(3, 40)))]
     for j, t in enumerate((5, 6)):

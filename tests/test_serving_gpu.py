@@ -108,6 +108,25 @@ def test_skinny_gemm(M, N, K, swiglu):
     assert torch.allclose(ops.skinny_gemm(xs, w, swiglu).float(), ops.skinny_gemm(xs.contiguous(), w, swiglu).float())
 
 
+def test_engine_prefill_batch_matches_per_prompt():
+    """Batched prefill on the GPU (flash attention over B padded sequences, GEMMs over all rows)
+    == per-prompt prefill: last-position logits and the KV rows below each prompt's length."""
+    from service_account_auth_improvements_amd.serving.engine import build_engine
+    e = build_engine("small", device=DEV, n_slots=6, max_len=512, n_layers=2)
+    prompts = [list(range(3, 3 + 200)), list(range(7, 7 + 33)), list(range(1, 1 + 130))]
+    slots = [4, 0, 2]
+    one = [e.prefill(s, p).float() for s, p in zip(slots, prompts)]
+    kc1, vc1 = e.kc.clone(), e.vc.clone()
+    e.kc.zero_()
+    e.vc.zero_()
+    lg = e.prefill_batch(slots, prompts).float()
+    for j, (s, p) in enumerate(zip(slots, prompts)):
+        assert (lg[j] - one[j]).abs().max().item() < 5e-2, j
+        n = len(p)
+        assert (e.kc[:, s, :, :n].float() - kc1[:, s, :, :n].float()).abs().max().item() < 5e-2
+        assert (e.vc[:, s, :, :n].float() - vc1[:, s, :, :n].float()).abs().max().item() < 5e-2
+
+
 @pytest.mark.parametrize("M,N,K,swiglu", [(1, 1000, 1792, False), (2, 4104, 520, True), (3, 16032, 4096, False),
                                          (4, 4096, 14336, False), (1, 4096, 14336, False), (2, 1000, 9000, False),
                                          (1, 2052, 8192, True), (1, 128256, 4096, False)])

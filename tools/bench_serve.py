@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--batches", default="1,8,32,64")
     ap.add_argument("--steps", type=int, default=32)
     ap.add_argument("--max-len", type=int, default=2048)
+    ap.add_argument("--prefill-batch", type=int, default=16, help="prompts per batched prefill pass")
     a = ap.parse_args()
     batches = [int(x) for x in a.batches.split(",")]
     nb = max(batches)
@@ -44,6 +45,19 @@ def main():
     print(json.dumps({"bench": "prefill", "model": a.model, "prompt_len": a.ctx, "sequences": nb,
                       "tokens_per_s": round(nb * a.ctx / pf, 1), "ms_per_seq": round(1e3 * pf / nb, 2),
                       "init_s": round(init_s, 1)}), flush=True)
+    # the scheduler's path: prompts admitted together are prefilled in one pass
+    pb = max(1, min(nb, a.prefill_batch))
+    e.prefill_batch(list(range(pb)), [prompt] * pb)
+    torch.cuda.synchronize()
+    t0 = time.time()
+    for s0 in range(0, nb - pb + 1, pb):
+        e.prefill_batch(list(range(s0, s0 + pb)), [prompt] * pb)
+    torch.cuda.synchronize()
+    pf = time.time() - t0
+    done = (nb // pb) * pb
+    print(json.dumps({"bench": "prefill_batch", "model": a.model, "prompt_len": a.ctx, "sequences": done,
+                      "batch": pb, "tokens_per_s": round(done * a.ctx / pf, 1),
+                      "ms_per_seq": round(1e3 * pf / done, 2)}), flush=True)
     for B in batches:
         toks, slots = [1] * B, list(range(B))
         pos = [a.ctx] * B
