@@ -49,6 +49,7 @@ SKINNY_MAX_N = 32768          # beyond this (LM head) hipBLASLt streams faster t
 GEMV_MAX_ROWS = 4             # ... but not than the VALU GEMV (ops/csrc/gemv.hip) the 1-4 row case takes
 # prompts admitted in one scheduler iteration are prefilled together up to this many tokens
 PREFILL_MAX_TOKENS = int(os.environ.get("KFAMD_PREFILL_MAX_TOKENS", "16384"))
+PREFILL_PAD_RATIO = 1.25      # ... in length groups padded to at most 1.25x
 # hipBLASLt/rocBLAS solutions for the decode GEMM shapes above SKINNY_MAX_ROWS where the library
 # heuristic picks a poor kernel (tools/tune_decode_gemm.py; only the shapes that measured >= 5 %
 # faster HBM-cold are kept, profiles/serve_large_batch.md).  Loaded into PyTorch TunableOp with
@@ -350,8 +351,20 @@ class Scheduler:
         self.free.append(slot)
 
     def _admit(self, batch: List[tuple]):
-        """Prefill newly admitted (slot, request) pairs together (Engine.prefill_batch) and
-        sample their first tokens."""
+        """Prefill newly admitted (slot, request) pairs (Engine.prefill_batch) and sample their
+        first tokens.  Prompts are length-sorted and grouped so that no group pads a prompt
+        to more than PREFILL_PAD_RATIO x its rows (every row of a group is computed; on the GPU
+        a prompt's rows are already rounded up to the flash kernel's 128-row tiles)."""
+        tile = 128 if self.e.dev.type == "cuda" else 1
+        rows = lambda sr: -(-len(sr[1].prompt) // tile) * tile      # noqa: E731
+        batch = sorted(batch, key=rows)
+        g0 = 0
+        for j in range(1, len(batch) + 1):
+            if j == len(batch) or rows(batch[j]) > PREFILL_PAD_RATIO * rows(batch[g0]):
+                self._admit_group(batch[g0:j])
+                g0 = j
+
+    def _admit_group(self, batch: List[tuple]):
         logits = self.e.prefill_batch([s for s, _ in batch], [r.prompt for _, r in batch])
         for j, (slot, req) in enumerate(batch):
             tok = int(sample(logits[j:j + 1], req.temperature, req.top_p)[0])

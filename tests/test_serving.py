@@ -55,6 +55,34 @@ def test_prefill_batch_matches_per_prompt_prefill(eng):
         assert torch.allclose(eng.vc[:, s, :, :n].float(), vc1[:, s, :, :n].float(), atol=1e-3)
 
 
+def test_scheduler_groups_prompts_by_length(eng, monkeypatch):
+    """Admitted prompts are prefilled in length groups (padding <= 1.25x of a prompt's rows);
+    the outputs equal one request at a time."""
+    calls = []
+    orig = eng.prefill_batch
+
+    def spy(slots, prompts):
+        calls.append(sorted(len(p) for p in prompts))
+        return orig(slots, prompts)
+
+    monkeypatch.setattr(eng, "prefill_batch", spy)
+    monkeypatch.setattr("service_account_auth_improvements_amd.serving.engine.PREFILL_PAD_RATIO", 1.25)
+    s = Scheduler(eng, max_batch=4)
+    prompts = [[3] * 4, [5] * 40, [7] * 5, [9] * 38]
+    reqs = [s.submit(Request(prompt=p, max_new_tokens=3)) for p in prompts]
+    monkeypatch.setattr("service_account_auth_improvements_amd.serving.engine.PREFILL_MAX_TOKENS", 1 << 20)
+    s.step()
+    assert calls == [[4, 5], [38, 40]]
+    s.run_until_idle()
+    solo = []
+    for p in prompts:
+        one = Scheduler(eng, max_batch=1)
+        r = one.submit(Request(prompt=p, max_new_tokens=3))
+        one.run_until_idle()
+        solo.append(r.output)
+    assert [r.output for r in reqs] == solo
+
+
 def test_continuous_batching_is_order_independent(eng):
     s = Scheduler(eng, max_batch=3)
     a = s.submit(Request(prompt=[1, 2, 3, 4], max_new_tokens=6))
