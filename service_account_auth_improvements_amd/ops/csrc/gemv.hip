@@ -28,7 +28,7 @@
 //    (tools/kbench/gemv_bench, profiles/serve_gemv_ksplit.txt): wd 24.1 -> 19.5 us at M = 1
 //    (6.0 TB/s), 29.2 -> 24.9 us at M = 4; at K = 4096 it is null at M = 1 and 10-15 % slower
 //    at M = 4, and with the norm prologue (every workgroup normalises X itself) 1.3-1.6x
-//    slower.  Hence: no prologue, K >= 8192 and < 4 workgroups per CU unsplit.
+//    slower.  Hence: no prologue, K >= 8192 (or M <= 2) and < 4 workgroups per CU unsplit.
 //    KFAMD_GEMV_KSPLIT=1 / 4 forces it off / on.
 #include "common.h"
 #include <cstdlib>
@@ -255,14 +255,15 @@ __global__ __launch_bounds__(64 * GV_WAVES) void gemv_kernel(const bf16_t* __res
 
 // K split for deep K without the norm prologue when the unsplit grid leaves the 256 CUs
 // with < 4 workgroups each; KFAMD_GEMV_KSPLIT=1 / 4 forces it off / on (A/B)
-bool use_ksplit(int blocks_unsplit, int K, bool norm) {
+bool use_ksplit(int blocks_unsplit, int M, int K, bool norm) {
   static const int force = [] {
     const char* e = getenv("KFAMD_GEMV_KSPLIT");
     return e ? atoi(e) : 0;
   }();
   if (force == 1) return false;
   if (force == GV_WAVES) return true;
-  return !norm && K >= 8192 && blocks_unsplit < 4 * 256;
+  // K = 4096 (wo) gains at 1-2 rows (8.9 -> 8.1-8.3 us, 9.7-10.1 -> 9.2-9.8 us) and loses at 4
+  return !norm && (K >= 8192 || M <= 2) && blocks_unsplit < 4 * 256;
 }
 
 template <int M, bool SWIGLU, bool NORM>
@@ -271,7 +272,7 @@ int gv_launch(const bf16_t* x, long ldx, const bf16_t* w, int N, int K, bf16_t* 
   constexpr int R = SWIGLU ? (GV_R_CFG > 1 ? GV_R_CFG / 2 : 1) : GV_R_CFG;
   const int blocks = (N + R * GV_WAVES - 1) / (R * GV_WAVES);
   const size_t dyn = NORM ? (size_t)M * K * 2 : 0;
-  if (use_ksplit(blocks, K, NORM))
+  if (use_ksplit(blocks, M, K, NORM))
     hipLaunchKernelGGL((gemv_kernel<M, R, SWIGLU, NORM, false, GV_WAVES>), dim3((N + R - 1) / R),
                        dim3(64 * GV_WAVES), dyn, st, x, ldx, w, N, K, y, ldy, up_off, na, GvRope{});
   else
@@ -297,7 +298,7 @@ template <int M>
 int gv_rope_launch(const bf16_t* x, long ldx, const bf16_t* w, int N, int K, bf16_t* y, long ldy, GvNorm na,
                    GvRope ra, hipStream_t st) {
   const int blocks = N / (4 * GV_WAVES);
-  if (use_ksplit(blocks, K, true))
+  if (use_ksplit(blocks, M, K, true))
     hipLaunchKernelGGL((gemv_kernel<M, 4, false, true, true, GV_WAVES>), dim3(N / 4), dim3(64 * GV_WAVES),
                        (size_t)M * K * 2, st, x, ldx, w, N, K, y, ldy, 0, na, ra);
   else
