@@ -145,12 +145,28 @@ def make_handler(server: APIServer):
                         ev = qq.get(timeout=wait)
                     except queue.Empty:
                         if bookmarks:
-                            self._chunk({"type": "BOOKMARK", "object": {
-                                "apiVersion": av, "kind": kind,
-                                "metadata": {"resourceVersion": server.resource_version}}})
+                            # The server assigns an RV and emits its event under its lock, so an
+                            # RV read under that lock with this stream's queue empty is covered:
+                            # every event up to it has been written to the client already.  A
+                            # bookmark read outside the lock could claim an event not yet queued,
+                            # and a client resuming from it would never see that event.
+                            with server._lock:
+                                brv = server.resource_version if qq.empty() else None
+                            if brv is not None:
+                                self._chunk({"type": "BOOKMARK", "object": {
+                                    "apiVersion": av, "kind": kind,
+                                    "metadata": {"resourceVersion": brv}}})
                         continue
                     self._chunk(ev)
-                self.wfile.write(b"0\r\n\r\n")       # timeoutSeconds reached: clean end
+                # timeoutSeconds reached: flush what is queued, then end cleanly (anything
+                # emitted after this is replayed when the client resumes from its last RV)
+                cancel()
+                while True:
+                    try:
+                        self._chunk(qq.get_nowait())
+                    except queue.Empty:
+                        break
+                self.wfile.write(b"0\r\n\r\n")
             except (BrokenPipeError, ConnectionResetError):
                 pass
             finally:

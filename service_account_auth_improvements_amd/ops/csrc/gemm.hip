@@ -41,15 +41,25 @@ typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 #define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
 
 namespace gm {
-constexpr int BM = 256, BN = 256, BK = 32, NBUF = 4;
+// K rows are staged BK at a time into an NBUF-deep LDS ring (KF_GEMM_NBUF: 4 = 128 KB, 5 = the
+// full 160 KB, DMA one stage further ahead)
+#ifndef KF_GEMM_NBUF
+#define KF_GEMM_NBUF 4
+#endif
+constexpr int BM = 256, BN = 256, BK = 32, NBUF = KF_GEMM_NBUF;
+static_assert(NBUF == 4 || NBUF == 5, "ring depth");
 constexpr int IMG = BK * 256;               // one [32][128] bf16 image: 8 KB
-constexpr int SMEM = 4 * NBUF * IMG;        // images laid out [image][buffer]: 128 KB
+constexpr int SMEM = 4 * NBUF * IMG;        // images laid out [image][buffer]: 128 / 160 KB
 // M-tiles per raster group: 4 measured 1.0-1.3 % faster than 8 over the step's dW shapes on
 // two boxes (16 / 32: -3 % / -6 %; tools/gpu_r2_gemm.sh); -DKF_GEMM_GROUP_M overrides
 #ifndef KF_GEMM_GROUP_M
 #define KF_GEMM_GROUP_M 4
 #endif
 constexpr int GROUP_M = KF_GEMM_GROUP_M;
+// 1 = waves 4-7 issue their stage's DMA pieces four MFMA groups after waves 0-3 (see kernel)
+#ifndef KF_GEMM_DMA_STAGGER
+#define KF_GEMM_DMA_STAGGER 0
+#endif
 
 __device__ __forceinline__ int blk_x(int row) { return (row & 3) | ((row >> 1) & 4); }
 
@@ -200,11 +210,14 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_kernel(TnGroup grp, int K) {
   u32 dmo[4];
   dma_offsets(lda, ldb, wave, lane, dmo);
   const u32 lds_w = __builtin_amdgcn_readfirstlane(lds_addr(smem) + 1024 * wave);
-  // prologue: stages 0..2 in flight, publish stage 0, first operand reads
+  // DMA issue point (KF_GEMM_DMA_STAGGER): waves 4-7 issue four MFMA groups after waves 0-3,
+  // so the two waves sharing a SIMD do not stall on DMA issue at the same time
+  const bool late = KF_GEMM_DMA_STAGGER && __builtin_amdgcn_readfirstlane(wave) >= 4;
+  // prologue: stages 0..NBUF-2 in flight, publish stage 0, first operand reads
 #pragma unroll
   for (int s = 0; s < NBUF - 1; ++s)
     if (s < nk) stage_dma(Ap + s * astep, Bp + s * bstep, dmo, lds_w + s * IMG);
-  if (nk >= 3) vm_wait<8>(); else vm_wait<0>();
+  if (nk >= NBUF - 1) vm_wait<4 * (NBUF - 2)>(); else vm_wait<0>();
   barrier();
 
   const char* dA = Ap + (NBUF - 1) * astep;   // next stage to DMA (loop-carried, wave-uniform)
@@ -215,10 +228,10 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_kernel(TnGroup grp, int K) {
   nb[2] = tr_frag<0>(bad[2]);  a[2] = tr_frag<0>(aad[2]);
   nb[3] = tr_frag<0>(bad[3]);  a[3] = tr_frag<0>(aad[3]);
 
-  // One ring revolution = 4 stages, buffer index a compile-time immediate.
+  // One ring revolution = NBUF stages, buffer index a compile-time immediate.
   auto stage = [&](auto bufc, int s) {
     constexpr int CB = decltype(bufc)::value, NX = (CB + 1) % NBUF;
-    constexpr int OC = CB * IMG, ON = NX * IMG;
+    constexpr int OC = CB * IMG, ON = NX * IMG, OF = ((CB + NBUF - 1) % NBUF) * IMG;
 #pragma unroll
     for (int u = 0; u < 4; ++u) b[u] = nb[u];
     auto group = [&](auto tc) {
@@ -228,19 +241,39 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_kernel(TnGroup grp, int K) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) acc[u][t] = mfma16(b[u], a[t], acc[u][t]);
       if constexpr (t == 3) {
-        // publish stage s+1 (its DMA was issued two stages ago), then refill the buffer
-        // every wave has finished with (stage s-1's) with stage s+3
-        if (s + 2 < nk) vm_wait<4>(); else vm_wait<0>();
+        // publish stage s+1 (its DMA went out NBUF-2 stages ago): wait until only the pieces
+        // of the stages after it that exist are outstanding
+        // (KF_ABL_* : anatomy builds for tools/kbench only -- numerics deliberately broken)
+#ifndef KF_ABL_NOVMW
+        if constexpr (NBUF == 5) {
+          if (s + 3 < nk) vm_wait<8>(); else if (s + 2 < nk) vm_wait<4>(); else vm_wait<0>();
+        } else {
+          if (s + 2 < nk) vm_wait<4>(); else vm_wait<0>();
+        }
+#endif
+#ifndef KF_ABL_NOBAR
         barrier();
-        if (s + 3 < nk) {
-          stage_dma(dA, dB, dmo, lds_w + ((CB + 3) % NBUF) * IMG);
+#endif
+      }
+      // refill the buffer every wave has finished with (stage s-1's) with stage s+NBUF-1
+      if constexpr (t == 3 || t == 7) {
+        if ((t == 3) != late && s + NBUF - 1 < nk) {
+#ifndef KF_ABL_NODMA
+#ifdef KF_ABL_DMASAME
+          stage_dma(Ap, Bp, dmo, lds_w + OF);   // always the (L2-resident) first panel rows
+#else
+          stage_dma(dA, dB, dmo, lds_w + OF);
+#endif
+#endif
           dA += astep;
           dB += bstep;
         }
       }
+#ifndef KF_ABL_NOREAD
       if constexpr (t >= 4) nb[t - 4] = tr_frag<ON>(bad[t - 4]);
       if constexpr (t < 4) a[t + 4] = tr_frag<OC>(aad[t + 4]);
       else a[t - 4] = tr_frag<ON>(aad[t - 4]);
+#endif
     };
     group(std::integral_constant<int, 0>());
     group(std::integral_constant<int, 1>());
@@ -251,11 +284,22 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_kernel(TnGroup grp, int K) {
     group(std::integral_constant<int, 6>());
     group(std::integral_constant<int, 7>());
   };
-  for (int s = 0; s < nk; s += NBUF) {
+  // the ring revolution is unrolled; a K that is not a multiple of NBUF stages leaves the
+  // last revolution early (wave-uniform)
+  int s = 0;
+  for (; s + NBUF <= nk; s += NBUF) {
     stage(std::integral_constant<int, 0>(), s);
     stage(std::integral_constant<int, 1>(), s + 1);
     stage(std::integral_constant<int, 2>(), s + 2);
     stage(std::integral_constant<int, 3>(), s + 3);
+    if constexpr (NBUF == 5) stage(std::integral_constant<int, 4 % NBUF>(), s + 4);
+  }
+  if constexpr (NBUF == 5) {
+    const int rem = nk - s;
+    if (rem >= 1) stage(std::integral_constant<int, 0>(), s);
+    if (rem >= 2) stage(std::integral_constant<int, 1>(), s + 1);
+    if (rem >= 3) stage(std::integral_constant<int, 2>(), s + 2);
+    if (rem >= 4) stage(std::integral_constant<int, 3>(), s + 3);
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 
@@ -282,7 +326,7 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_kernel(TnGroup grp, int K) {
 
 static bool tn_shape_ok(const void* A, long lda, const void* B, long ldb, const void* C, long ldc, int M, int N,
                         int K) {
-  if (M % BM || N % BN || K % (BK * NBUF) || lda % 8 || ldb % 8 || ldc % 4) return false;
+  if (M % BM || N % BN || K % (NBUF == 4 ? BK * NBUF : BK) || K < BK * NBUF || lda % 8 || ldb % 8 || ldc % 4) return false;
   return !(((uintptr_t)A | (uintptr_t)B) & 15) && !((uintptr_t)C & 7);
 }
 

@@ -130,6 +130,48 @@ def test_watch_bookmarks_and_timeout(rest, monkeypatch):
     assert lines[-1]["object"]["metadata"]["resourceVersion"] == s.resource_version
 
 
+def test_bookmark_never_covers_an_unsent_event(monkeypatch):
+    """Writers race short watch streams that bookmark constantly and end at timeoutSeconds: the
+    client resumes from its last BOOKMARK / event RV each time, so a bookmark whose RV covers an
+    event not yet written to the stream would lose that event for good.  The history
+    is large enough that no resume hits 410 (whose re-list would mask a loss)."""
+    from service_account_auth_improvements_amd.controlplane import httpapi
+    monkeypatch.setattr(httpapi, "BOOKMARK_PERIOD", 0.002)
+    monkeypatch.setattr(RestClient, "WATCH_TIMEOUT", 0.05)
+    s = APIServer(history=100000)
+    s.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "default"}})
+    emit = s._emit
+
+    def slow_emit(*a, **kw):        # widen the window between RV assignment and the event
+        time.sleep(0.01)
+        return emit(*a, **kw)
+    s._emit = slow_emit
+    h = APIServerHTTP(s).start()
+    try:
+        c = RestClient(h.url)
+        seen, lk = set(), threading.Lock()
+
+        def on(et, o):
+            if et == "ADDED":
+                with lk:
+                    seen.add(o["metadata"]["name"])
+        stop = c.watch(on, "v1", "ConfigMap")
+
+        def writer(k):
+            for i in range(40):
+                s.create(_cm(f"w{k}-{i}"))
+        ws = [threading.Thread(target=writer, args=(k,)) for k in range(3)]
+        for w in ws:
+            w.start()
+        for w in ws:
+            w.join()
+        ok = _wait(lambda: len(seen) == 120, timeout=20)
+        stop()
+        assert ok, sorted({f"w{k}-{i}" for k in range(3) for i in range(40)} - seen)[:10]
+    finally:
+        h.stop()
+
+
 def test_workqueue_is_fifo_dedup_and_never_concurrent():
     q = WorkQueue()
     for k in ("a", "b", "a", "c"):

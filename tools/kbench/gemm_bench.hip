@@ -1,5 +1,5 @@
 // Standalone microbench for the dW GEMM (ops/csrc/gemm.hip) at the Llama-3-8B training shapes
-// (K = 16384 tokens): C[M,N] = A^T B with A [K, M], B [K, N].  Prints per-shape time, TFLOP/s
+// (K = 32768 tokens = micro-batch 4 x 8192 by default): C[M,N] = A^T B with A [K, M], B [K, N].  Prints per-shape time, TFLOP/s
 // and a checksum so build variants (-D flags) can be compared.  Run: gemm_bench [iters].
 #include "../../service_account_auth_improvements_amd/ops/csrc/gemm.hip"
 
@@ -35,7 +35,7 @@ __global__ void checksum(const bf16_t* c, long n, double* out) {
 
 int main(int argc, char** argv) {
   const int iters = argc > 1 ? atoi(argv[1]) : 20;
-  const int K = 16384;
+  const int K = argc > 2 ? atoi(argv[2]) : 32768;
   struct Shape { const char* name; int M, N; };
   const Shape shapes[] = {{"wqkv", 6144, 4096}, {"wo", 4096, 4096}, {"wgu", 28672, 4096},
                           {"wd", 4096, 14336}, {"lm_head", 128256, 4096}};
