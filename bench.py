@@ -18,6 +18,11 @@ Multi-GPU (N > 1): data parallel over RCCL.  Default is ZeRO-1 -- gradient bucke
 reduce-scattered while backward runs, AdamW updates 1/N of the fp32 state per GPU, and the
 bf16 parameter all-gather is launched right after the update and waited on per bucket by
 the next forward (runtime/trainer.py, parallel/ddp.py).  ``--no-zero1`` = all-reduce DDP.
+
+CRD-to-first-step (the metric's second half): before any GPU use, ``--crd-jobs`` PyTorchJob CRs
+of the same model (micro-batch 1, one step each) go through the in-repo control plane running
+as processes; the JSON line carries ``crd_to_first_step_p50_s`` / ``_p90_s`` and the breakdown
+(service_account_auth_improvements_amd/crdbench.py).
 """
 from __future__ import annotations
 
@@ -69,14 +74,41 @@ def _auto_micro_batch(dp: int, zero1: bool, grad_reduce: str, collectives: bool,
     return 1
 
 
-def _launch_ranks(n: int) -> int:
+def _launch_ranks(n: int, crd: "dict | None") -> int:
     """Run this script as N ranks under torch.distributed.run (a child process; this process
-    has not initialised the GPU and never does)."""
+    has not initialised the GPU and never does).  The CRD-to-first-step result measured here
+    travels to rank 0 in the environment."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.abspath(__file__), *sys.argv[1:]]
     print(f"bench: launching {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
-    return subprocess.call(cmd)
+    env = dict(os.environ)
+    if crd is not None:
+        env[CRD_ENV] = json.dumps(crd)
+    return subprocess.call(cmd, env=env)
+
+
+CRD_ENV = "KFAMD_BENCH_CRD_RESULT"
+
+
+def _crd_to_first_step(a) -> "dict | None":
+    """The metric's second half, measured before this process touches the GPU: the in-repo
+    control plane as processes (apiserver / controller-manager / kubelet), ``--crd-jobs``
+    PyTorchJobs of this bench's model, one after another, each a fresh worker process that
+    runs one step and exits (service_account_auth_improvements_amd/crdbench.py)."""
+    if a.crd_jobs <= 0:
+        return None
+    from service_account_auth_improvements_amd.crdbench import measure
+    gpus = 1 if torch.cuda.device_count() > 0 else 0          # counts devices, no HIP context
+    t0 = time.time()
+    try:
+        res = measure(jobs=a.crd_jobs, model=a.model, gpus=gpus, seq_len=a.seq_len, micro_batch=1,
+                      layers=a.layers, device="cuda" if gpus else "cpu", timeout=a.crd_timeout)
+    except Exception as e:   # the throughput half still runs; the record says what failed
+        print(f"bench: CRD-to-first-step failed: {e}", file=sys.stderr, flush=True)
+        return {"error": str(e)[-500:]}
+    res["phase_s"] = round(time.time() - t0, 1)
+    return res
 
 
 def main():
@@ -117,15 +149,24 @@ def main():
                          "group, to check the N > 1 path's memory and call sequence at full size on one GPU")
     ap.add_argument("--layers", type=int, default=None, help="DEBUG ONLY: invalid for reporting")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--crd-jobs", type=int, default=3,
+                    help="PyTorchJobs submitted to the process-level control plane before the throughput run "
+                         "to measure CRD-to-first-step (0 = skip)")
+    ap.add_argument("--crd-timeout", type=float, default=300.0)
     a = ap.parse_args()
 
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None and a.gpus > 1:
-        sys.exit(_launch_ranks(a.gpus))
+        sys.exit(_launch_ranks(a.gpus, _crd_to_first_step(a)))
     if int(env_world or 1) != a.gpus:
         print(f"bench: --gpus {a.gpus} but WORLD_SIZE={env_world}: refusing to report a "
               "different GPU count", file=sys.stderr)
         sys.exit(2)
+    crd = None
+    if int(os.environ.get("RANK", "0")) == 0:
+        # self-launched ranks inherit the parent's measurement; under an external launcher rank 0
+        # measures it while the other ranks wait in the process-group rendezvous
+        crd = json.loads(os.environ[CRD_ENV]) if CRD_ENV in os.environ else _crd_to_first_step(a)
     if a.force_collectives:
         if a.gpus != 1:
             sys.exit("bench: --force-collectives is a one-GPU rehearsal")
@@ -243,6 +284,10 @@ def main():
             "loss_first": round(float(lt[0]), 4),
             "loss_last": round(float(lt[1]), 4),
         }
+        if crd is not None:
+            out["crd_to_first_step_p50_s"] = crd.get("p50_s")
+            out["crd_to_first_step_p90_s"] = crd.get("p90_s")
+            out["crd_to_first_step"] = crd
         if a.layers is not None:
             out["INVALID"] = "reduced layer count (debug run)"
         if a.force_collectives:

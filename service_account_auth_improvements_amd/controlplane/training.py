@@ -173,7 +173,8 @@ class _JobBase(Controller):
                 policy = self._restart_policy(job, rtype, specs)
                 code = self._exit_code(live)
                 retryable = policy == "OnFailure" or (policy == "ExitCode" and code is not None and code >= 128)
-                if retryable and not terminal and (backoff is None or restarts < int(backoff)):
+                limit = self._backoff_limit(rtype, backoff)
+                if retryable and not terminal and (limit is None or restarts < int(limit)):
                     restarts += 1
                     c.delete("v1", "Pod", live["metadata"]["name"], req.namespace)
                     _set_condition(status, "Restarting", f"{self.kind}Restarting",
@@ -181,7 +182,9 @@ class _JobBase(Controller):
                     rs["active"] += 1
                 else:
                     rs["failed"] += 1
-                    failed_msg = f'{self.kind} {req.name} has failed because {rtype} replica(s) failed.'
+                    msg = self._failure_message(req.name, rtype, live)
+                    if msg:
+                        failed_msg = msg
             elif phase in ("Running", "Pending", None) and live is not None:
                 rs["active"] += 1
         status["replicaStatuses"] = rstat
@@ -194,7 +197,7 @@ class _JobBase(Controller):
                 _set_condition(status, "Succeeded", f"{self.kind}Succeeded",
                                f'{self.kind} {req.name} is successfully completed.')
                 status["completionTime"] = now_rfc3339()
-            elif any(p.get("status", {}).get("phase") == "Running" for p in pods.values()):
+            elif self._running(pods, rstat):
                 if not _has(status, "Running"):
                     _set_condition(status, "Running", f"{self.kind}Running", f'{self.kind} {req.name} is running.')
                 status.setdefault("startTime", now_rfc3339())
@@ -214,6 +217,19 @@ class _JobBase(Controller):
 
     def _restart_policy(self, job, rtype, specs) -> str:
         return specs[rtype].get("restartPolicy", "OnFailure")
+
+    def _backoff_limit(self, rtype: str, backoff):
+        """How many restarts ``runPolicy.backoffLimit`` allows a replica of this type (None =
+        unlimited)."""
+        return backoff
+
+    def _failure_message(self, name: str, rtype: str, pod: dict) -> Optional[str]:
+        """The Failed condition's message when a non-retried ``rtype`` pod failing ends the job,
+        or None when that failure does not decide the job."""
+        return f'{self.kind} {name} has failed because {rtype} replica(s) failed.'
+
+    def _running(self, pods: dict, rstat: dict) -> bool:
+        return any(p.get("status", {}).get("phase") == "Running" for p in pods.values())
 
     @staticmethod
     def _exit_code(pod):
@@ -412,6 +428,34 @@ class MPIJobReconciler(_JobBase):
 
     def _succeeded(self, rstat, specs):
         return rstat.get("Launcher", {}).get("succeeded", 0) >= 1
+
+    # --- mpi-operator v2beta1 outcome semantics (pkg/controller/mpi_job_controller.go
+    # updateMPIJobStatus): the Launcher decides the job.  It runs as a batch Job whose
+    # backoffLimit is runPolicy.backoffLimit (the batch default, 6, when unset); a Worker that
+    # fails is counted in replicaStatuses but reaches the job only through the Launcher's exit
+    # code (mpirun / mpi-wait sees the rank die) -- except an evicted Worker, which fails the job.
+    BATCH_BACKOFF_DEFAULT = 6
+
+    def _backoff_limit(self, rtype, backoff):
+        if rtype == "Launcher":
+            return self.BATCH_BACKOFF_DEFAULT if backoff is None else backoff
+        return backoff
+
+    def _failure_message(self, name, rtype, pod):
+        if rtype == "Launcher":
+            return f"MPIJob {name} has failed because the launcher failed."
+        if (pod.get("status") or {}).get("reason") == "Evicted":
+            return f"MPIJob {name} has failed because a worker was evicted."
+        return None
+
+    def _running(self, pods, rstat):
+        """Running once the Launcher runs and every Worker has started (upstream: launcher
+        active and all workers Running; a Worker mpirun placed no rank on exits at once)."""
+        phases = {p["metadata"]["labels"].get(LBL_RTYPE): [] for p in pods.values()}
+        for p in pods.values():
+            phases[p["metadata"]["labels"].get(LBL_RTYPE)].append(p.get("status", {}).get("phase"))
+        return ("Running" in phases.get("launcher", []) and
+                all(ph in ("Running", "Succeeded") for ph in phases.get("worker", [])))
 
 
 def pytorchjob_manifest(name: str, namespace: str, image: str, command: List[str], n_nodes: int = 1,

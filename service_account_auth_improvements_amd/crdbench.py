@@ -1,0 +1,142 @@
+"""CRD-to-first-step latency -- the second half of BASELINE.json's headline metric
+("... ; CRD-to-first-step p50", SURVEY.md §3.7: CR creationTimestamp -> the first step's log
+line).
+
+The platform runs as separate processes over HTTP (``cluster.ProcessCluster``: apiserver,
+controller-manager with the training operator and scheduler, one kubelet per node with the
+``amd.com/gpu`` device plugin); pods are real processes on this host.  Jobs are submitted one
+after another; each job's workers are fresh processes (kfamd-launch -> ``python -m
+service_account_auth_improvements_amd train``) that run one optimizer step and exit before
+the next job's CR is created.  Per job the wall-clock time from the CR ``create`` call to rank
+0's ``first_step`` event is measured, with a breakdown:
+
+* ``cr_to_running``      CR create -> rank-0 pod Running (operator, scheduler, kubelet)
+* ``running_to_process`` pod Running -> worker process start (kfamd-launch, interpreter)
+* ``import``             worker start -> torch + runtime imported
+* ``dist_init``          HIP runtime / device (+ process group when world > 1)
+* ``model_init``         parameters, optimizer state
+* ``init_to_first_step`` the first train step (first kernel / library loads included)
+
+Used by ``bench.py`` (reported in its JSON line, measured before the bench process touches
+the GPU) and by ``tools/bench_crd_to_step.py``.
+"""
+from __future__ import annotations
+
+import json
+import os
+import statistics
+import sys
+import tempfile
+import time
+from typing import Callable, List, Optional
+
+BREAKDOWN = ("cr_to_running", "running_to_process", "import", "dist_init", "model_init",
+             "init_to_first_step", "process_to_init", "params_alloc_init", "optimizer_state")
+
+
+def _events(path: str) -> list:
+    try:
+        with open(path) as f:
+            return [json.loads(x) for x in f.read().splitlines() if x.strip()]
+    except (OSError, ValueError):
+        return []
+
+
+def measure(jobs: int = 3, model: str = "llama3-8b", gpus: int = 1, nodes: int = 1, seq_len: int = 8192,
+            micro_batch: int = 1, layers: Optional[int] = None, device: str = "cuda", kind: str = "pytorchjob",
+            processes: bool = True, gap: float = 0.0, timeout: float = 300.0, port_base: int = 29700,
+            log: Callable[[str], None] = lambda s: print(s, file=sys.stderr, flush=True)) -> dict:
+    """Submit ``jobs`` jobs one after another; returns p50 / p90 / min and the breakdown."""
+    from .cluster import LocalCluster, ProcessCluster
+    from .controlplane import training
+    from .native import build_native
+    build_native()
+    tmp = tempfile.mkdtemp(prefix="crd2step-")
+    events = os.path.join(tmp, "events.jsonl")
+    env = {"KFAMD_EVENTS_FILE": events, "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS", "4")}
+    t_up = time.time()
+    if processes:
+        cl = ProcessCluster(nodes=nodes, gpus_per_node=gpus, exec_pods=True, log_dir=tmp, extra_env=env).start()
+        client, pod_log = cl.client, cl.pod_log
+        client.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "bench"}})
+    else:
+        cl = LocalCluster(n_gpus=gpus * nodes, exec_pods=True, api_port=None, log_dir=tmp, extra_env=env).start()
+        client, pod_log = cl.client, cl.kubelet.pod_log
+        cl.server.ensure_namespace("bench")
+    t_up = time.time() - t_up
+    cmd = [sys.executable, "-m", "service_account_auth_improvements_amd", "train", "--model", model,
+           "--steps", "1", "--device", device]
+    if model != "mnist":
+        cmd += ["--seq-len", str(seq_len), "--micro-batch", str(micro_batch)]
+    else:
+        cmd += ["--micro-batch", "64"]
+    if layers:
+        cmd += ["--layers", str(layers)]
+    rows: List[dict] = []
+    try:
+        for j in range(jobs):
+            if j and gap:
+                time.sleep(gap)
+            name = f"job{j}"
+            open(events, "w").close()
+            port = port_base + 7 * j
+            if kind == "mpijob":
+                job = training.mpijob_manifest(name, "bench", "local", cmd, workers=nodes, gpus_per_worker=gpus,
+                                               master_port=port)
+                rank0_pod = f"{name}-worker-0"
+            else:
+                job = training.pytorchjob_manifest(name, "bench", "local", cmd, n_nodes=nodes, gpus_per_node=gpus,
+                                                   master_port=port)
+                if not gpus:
+                    job["spec"]["nprocPerNode"] = "1"
+                rank0_pod = f"{name}-master-0"
+            t0 = time.time()
+            client.create(job)
+            t_running = None
+            first = None
+            evs: list = []
+            deadline = t0 + timeout
+            while time.time() < deadline:
+                if t_running is None:
+                    p = client.get_or_none("v1", "Pod", rank0_pod, "bench")
+                    if p and (p.get("status") or {}).get("phase") == "Running":
+                        t_running = time.time()
+                evs = _events(events)
+                fs = [e for e in evs if e["event"] == "first_step" and e.get("rank") == 0]
+                if fs:
+                    first = fs[0]
+                    break
+                time.sleep(0.01)
+            if first is None:
+                raise RuntimeError(f"{name}: no first_step within {timeout}s\n" + pod_log("bench", rank0_pod)[-3000:])
+            r0 = [e for e in evs if e.get("rank") == 0]
+            ps = next(e["ts"] for e in r0 if e["event"] == "process_start")
+            ie = next(e for e in r0 if e["event"] == "init_done")
+            imp = next((e["ts"] for e in r0 if e["event"] == "imported"), ps)
+            dr = next((e["ts"] for e in r0 if e["event"] == "dist_ready"), imp)
+            tr = t_running or ps
+            rows.append({"total": first["ts"] - t0, "cr_to_running": tr - t0, "running_to_process": ps - tr,
+                         "process_to_init": ie["ts"] - ps, "import": imp - ps, "dist_init": dr - imp,
+                         "model_init": ie["ts"] - dr, "init_to_first_step": first["ts"] - ie["ts"],
+                         "params_alloc_init": ie.get("params_alloc_init_s", 0.0),
+                         "optimizer_state": ie.get("optimizer_state_s", 0.0)})
+            log(json.dumps({"crd_job": name, **{k: round(v, 3) for k, v in rows[-1].items()}}))
+            # the job ends after its step; wait for it (and its pods' processes) so the devices
+            # are free for the next job and for whatever runs after this measurement
+            while time.time() < deadline:
+                jb = client.get(job["apiVersion"], job["kind"], name, "bench")
+                conds = (jb.get("status") or {}).get("conditions", [])
+                if any(c["type"] in ("Succeeded", "Failed") and c["status"] == "True" for c in conds):
+                    break
+                time.sleep(0.05)
+    finally:
+        cl.stop()
+    tot = sorted(r["total"] for r in rows)
+    return {"jobs": len(rows), "kind": kind, "model": model, "gpus_per_node": gpus, "nodes": nodes,
+            "control_plane": "processes over HTTP" if processes else "in-process",
+            "p50_s": round(statistics.median(tot), 3),
+            "p90_s": round(tot[min(len(tot) - 1, int(0.9 * len(tot)))], 3),
+            "min_s": round(tot[0], 3), "max_s": round(tot[-1], 3),
+            "per_job_s": [round(r["total"], 3) for r in rows],
+            "cluster_up_s": round(t_up, 2),
+            "breakdown_p50_s": {k: round(statistics.median(r[k] for r in rows), 3) for k in BREAKDOWN}}

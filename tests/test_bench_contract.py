@@ -9,7 +9,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
         "vs_baseline", "dtype", "data", "config"}
-ARGS = ["--model", "tiny", "--seq-len", "64", "--micro-batch", "1", "--steps", "2", "--warmup", "1"]
+ARGS = ["--model", "tiny", "--seq-len", "64", "--micro-batch", "1", "--steps", "2", "--warmup", "1", "--crd-jobs", "0"]
 
 
 def _port():
@@ -41,6 +41,26 @@ def test_bench_single_process_json():
     recs = _json_lines(r.stdout)
     assert len(recs) == 1
     _check(recs[0], 1)
+
+
+def test_bench_reports_crd_to_first_step():
+    """The metric's second half: PyTorchJobs through the process-level control plane before the
+    throughput run; p50 / p90 and the breakdown land in the same JSON line."""
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="2")
+    args = [x for x in ARGS if x not in ("--crd-jobs", "0")] + ["--crd-jobs", "2"]
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], capture_output=True, text=True,
+                       timeout=600, env=env, cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-3000:]
+    (rec,) = _json_lines(r.stdout)
+    _check(rec, 1)
+    crd = rec["crd_to_first_step"]
+    assert "error" not in crd, crd
+    assert crd["jobs"] == 2 and crd["control_plane"] == "processes over HTTP" and crd["model"] == "tiny"
+    assert 0 < rec["crd_to_first_step_p50_s"] <= rec["crd_to_first_step_p90_s"] < 120
+    b = crd["breakdown_p50_s"]
+    assert b["cr_to_running"] < b["import"] + b["init_to_first_step"] + 5
+    assert abs(sum(b[k] for k in ("cr_to_running", "running_to_process", "import", "dist_init", "model_init",
+                                   "init_to_first_step")) - crd["p50_s"]) < 1.0
 
 
 def test_bench_two_ranks_torchrun_json():

@@ -37,7 +37,7 @@ def test_parse_mpirun_and_rank_layout():
         {"name": "NCCL_DEBUG", "value": "INFO"}, {"name": "PATH", "value": "/opt/rocm/bin"}]
 
 
-def _mpijob(name, ns, program, np_, workers=2, slots=2, port=29781):
+def _mpijob(name, ns, program, np_, workers=2, slots=2, port=29781, backoff=None):
     lt = {"spec": {"containers": [{"name": "launcher", "image": "kfamd/trainer-rocm",
                                    "command": ["mpirun", "--allow-run-as-root", "-np", str(np_),
                                                "-x", "KFAMD_MARK=mpijob", "-x", "TRACE"] + program,
@@ -46,7 +46,8 @@ def _mpijob(name, ns, program, np_, workers=2, slots=2, port=29781):
                                    "command": ["/usr/sbin/sshd", "-De"]}]}}
     return {"apiVersion": training.MPI_API, "kind": "MPIJob",
             "metadata": {"name": name, "namespace": ns, "annotations": {"kfamd.io/master-port": str(port)}},
-            "spec": {"slotsPerWorker": slots, "runPolicy": {"cleanPodPolicy": "None"},
+            "spec": {"slotsPerWorker": slots,
+                     "runPolicy": {"cleanPodPolicy": "None", **({} if backoff is None else {"backoffLimit": backoff})},
                      "mpiReplicaSpecs": {"Launcher": {"replicas": 1, "template": lt},
                                          "Worker": {"replicas": workers, "template": wt}}}}
 
@@ -94,7 +95,7 @@ def test_mpirun_mpijob_end_to_end_across_processes(tmp_path, fail):
         c = pc.client
         c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "team"}})
         c.create(_mpijob("mj", "team", [sys.executable, "-c", code], np_=3, workers=2, slots=2,
-                         port=29791 + int(fail) * 7))
+                         port=29791 + int(fail) * 7, backoff=1))
         deadline = time.time() + 120
         state = None
         while time.time() < deadline and state is None:
@@ -110,8 +111,81 @@ def test_mpirun_mpijob_end_to_end_across_processes(tmp_path, fail):
                    and r["OMPI_COMM_WORLD_RANK"] == r["RANK"] for r in ranks)
         assert ("failed with exit code 3" in log) == fail
         assert ("all 2 workers succeeded" in log) == (not fail)
+        if fail:      # the Launcher decided it, after its one allowed restart (backoffLimit 1)
+            j = c.get(training.MPI_API, "MPIJob", "mj", "team")
+            assert j["status"]["restartCount"] == 1
+            assert "launcher failed" in next(x["message"] for x in j["status"]["conditions"] if x["type"] == "Failed")
     finally:
         pc.stop()
+
+
+def _set_phase(c, name, ns, phase, code=None, reason=None):
+    p = c.get("v1", "Pod", name, ns)
+    st = {"phase": phase}
+    if code is not None:
+        st["containerStatuses"] = [{"name": "x", "state": {"terminated": {"exitCode": code}}}]
+    if reason:
+        st["reason"] = reason
+    p["status"] = st
+    c.update_status(p)
+
+
+def _conds(c, name, ns):
+    j = c.get(training.MPI_API, "MPIJob", name, ns)
+    return {x["type"] for x in (j.get("status") or {}).get("conditions", []) if x["status"] == "True"}, j
+
+
+def test_worker_failure_reaches_the_job_only_through_the_launcher():
+    """mpi-operator v2beta1: a failed Worker pod is counted, but the job stays Running until the
+    Launcher exits; the Launcher's failure (after runPolicy.backoffLimit restarts) fails it."""
+    srv = APIServer()
+    c = InMemoryClient(srv)
+    srv.ensure_namespace("team")
+    mgr = Manager(c)
+    mgr.add(training.MPIJobReconciler(c))
+    c.create(_mpijob("w", "team", ["python", "train.py"], np_=4, workers=2, slots=2, backoff=1))
+    mgr.run_until_idle()
+    for n in ("w-launcher-0", "w-worker-0", "w-worker-1"):
+        _set_phase(c, n, "team", "Running")
+    mgr.run_until_idle()
+    conds, _ = _conds(c, "w", "team")
+    assert "Running" in conds
+    _set_phase(c, "w-worker-1", "team", "Failed", code=3)       # a rank dies
+    mgr.run_until_idle()
+    conds, j = _conds(c, "w", "team")
+    assert "Failed" not in conds and "Running" in conds, j["status"]
+    assert j["status"]["replicaStatuses"]["Worker"]["failed"] == 1
+    assert c.get_or_none("v1", "Pod", "w-worker-1", "team") is not None   # not restarted behind mpirun
+    _set_phase(c, "w-launcher-0", "team", "Failed", code=1)     # mpi-wait reports it: restart 1 of 1
+    mgr.run_until_idle()
+    conds, j = _conds(c, "w", "team")
+    assert "Failed" not in conds and "Restarting" in conds and j["status"]["restartCount"] == 1
+    _set_phase(c, "w-launcher-0", "team", "Failed", code=1)     # the recreated launcher fails too
+    mgr.run_until_idle()
+    conds, j = _conds(c, "w", "team")
+    assert "Failed" in conds and "launcher failed" in next(
+        x["message"] for x in j["status"]["conditions"] if x["type"] == "Failed")
+
+
+def test_launcher_success_decides_even_with_a_failed_worker_and_eviction_fails():
+    srv = APIServer()
+    c = InMemoryClient(srv)
+    srv.ensure_namespace("team")
+    mgr = Manager(c)
+    mgr.add(training.MPIJobReconciler(c))
+    c.create(_mpijob("s", "team", ["python", "t.py"], np_=4, workers=2, slots=2))
+    c.create(_mpijob("e", "team", ["python", "t.py"], np_=4, workers=2, slots=2, port=29782))
+    mgr.run_until_idle()
+    _set_phase(c, "s-worker-0", "team", "Failed", code=1)
+    _set_phase(c, "s-launcher-0", "team", "Succeeded", code=0)
+    mgr.run_until_idle()
+    assert "Succeeded" in _conds(c, "s", "team")[0]
+    _set_phase(c, "e-launcher-0", "team", "Running")
+    _set_phase(c, "e-worker-0", "team", "Failed", reason="Evicted")
+    mgr.run_until_idle()
+    conds, j = _conds(c, "e", "team")
+    assert "Failed" in conds and "evicted" in next(x["message"] for x in j["status"]["conditions"]
+                                                   if x["type"] == "Failed")
 
 
 def test_sample_mpijob_translates():
