@@ -404,11 +404,29 @@ class Llama:
     def head_fwd(self, r, d, labels: torch.Tensor, scale: float):
         """Final RMSNorm only.  Returns (loss, ctx): ``loss`` is a 0-d fp32 device tensor that
         :meth:`head_bwd` fills in (already multiplied by ``scale``) -- the logits are produced,
-        consumed and discarded chunk by chunk there (K5), never as one [T, vocab] buffer."""
+        consumed and discarded chunk by chunk there (K5), never as one [T, vocab] buffer.
+        Until then it holds NaN, so a caller that reads it without running the backward gets an
+        unmistakable value, never a plausible 0; forward-only callers use :meth:`head_loss`."""
         cfg = self.cfg
         y, h, rstd = ops.rmsnorm_fwd(r, self.P("final_norm"), cfg.norm_eps, residual=d)
-        loss = torch.zeros((), device=y.device, dtype=torch.float32)
+        loss = torch.full((), float("nan"), device=y.device, dtype=torch.float32)
         return loss, (h, rstd, y, labels, scale, loss)
+
+    @torch.no_grad()
+    def head_loss(self, ctx) -> torch.Tensor:
+        """Forward-only K5: the chunked LM head + CE loss (times ``scale``) without gradients --
+        evaluation and any caller that wants the loss without a backward pass."""
+        h, rstd, y, labels, scale, _ = ctx
+        y = self._gather(y)
+        W = self.P("lm_head")
+        T = y.shape[0]
+        tc = self.head_chunk if self.head_chunk and self.head_chunk < T else T
+        tot = None
+        for c0 in range(0, T, tc):
+            c1 = min(T, c0 + tc)
+            rows = self._ce_chunk(torch.mm(y[c0:c1], W.t()), labels[c0:c1], scale)
+            tot = rows.sum() if tot is None else tot + rows.sum()
+        return (tot * scale).float()
 
     def _ce_chunk(self, logits, labels, scale):
         """Cross-entropy of one row chunk: loss rows (fp32); ``logits`` now hold dlogits."""
@@ -453,7 +471,7 @@ class Llama:
                 torch.mm(logits, W, out=dy[c0:c1])
             self._mm_into(self.G("lm_head"), logits.t(), yc, accumulate or c0 > 0)
             del logits, rows
-        loss.add_(tot * scale)
+        loss.copy_(tot * scale)
         del Wt
         dy = self._reduce_out(dy)
         self._ready(self.mats, "lm_head")
@@ -492,7 +510,9 @@ class Llama:
 
     def stage_forward(self, inp, B: int, S: int, labels=None, scale: float = 1.0):
         """inp: tokens [B*S] (first stage) or activation [B*S, H].  Returns (out, ctx) where
-        out is the loss (last stage) or the activation handed to the next stage."""
+        out is the loss (last stage) or the activation handed to the next stage.  The last
+        stage's loss is computed by :meth:`stage_backward` (K5 fuses it with the head's
+        gradient) and is NaN until then; :meth:`forward_loss` is the forward-only form."""
         ctx = {"layers": []}
         if self._sp:
             assert (B * S) % self.tp == 0, f"sequence parallelism needs B*S divisible by tp ({B}x{S}, tp {self.tp})"
@@ -551,6 +571,14 @@ class Llama:
         loss, ctx = self.stage_forward(tokens.reshape(-1), B, S, labels.reshape(-1), scale)
         self.stage_backward(ctx, None, B, S, accumulate)
         return loss
+
+    @torch.no_grad()
+    def forward_loss(self, tokens: torch.Tensor, labels: torch.Tensor, scale: Optional[float] = None):
+        """Mean next-token loss of tokens/labels [B, S] with no backward pass (evaluation)."""
+        B, S = tokens.shape
+        scale = scale if scale is not None else 1.0 / (B * S)
+        _, ctx = self.stage_forward(tokens.reshape(-1), B, S, labels.reshape(-1), scale)
+        return self.head_loss(ctx["head"])
 
     @torch.no_grad()
     def forward_logits(self, tokens: torch.Tensor) -> torch.Tensor:

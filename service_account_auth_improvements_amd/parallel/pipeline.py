@@ -198,6 +198,7 @@ class PipelineTrainer:
         if self.model.sequence_parallel and st.tp > 1:
             T //= st.tp                     # stages exchange this rank's block of token rows
         self.p2p = P2P(st, (T, mcfg.hidden), torch.bfloat16, st.device)
+        self.step_idx = 0          # optimizer steps taken (restored by load_checkpoint)
 
     def _hook(self, on: bool):
         self.model.on_grad_ready = self.reducer.grad_ready if on else None
@@ -208,4 +209,5 @@ class PipelineTrainer:
         loss = one_f_one_b(self.model, self.p2p, micro_batches, 1.0 / ntok, self._hook, reducer=self.reducer)
         self.reducer.finish()
         self.opt.step(grad_scale=1.0 / self.st.dp)
+        self.step_idx += 1
         return loss

@@ -68,7 +68,8 @@ def test_rope(T, S, Hq, Hkv, D):
     assert _rel(x, xr) < 1e-2
 
 
-@pytest.mark.parametrize("rows,F", [(17, 14336), (256, 512), (3, 8)])
+# rows > 65535 take the grid-stride kernels (the row-tiled ones cover <= 65535 rows per grid y)
+@pytest.mark.parametrize("rows,F", [(17, 14336), (256, 512), (3, 8), (65536, 16), (70001, 8)])
 def test_swiglu(rows, F):
     torch.manual_seed(2)
     gu = torch.randn(rows, 2 * F, device=DEV, dtype=torch.bfloat16) * 3

@@ -87,3 +87,23 @@ def test_chunked_lm_head_matches_unchunked(tp_vocab):
         assert abs(res[chunk][0] - res[0][0]) < 1e-5 * res[0][0]
         for a, b in zip(res[chunk][1:], res[0][1:]):
             assert ((a - b).abs().max() / b.abs().max()).item() < 1e-2
+
+
+def test_loss_before_backward_is_not_a_silent_zero_and_forward_loss_matches():
+    """K5 fuses the loss with the head's backward: the stage's loss tensor is NaN until
+    stage_backward fills it, and forward_loss gives the same value with no backward."""
+    import math
+    from service_account_auth_improvements_amd.models.llama import Llama, LlamaConfig
+    from service_account_auth_improvements_amd.parallel.state import ParallelState
+    cfg = LlamaConfig.preset("tiny")
+    m = Llama(cfg, ParallelState(), device="cpu").allocate()
+    m.head_chunk = 16                       # several chunks
+    g = torch.Generator().manual_seed(3)
+    tok = torch.randint(0, cfg.vocab_size, (2, 32), generator=g)
+    lab = torch.randint(0, cfg.vocab_size, (2, 32), generator=g)
+    loss, ctx = m.stage_forward(tok.reshape(-1), 2, 32, lab.reshape(-1), 1.0 / 64)
+    assert math.isnan(float(loss))
+    m.stage_backward(ctx, None, 2, 32, accumulate=False)
+    trained = float(loss)
+    assert math.isfinite(trained) and trained > 0
+    assert abs(float(m.forward_loss(tok, lab)) - trained) < 1e-5 * trained
