@@ -35,7 +35,7 @@ import torch.nn.functional as F
 from .. import ops
 from ..ops.attention import attention_bwd, attention_fwd
 from ..parallel import context as cpx
-from ..parallel.state import (ParallelState, get_state, tp_all_gather_rows, tp_all_reduce,
+from ..parallel.state import (ParallelState, _chunk_rows, get_state, tp_all_gather_rows, tp_all_reduce,
                               tp_reduce_scatter_rows)
 
 # KFAMD_DX_T=0 runs the activation-gradient GEMMs on the untransposed weights (A/B switch)
@@ -154,6 +154,11 @@ class Llama:
         # row-parallel one -- the same bytes per layer, 1/tp of the norm/residual activations
         self.sequence_parallel = False
         self._sp_norm_parts: list = []
+        # TP communication chunks: each row-parallel GEMM (wo, wd) runs in this many token
+        # chunks, chunk k's all-reduce / SP reduce-scatter on the wire while chunk k+1
+        # multiplies, and under SP each column-parallel GEMM (wqkv, wgu) multiplies chunk k
+        # while the all-gather of chunk k+1 is in flight (parallel/state.py row layout)
+        self.tp_comm_chunks = 4 if tp > 1 else 1
         # context parallelism (parallel/context.py): this rank holds 1/cp of every sequence's
         # tokens; attention runs on all tokens for 1/cp of the heads between two all-to-alls
         self.cp, self.cp_rank, self.cp_group = 1, 0, None
@@ -262,31 +267,74 @@ class Llama:
 
     def _gather(self, x):
         """SP: this rank's token rows -> all rows (identity without SP)."""
-        return tp_all_gather_rows(x, self.st) if self._sp else x
+        return tp_all_gather_rows(x, self.st, self.tp_comm_chunks) if self._sp else x
 
     def _reduce_out(self, x):
         """Partial sums of a row-parallel product: SP -> this rank's rows (reduce-scatter),
         else all rows (all-reduce; a no-op at tp 1)."""
-        return tp_reduce_scatter_rows(x, self.st) if self._sp else tp_all_reduce(x, self.st)
+        return tp_reduce_scatter_rows(x, self.st, self.tp_comm_chunks) if self._sp else tp_all_reduce(x, self.st)
 
     def _reduce_out_async(self, x):
         """:meth:`_reduce_out` launched asynchronously on the TP communicator's stream; returns
-        (result, handle) -- :meth:`_finish` makes the compute stream wait for it.  The backward
-        overlaps its input-gradient reductions with the weight-gradient GEMMs that do not need
-        them (at TP=8 over xGMI each all-reduce costs several times its producing GEMM)."""
+        (result, handles) -- :meth:`_finish` makes the compute stream wait for them.  The
+        backward overlaps its input-gradient reductions with the weight-gradient GEMMs that do
+        not need them (at TP=8 over xGMI each all-reduce costs several times its producing GEMM)."""
         if self.tp == 1:
-            return x, None
+            return x, []
         if self._sp:
-            out = torch.empty((x.shape[0] // self.tp,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
-            return out, dist.reduce_scatter_tensor(out, x.contiguous(), group=self.st.tp_group, async_op=True)
-        return x, dist.all_reduce(x, group=self.st.tp_group, async_op=True)
+            return tp_reduce_scatter_rows(x, self.st, self.tp_comm_chunks, async_op=True)
+        return x, [dist.all_reduce(x, group=self.st.tp_group, async_op=True)]
 
     @staticmethod
     def _finish(pending):
-        y, work = pending
-        if work is not None:
-            work.wait()
+        y, works = pending
+        for w in works:
+            w.wait()
         return y
+
+    def _row_parallel(self, x, W):
+        """Forward of a row-parallel projection: (x W^T) reduced over the TP group, in
+        ``tp_comm_chunks`` token chunks so the reduction of chunk k overlaps the GEMM of chunk
+        k+1 (each chunk's rows are complete products: the same values as one big GEMM)."""
+        T = x.shape[0]
+        c = _chunk_rows(T, self.tp_comm_chunks, self.tp)
+        if self.tp == 1 or c == 1:
+            return self._reduce_out(torch.mm(x, W.t()))
+        n, tp, g = T // c, self.tp, self.st.tp_group
+        works, keep = [], []
+        if self._sp:
+            out = torch.empty((T // tp, W.shape[0]), dtype=x.dtype, device=x.device)
+            for k in range(c):
+                yk = torch.mm(x[k * n:(k + 1) * n], W.t())
+                keep.append(yk)               # alive until its reduce-scatter has run
+                works.append(dist.reduce_scatter_tensor(out[k * n // tp:(k + 1) * n // tp], yk, group=g,
+                                                        async_op=True))
+        else:
+            out = torch.empty((T, W.shape[0]), dtype=x.dtype, device=x.device)
+            for k in range(c):
+                torch.mm(x[k * n:(k + 1) * n], W.t(), out=out[k * n:(k + 1) * n])
+                works.append(dist.all_reduce(out[k * n:(k + 1) * n], group=g, async_op=True))
+        for w in works:
+            w.wait()
+        return out
+
+    def _col_parallel(self, a, W):
+        """Forward of a column-parallel projection on the SP-gathered input: chunk k's GEMM
+        starts as soon as chunk k's all-gather has landed, while the later chunks are still on
+        the wire.  Without SP the input is already complete: one GEMM."""
+        if not self._sp:
+            return torch.mm(a, W.t())
+        full, works = tp_all_gather_rows(a, self.st, self.tp_comm_chunks, async_op=True)
+        c = len(works)
+        if c == 1:
+            works[0].wait()
+            return torch.mm(full, W.t())
+        n = full.shape[0] // c
+        out = torch.empty((full.shape[0], W.shape[0]), dtype=a.dtype, device=a.device)
+        for k in range(c):
+            works[k].wait()
+            torch.mm(full[k * n:(k + 1) * n], W.t(), out=out[k * n:(k + 1) * n])
+        return out
 
     def _norm_bwd(self, dy, h, rstd, name: str, accumulate: bool, dres=None):
         """K1 backward.  Under SP each rank sees 1/tp of the rows, so the norm weight gradient
@@ -326,7 +374,7 @@ class Llama:
         cfg = self.cfg
         c = _LayerCtx()
         a, h1, rstd1 = ops.rmsnorm_fwd(r, self.P(f"l{i}.norm1"), cfg.norm_eps, residual=d)
-        qkv = torch.mm(self._gather(a), self.P(f"l{i}.wqkv").t())
+        qkv = self._col_parallel(a, self.P(f"l{i}.wqkv"))
         D, cp = cfg.head_dim, self.cp
         hq, hkv, Sa = self.hq // cp, self.hkv // cp, S * cp
         if cp > 1:   # own tokens x all heads -> all tokens x own head group
@@ -334,12 +382,12 @@ class Llama:
         ops.rope_(qkv, hq + hkv, D, self.cos, self.sin, seq_len=Sa)
         o, lse = attention_fwd(qkv, B, Sa, hq, hkv, D)
         o_tok = cpx.to_tokens(o, B, S, [hq * D], cp, self.cp_group) if cp > 1 else o
-        da = self._reduce_out(torch.mm(o_tok, self.P(f"l{i}.wo").t()))
+        da = self._row_parallel(o_tok, self.P(f"l{i}.wo"))
         m, h2, rstd2 = ops.rmsnorm_fwd(h1, self.P(f"l{i}.norm2"), cfg.norm_eps, residual=da)
         del da
-        gu = torch.mm(self._gather(m), self.P(f"l{i}.wgu").t())
+        gu = self._col_parallel(m, self.P(f"l{i}.wgu"))
         s = ops.swiglu_fwd(gu)
-        dm = self._reduce_out(torch.mm(s, self.P(f"l{i}.wd").t()))
+        dm = self._row_parallel(s, self.P(f"l{i}.wd"))
         c.h1, c.rstd1, c.a, c.qkv, c.o, c.o_tok, c.lse = h1, rstd1, a, qkv, o, o_tok, lse
         c.h2, c.rstd2, c.m, c.gu, c.s = h2, rstd2, m, gu, s
         return h2, dm, c

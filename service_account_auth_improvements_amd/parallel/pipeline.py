@@ -182,6 +182,8 @@ class PipelineTrainer:
         self.model.recompute = tcfg.recompute
         self.model.head_chunk = getattr(tcfg, "head_chunk", self.model.head_chunk)
         self.model.sequence_parallel = getattr(tcfg, "sequence_parallel", False)
+        if self.st.tp > 1:
+            self.model.tp_comm_chunks = getattr(tcfg, "tp_comm_chunks", self.model.tp_comm_chunks)
         assert not getattr(tcfg, "context_parallel", False), "context parallelism is not combined with PP"
         self.model.allocate()
         self.reducer = GradReducer(self.model.groups, st.dp_group, st.dp,

@@ -127,26 +127,50 @@ def tp_all_reduce(x: torch.Tensor, st: Optional[ParallelState] = None) -> torch.
     return x
 
 
-def tp_all_gather_rows(x: torch.Tensor, st: Optional[ParallelState] = None) -> torch.Tensor:
-    """Sequence parallelism: this rank's contiguous block of token rows -> all rows (rank order)."""
+def _chunk_rows(n: int, chunks: int, tp: int) -> int:
+    """The chunk count actually used for ``n`` rows: ``chunks`` when every chunk splits evenly
+    over the TP ranks, else 1 (so one model always uses one layout for a given token count)."""
+    return chunks if chunks > 1 and n % (chunks * tp) == 0 else 1
+
+
+def tp_all_gather_rows(x: torch.Tensor, st: Optional[ParallelState] = None, chunks: int = 1,
+                       async_op: bool = False):
+    """Sequence parallelism: this rank's token rows -> all rows.
+
+    Row layout with ``chunks`` = c: the global rows are c consecutive chunks and each rank holds
+    the r-th 1/tp block of every chunk (c = 1: one contiguous block per rank, rank order).  The
+    matching :func:`tp_reduce_scatter_rows` produces exactly this layout, so a model that uses
+    one c for both everywhere (its residual stream, norms, pipeline hand-offs) is consistent,
+    and the chunked form lets a GEMM consume chunk k while chunk k+1 is still on the wire.
+    ``async_op``: returns (out, [work per chunk]) -- ``work[k].wait()`` before reading chunk k."""
     st = st or get_state()
     if st.tp == 1:
-        return x
+        return (x, []) if async_op else x
+    c = _chunk_rows(x.shape[0] * st.tp, chunks, st.tp)
     out = torch.empty((x.shape[0] * st.tp,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
-    dist.all_gather_into_tensor(out, x.contiguous(), group=st.tp_group)
-    return out
+    x = x.contiguous()
+    n = x.shape[0] // c
+    works = [dist.all_gather_into_tensor(out[k * n * st.tp:(k + 1) * n * st.tp], x[k * n:(k + 1) * n],
+                                         group=st.tp_group, async_op=async_op) for k in range(c)]
+    return (out, works) if async_op else out
 
 
-def tp_reduce_scatter_rows(x: torch.Tensor, st: Optional[ParallelState] = None) -> torch.Tensor:
-    """Sequence parallelism: partial sums over all token rows -> this rank's block of summed rows
-    (replaces the all-reduce after a row-parallel GEMM: same result rows, half the bytes)."""
+def tp_reduce_scatter_rows(x: torch.Tensor, st: Optional[ParallelState] = None, chunks: int = 1,
+                           async_op: bool = False):
+    """Sequence parallelism: partial sums over all token rows -> this rank's summed rows in the
+    layout of :func:`tp_all_gather_rows` (replaces the all-reduce after a row-parallel GEMM:
+    same result rows, half the bytes).  ``async_op``: returns (out, [work per chunk])."""
     st = st or get_state()
     if st.tp == 1:
-        return x
+        return (x, []) if async_op else x
     assert x.shape[0] % st.tp == 0, (x.shape, st.tp)
+    c = _chunk_rows(x.shape[0], chunks, st.tp)
     out = torch.empty((x.shape[0] // st.tp,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
-    dist.reduce_scatter_tensor(out, x.contiguous(), group=st.tp_group)
-    return out
+    x = x.contiguous()
+    n = x.shape[0] // c
+    works = [dist.reduce_scatter_tensor(out[k * n // st.tp:(k + 1) * n // st.tp], x[k * n:(k + 1) * n],
+                                        group=st.tp_group, async_op=async_op) for k in range(c)]
+    return (out, works) if async_op else out
 
 
 def barrier():

@@ -49,6 +49,9 @@ class TrainConfig:
     # context parallelism (parallel/context.py): the DP group becomes ONE context-parallel group --
     # its ranks share the same sequences, each holding 1/dp of every sequence's tokens
     context_parallel: bool = False
+    # TP forward communication overlap: token chunks per row-/column-parallel projection
+    # (models/llama.py _row_parallel / _col_parallel); 1 = one GEMM + one blocking collective
+    tp_comm_chunks: int = 4
 
 
 class Trainer:
@@ -68,6 +71,8 @@ class Trainer:
         self.model.recompute = tcfg.recompute
         self.model.head_chunk = tcfg.head_chunk
         self.model.sequence_parallel = tcfg.sequence_parallel
+        if self.st.tp > 1:
+            self.model.tp_comm_chunks = getattr(tcfg, "tp_comm_chunks", self.model.tp_comm_chunks)
         self.cp = self.st.dp if tcfg.context_parallel else 1
         if self.cp > 1:
             self.model.set_context_parallel(self.st.dp_group, self.st.dp, self.st.dp_rank)

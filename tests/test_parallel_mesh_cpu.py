@@ -170,3 +170,30 @@ def test_fp32_microbatch_accumulation():
         assert _rel(tr.reduced_grads(tr.model.mats), exact) <= errs[mode] * 1.0001 + 1e-12
     assert errs["fp32"] < 1e-6, errs
     assert errs["fp32"] < errs["bf16"], errs
+
+
+# ------------------------------------------------------------------ TP forward overlap
+def _chunk_body(rank, world, chunks, sp):
+    from service_account_auth_improvements_amd.parallel.state import init_distributed
+    from service_account_auth_improvements_amd.runtime.trainer import TrainConfig, Trainer
+    st = init_distributed(tp=world, pp=1, device="cpu")
+    tr = Trainer(TrainConfig(model="tiny", seq_len=32, micro_batch=2, n_layers=2, lr=LR, sequence_parallel=sp,
+                             tp_comm_chunks=chunks), st, full_init=True)
+    assert tr.model.tp_comm_chunks == chunks
+    losses = [float(tr.train_step(_batches(tr.mcfg.vocab_size, 1, seed=500 + s))) for s in range(STEPS)]
+    return dict(losses=losses, params={s.name: tr.model.P(s.name).float() for g in tr.model.groups
+                                       for s in g.specs})
+
+
+@pytest.mark.parametrize("sp", [False, True], ids=["tp2", "tp2+sp"])
+def test_tp_chunked_forward_overlap_is_bit_identical(sp):
+    """Row-parallel GEMMs in 4 token chunks with each chunk's all-reduce / reduce-scatter in
+    flight behind the next chunk's GEMM (and, under SP, chunked all-gathers feeding the
+    column-parallel GEMMs) give bit-identical losses and parameters to one GEMM + one blocking
+    collective (two ranks: the reduction order of a sum of two is fixed)."""
+    one = run_ranks(_chunk_body, world=2, args=(1, sp))
+    four = run_ranks(_chunk_body, world=2, args=(4, sp))
+    for a, b in zip(one, four):
+        assert a["losses"] == b["losses"]
+        for name in a["params"]:
+            assert torch.equal(a["params"][name], b["params"][name]), name

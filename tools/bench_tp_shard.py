@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--recompute", action="store_true")
+    ap.add_argument("--tp-comm-chunks", type=int, default=4,
+                    help="token chunks per TP projection (forward comm/compute overlap; 1 = off)")
     ap.add_argument("--busbw-gbs", type=float, default=300.0,
                     help="assumed RCCL all-reduce bus bandwidth over xGMI for the wire-time estimate")
     a = ap.parse_args()
@@ -53,7 +55,8 @@ def main():
     st = ParallelState(world_size=1, rank=0, tp=a.tp, tp_rank=0, device=dev, backend="nccl")
     set_state(st)
     t0 = time.time()
-    tr = Trainer(TrainConfig(model=a.model, seq_len=a.seq_len, micro_batch=a.micro_batch, recompute=a.recompute), st)
+    tr = Trainer(TrainConfig(model=a.model, seq_len=a.seq_len, micro_batch=a.micro_batch, recompute=a.recompute,
+                                 tp_comm_chunks=a.tp_comm_chunks), st)
     torch.cuda.synchronize()
     init_s = time.time() - t0
     data = SyntheticData(tr.mcfg.vocab_size, a.micro_batch, a.seq_len, dev, seed=1)
@@ -77,7 +80,8 @@ def main():
     flops = c.flops_per_token(a.seq_len) * T / a.tp
     print(json.dumps({"what": f"one TP={a.tp} rank's share of a {a.model} step (collectives are one-rank copies)",
                       "seq_len": a.seq_len, "micro_batch": a.micro_batch, "n_layers": c.n_layers,
-                      "recompute": a.recompute, "ms_per_step_compute": round(ms, 1),
+                      "recompute": a.recompute, "tp_comm_chunks": a.tp_comm_chunks,
+                      "ms_per_step_compute": round(ms, 1),
                       "model_tflops_per_gpu": round(flops / (ms / 1e3) / 1e12, 1),
                       "tokens_per_s_per_tp_group_compute_bound": round(tok_s, 1),
                       "tp_allreduce_wire_ms_est": round(wire_ms, 1), "assumed_busbw_GBps": a.busbw_gbs,
