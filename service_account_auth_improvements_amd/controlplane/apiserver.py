@@ -192,6 +192,31 @@ def _check_schema(v, sch: dict, path: str, errs: List[str]):
             _check_schema(x, sch["items"], f"{path}[{i}]", errs)
 
 
+def _prune_unknown(v, sch: dict, path: str, found: List[str]):
+    """Structural-schema pruning (apiextensions.k8s.io/v1): drop, in place, every object field
+    the schema does not declare, and record its path.  Objects that preserve unknown fields,
+    maps (``additionalProperties``) and schema-less objects (``type: object`` alone) keep
+    everything."""
+    if not isinstance(sch, dict) or sch.get("x-kubernetes-preserve-unknown-fields"):
+        return
+    if isinstance(v, dict):
+        props = sch.get("properties")
+        extra = sch.get("additionalProperties")
+        if props is None and not isinstance(extra, dict):
+            return
+        for k in list(v):
+            if props is not None and k in props:
+                _prune_unknown(v[k], props[k], f"{path}.{k}", found)
+            elif isinstance(extra, dict):
+                _prune_unknown(v[k], extra, f"{path}.{k}", found)
+            else:
+                found.append(f"{path}.{k}")
+                del v[k]
+    elif isinstance(v, list) and isinstance(sch.get("items"), dict):
+        for i, x in enumerate(v):
+            _prune_unknown(x, sch["items"], f"{path}[{i}]", found)
+
+
 def split_api_version(api_version: str) -> Tuple[str, str]:
     if "/" in api_version:
         g, v = api_version.split("/", 1)
@@ -431,6 +456,9 @@ class APIServer:
 
     def __init__(self, types: Optional[List[ResourceType]] = None, history: Optional[int] = None):
         self._lock = threading.RLock()
+        # unknown CRD fields when a request does not say (kube-apiserver's default): pruned
+        # ("Warn"/"Ignore"); "Strict" rejects them
+        self.field_validation = "Warn"
         self._types: Dict[Tuple[str, str], ResourceType] = {}
         self._by_plural: Dict[Tuple[str, str], ResourceType] = {}
         for t in (types or BUILTIN_TYPES):
@@ -470,7 +498,10 @@ class APIServer:
         self._schemas[(sp["group"], names["kind"])] = {
             v["name"]: (v.get("schema") or {}).get("openAPIV3Schema") for v in vers}
 
-    def _validate_schema(self, t: ResourceType, obj: dict):
+    def _validate_schema(self, t: ResourceType, obj: dict, field_validation: Optional[str] = None):
+        """CRD schema validation.  Fields the structural schema does not declare are pruned
+        (as kube-apiserver does); with ``fieldValidation=Strict`` (kubectl's default) they are an
+        error instead, so a misspelt field is reported rather than dropped."""
         schemas = self._schemas.get((t.group, t.kind))
         if not schemas:
             return
@@ -479,6 +510,19 @@ class APIServer:
         if not sch:
             return
         errs: List[str] = []
+        unknown: List[str] = []
+        for k in list(obj):
+            if k in ("metadata", "apiVersion", "kind"):
+                continue
+            if k not in (sch.get("properties") or {}):
+                if not sch.get("x-kubernetes-preserve-unknown-fields"):
+                    unknown.append(f".{k}")
+                    del obj[k]
+                continue
+            _prune_unknown(obj[k], sch["properties"][k], f".{k}", unknown)
+        if unknown and (field_validation or self.field_validation) == "Strict":
+            raise Invalid(f'{t.kind}.{t.group} "{obj.get("metadata", {}).get("name")}" is invalid: strict decoding '
+                          "error: " + ", ".join(f'unknown field "{u[1:]}"' for u in unknown))
         body = {k: v for k, v in obj.items() if k not in ("metadata", "apiVersion", "kind")}
         _check_schema(body, {k: v for k, v in sch.items() if k != "properties"} | {
             "type": "object", "properties": {k: v for k, v in (sch.get("properties") or {}).items()
@@ -618,7 +662,8 @@ class APIServer:
         return obj
 
     # --- CRUD
-    def create(self, obj: dict, dry_run: bool = False, user: str = "system:admin") -> dict:
+    def create(self, obj: dict, dry_run: bool = False, user: str = "system:admin",
+               field_validation: Optional[str] = None) -> dict:
         obj = copy.deepcopy(obj)
         t = self.type_for(obj.get("apiVersion", ""), obj.get("kind", ""))
         meta = obj.setdefault("metadata", {})
@@ -647,7 +692,7 @@ class APIServer:
             if key in bucket:
                 raise AlreadyExists(f'{t.plural} "{meta["name"]}" already exists')
             obj = self._admit("CREATE", t, obj, None, dry_run, user)
-            self._validate_schema(t, obj)
+            self._validate_schema(t, obj, field_validation)
             if t.kind == "CustomResourceDefinition" and not dry_run:
                 self._register_crd(obj)
             meta = obj["metadata"]
@@ -690,7 +735,8 @@ class APIServer:
             o["apiVersion"] = api_version if "/" in api_version or not t.group else t.api_version()
         return items
 
-    def _write(self, t, cur, new, status_only: bool, dry_run: bool, user: str):
+    def _write(self, t, cur, new, status_only: bool, dry_run: bool, user: str,
+               field_validation: Optional[str] = None):
         meta, cmeta = new.setdefault("metadata", {}), cur["metadata"]
         rv = meta.get("resourceVersion")
         if rv and rv != cmeta["resourceVersion"]:
@@ -714,7 +760,7 @@ class APIServer:
                 else:
                     out.pop("status", None)
             out = self._admit("UPDATE", t, out, cur, dry_run, user)
-            self._validate_schema(t, out)
+            self._validate_schema(t, out, field_validation)
             if t.kind == "CustomResourceDefinition" and not dry_run:
                 self._register_crd(out)
             strip = lambda o: {k: v for k, v in o.items() if k not in ("metadata", "status", "apiVersion")}  # noqa
@@ -737,14 +783,15 @@ class APIServer:
         self._emit("MODIFIED", t, out)
         return copy.deepcopy(out)
 
-    def update(self, obj: dict, dry_run: bool = False, user: str = "system:admin") -> dict:
+    def update(self, obj: dict, dry_run: bool = False, user: str = "system:admin",
+               field_validation: Optional[str] = None) -> dict:
         t = self.type_for(obj.get("apiVersion", ""), obj.get("kind", ""))
         meta = obj.get("metadata", {})
         with self._lock:
             cur = self._bucket(t).get(self._key(t, meta.get("namespace"), meta.get("name")))
             if cur is None:
                 raise NotFound(f'{t.plural} "{meta.get("name")}" not found')
-            return self._write(t, cur, copy.deepcopy(obj), False, dry_run, user)
+            return self._write(t, cur, copy.deepcopy(obj), False, dry_run, user, field_validation)
 
     def update_status(self, obj: dict) -> dict:
         t = self.type_for(obj.get("apiVersion", ""), obj.get("kind", ""))
@@ -776,6 +823,7 @@ class APIServer:
 
     def patch(self, api_version: str, kind: str, name: str, namespace: Optional[str], patch,
               patch_type: str = "merge", subresource: Optional[str] = None, dry_run: bool = False,
+              field_validation: Optional[str] = None,
               user: str = "system:admin") -> dict:
         t = self.type_for(api_version, kind)
         with self._lock:
@@ -787,7 +835,8 @@ class APIServer:
             else:  # merge / strategic-merge treated as JSON merge patch
                 new = merge_patch(cur, patch)
             new["metadata"]["resourceVersion"] = cur["metadata"]["resourceVersion"]
-            return self._write(t, cur, new, subresource == "status" and t.status_subresource, dry_run, user)
+            return self._write(t, cur, new, subresource == "status" and t.status_subresource, dry_run, user,
+                               field_validation)
 
     def delete(self, api_version: str, kind: str, name: str, namespace: Optional[str] = None,
                propagation: str = "Background", dry_run: bool = False) -> dict:

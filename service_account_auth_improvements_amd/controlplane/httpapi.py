@@ -73,6 +73,7 @@ def make_handler(server: APIServer):
                 t = server.type_for_plural(g, plural)
                 av = f"{g}/{v}" if g else v
                 dry = q.get("dryRun") == "All"
+                fv = q.get("fieldValidation")       # Strict | Warn | Ignore (unknown CRD fields)
                 if method == "GET" and q.get("watch") in ("true", "1"):
                     return self._watch(av, t.kind, ns, q.get("resourceVersion"),
                                        q.get("allowWatchBookmarks") in ("true", "1"),
@@ -92,16 +93,17 @@ def make_handler(server: APIServer):
                     body.setdefault("kind", t.kind)
                     if ns:
                         body.setdefault("metadata", {}).setdefault("namespace", ns)
-                    return self._send(201, server.create(body, dry_run=dry))
+                    return self._send(201, server.create(body, dry_run=dry, field_validation=fv))
                 if method == "PUT":
                     body = self._body()
                     if sub == "status":
                         return self._send(200, server.update_status(body))
-                    return self._send(200, server.update(body, dry_run=dry))
+                    return self._send(200, server.update(body, dry_run=dry, field_validation=fv))
                 if method == "PATCH":
                     ct = self.headers.get("Content-Type", "")
                     pt = "json" if "json-patch" in ct else "merge"
-                    return self._send(200, server.patch(av, t.kind, name, ns, self._body(), pt, sub, dry))
+                    return self._send(200, server.patch(av, t.kind, name, ns, self._body(), pt, sub, dry,
+                                                        field_validation=fv))
                 if method == "DELETE":
                     body = self._body() or {}
                     return self._send(200, server.delete(av, t.kind, name, ns,

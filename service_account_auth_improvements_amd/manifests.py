@@ -32,6 +32,14 @@ PKG = "service_account_auth_improvements_amd"
 IMAGE_PREFIX = "kfamd"
 TAG = "latest"
 
+class NoAliasDumper(yaml.SafeDumper):
+    """Plain YAML: a schema node reused in several places is written out each time, never as an
+    ``&anchor`` / ``*alias`` pair (manifest tools and kustomize patches edit nodes in place)."""
+
+    def ignore_aliases(self, data):
+        return True
+
+
 # ------------------------------------------------------------------ schema helpers
 OBJ_ANY = {"type": "object", "x-kubernetes-preserve-unknown-fields": True}
 
@@ -67,84 +75,34 @@ def open_obj(props=None, required=None):
     return o
 
 
-# ---- core/v1 PodSpec subset (k8s.io/api/core/v1 types the controllers and web apps read)
-KEY_REF = open_obj({"name": STR, "key": STR, "optional": BOOL}, ["key"])
-ENV_VAR = open_obj({"name": STR, "value": STR,
-                    "valueFrom": open_obj({"configMapKeyRef": KEY_REF, "secretKeyRef": KEY_REF,
-                                           "fieldRef": open_obj({"fieldPath": STR, "apiVersion": STR},
-                                                                ["fieldPath"]),
-                                           "resourceFieldRef": open_obj({"resource": STR, "containerName": STR,
-                                                                         "divisor": INT_OR_STR}, ["resource"])})},
-                   ["name"])
-ENV_FROM = open_obj({"prefix": STR, "configMapRef": open_obj({"name": STR, "optional": BOOL}),
-                     "secretRef": open_obj({"name": STR, "optional": BOOL})})
-RESOURCES = open_obj({"limits": QUANTITY_MAP, "requests": QUANTITY_MAP})
-CONTAINER_PORT = open_obj({"containerPort": {"type": "integer", "minimum": 1}, "name": STR, "hostPort": INT,
-                           "protocol": {"type": "string", "enum": ["TCP", "UDP", "SCTP"]}}, ["containerPort"])
-VOLUME_MOUNT = open_obj({"name": STR, "mountPath": STR, "subPath": STR, "readOnly": BOOL,
-                         "mountPropagation": STR}, ["name", "mountPath"])
-PROBE = open_obj({"httpGet": open_obj({"path": STR, "port": INT_OR_STR, "scheme": STR}, ["port"]),
-                  "tcpSocket": open_obj({"port": INT_OR_STR}, ["port"]),
-                  "exec": open_obj({"command": arr(STR)}),
-                  "initialDelaySeconds": INT, "periodSeconds": INT, "timeoutSeconds": INT,
-                  "failureThreshold": INT, "successThreshold": INT})
-SECURITY_CONTEXT = open_obj({"runAsUser": INT, "runAsGroup": INT, "runAsNonRoot": BOOL, "privileged": BOOL,
-                             "allowPrivilegeEscalation": BOOL, "readOnlyRootFilesystem": BOOL})
+# ---- core/v1 types: full structural schemas (corev1.py), no preserve-unknown holes
+from . import corev1 as _core  # noqa: E402
+
+ENV_VAR = _core.schema("EnvVar")
+ENV_FROM = _core.schema("EnvFromSource")
+VOLUME = _core.schema("Volume")
+VOLUME_MOUNT = _core.schema("VolumeMount")
+TOLERATION = _core.schema("Toleration")
+AFFINITY = _core.schema("Affinity")
+RESOURCES = _core.schema("ResourceRequirements")
+LABEL_SELECTOR = _core.schema("LabelSelector")
+LOCAL_REF = _core.schema("LocalObjectReference")
+container = _core.container
+pod_spec = _core.pod_spec
 
 
-def container(required=("name",)):
-    return open_obj({"name": STR, "image": STR, "command": arr(STR), "args": arr(STR), "workingDir": STR,
-                     "env": arr(ENV_VAR), "envFrom": arr(ENV_FROM), "ports": arr(CONTAINER_PORT),
-                     "resources": RESOURCES, "volumeMounts": arr(VOLUME_MOUNT),
-                     "imagePullPolicy": {"type": "string", "enum": ["Always", "Never", "IfNotPresent"]},
-                     "livenessProbe": PROBE, "readinessProbe": PROBE, "startupProbe": PROBE,
-                     "securityContext": SECURITY_CONTEXT, "stdin": BOOL, "tty": BOOL}, list(required))
+def _fresh(x):
+    """A deep copy, so no two places of a generated CRD share one dict (alias-free YAML)."""
+    return copy.deepcopy(x)
 
 
-VOLUME = open_obj({"name": STR,
-                   "persistentVolumeClaim": open_obj({"claimName": STR, "readOnly": BOOL}, ["claimName"]),
-                   "emptyDir": open_obj({"medium": STR, "sizeLimit": INT_OR_STR}),
-                   "configMap": open_obj({"name": STR, "defaultMode": INT, "optional": BOOL, "items": arr(OBJ_ANY)}),
-                   "secret": open_obj({"secretName": STR, "defaultMode": INT, "optional": BOOL,
-                                       "items": arr(OBJ_ANY)}),
-                   "hostPath": open_obj({"path": STR, "type": STR}, ["path"]),
-                   "csi": open_obj({"driver": STR}, ["driver"])}, ["name"])
-TOLERATION = open_obj({"key": STR, "operator": {"type": "string", "enum": ["Exists", "Equal"]}, "value": STR,
-                       "effect": {"type": "string", "enum": ["NoSchedule", "PreferNoSchedule", "NoExecute", ""]},
-                       "tolerationSeconds": INT})
-NODE_SELECTOR_TERM = open_obj({"matchExpressions": arr(open_obj({"key": STR, "operator": STR, "values": arr(STR)},
-                                                                ["key", "operator"])),
-                               "matchFields": arr(OBJ_ANY)})
-AFFINITY = open_obj({
-    "nodeAffinity": open_obj({
-        "requiredDuringSchedulingIgnoredDuringExecution": open_obj({"nodeSelectorTerms": arr(NODE_SELECTOR_TERM)},
-                                                                   ["nodeSelectorTerms"]),
-        "preferredDuringSchedulingIgnoredDuringExecution": arr(open_obj({"weight": {"type": "integer", "minimum": 1},
-                                                                         "preference": NODE_SELECTOR_TERM},
-                                                                        ["weight", "preference"]))}),
-    "podAffinity": OBJ_ANY, "podAntiAffinity": OBJ_ANY})
-
-
-def pod_spec(containers_min=0, container_required=("name",)):
-    c = arr(container(container_required))
-    if containers_min:
-        c["minItems"] = containers_min
-    return open_obj({"containers": c, "initContainers": arr(container()), "volumes": arr(VOLUME),
-                     "tolerations": arr(TOLERATION), "affinity": AFFINITY, "nodeSelector": STR_MAP,
-                     "serviceAccountName": STR, "automountServiceAccountToken": BOOL,
-                     "imagePullSecrets": arr(open_obj({"name": STR})),
-                     "securityContext": open_obj({"fsGroup": INT, "runAsUser": INT, "runAsGroup": INT,
-                                                  "runAsNonRoot": BOOL, "supplementalGroups": arr(INT)}),
-                     "restartPolicy": {"type": "string", "enum": ["Always", "OnFailure", "Never"]},
-                     "hostIPC": BOOL, "hostNetwork": BOOL, "priorityClassName": STR, "schedulerName": STR,
-                     "terminationGracePeriodSeconds": INT})
-
-
-OBJECT_META = open_obj({"labels": STR_MAP, "annotations": STR_MAP, "name": STR, "namespace": STR})
+OBJECT_META = _core.schema("ObjectMeta")
 POD_TEMPLATE = obj({"metadata": OBJECT_META, "spec": pod_spec(containers_min=1)})
 REPLICA_SPEC = obj({"replicas": {"type": "integer", "minimum": 0},
                     "restartPolicy": {"type": "string", "enum": ["Always", "OnFailure", "Never", "ExitCode"]},
                     "template": POD_TEMPLATE})
+REPLICA_STATUS = obj({"active": INT, "succeeded": INT, "failed": INT, "labelSelector": LABEL_SELECTOR,
+                      "selector": STR})
 
 
 def crd(group, kind, plural, scope, versions, short=None, categories=None, printer=None):
@@ -173,17 +131,22 @@ def crds() -> Dict[str, dict]:
     # patches (containers minItems 1, name + image required per container)
     nb_spec = obj({"template": obj({"metadata": OBJECT_META,
                                     "spec": pod_spec(containers_min=1, container_required=("name", "image"))})})
-    nb_status = obj({"conditions": CONDITIONS, "readyReplicas": INT, "containerState": OBJ_ANY})
+    nb_status = obj({"conditions": CONDITIONS, "readyReplicas": INT, "containerState": _core.schema("ContainerState")})
     prof_spec = obj({"owner": obj({"kind": {"type": "string", "enum": ["User", "Group", "ServiceAccount"]},
                                    "name": STR, "apiGroup": STR, "namespace": STR}, ["kind", "name"]),
+                     # a plugin's spec is a runtime.RawExtension: its shape is the plugin's own
                      "plugins": arr(obj({"kind": STR, "spec": OBJ_ANY}, ["kind"])),
-                     "resourceQuotaSpec": OBJ_ANY}, ["owner"])
+                     "resourceQuotaSpec": obj({"hard": {"type": "object", "additionalProperties": INT_OR_STR},
+                                               "scopes": arr(STR),
+                                               "scopeSelector": obj({"matchExpressions": arr(obj(
+                                                   {"operator": STR, "scopeName": STR, "values": arr(STR)},
+                                                   ["operator", "scopeName"]))})})}, ["owner"])
     prof_status = obj({"conditions": CONDITIONS})
-    pd_spec = obj({"selector": open_obj({"matchLabels": STR_MAP, "matchExpressions": arr(OBJ_ANY)}), "desc": STR,
+    pd_spec = obj({"selector": LABEL_SELECTOR, "desc": STR,
                    "serviceAccountName": STR, "automountServiceAccountToken": BOOL, "env": arr(ENV_VAR),
                    "envFrom": arr(ENV_FROM), "volumes": arr(VOLUME), "volumeMounts": arr(VOLUME_MOUNT),
                    "initContainers": arr(container()), "sidecars": arr(container()), "tolerations": arr(TOLERATION),
-                   "imagePullSecrets": arr(open_obj({"name": STR})), "annotations": STR_MAP, "labels": STR_MAP,
+                   "imagePullSecrets": arr(LOCAL_REF), "annotations": STR_MAP, "labels": STR_MAP,
                    "args": arr(STR), "command": arr(STR)}, ["selector"])
     tb_spec = obj({"logspath": STR}, ["logspath"])
     tb_status = obj({"conditions": arr(obj({"deploymentState": STR, "lastProbeTime": STR})), "readyReplicas": INT})
@@ -195,8 +158,9 @@ def crds() -> Dict[str, dict]:
     run_policy = obj({"cleanPodPolicy": {"type": "string", "enum": ["All", "Running", "None"]},
                       "backoffLimit": {"type": "integer", "minimum": 0},
                       "activeDeadlineSeconds": INT, "ttlSecondsAfterFinished": INT})
-    job_status = obj({"conditions": CONDITIONS, "replicaStatuses": OBJ_ANY, "startTime": STR,
-                      "completionTime": STR, "lastReconcileTime": STR})
+    job_status = obj({"conditions": CONDITIONS,
+                      "replicaStatuses": {"type": "object", "additionalProperties": REPLICA_STATUS},
+                      "restartCount": INT, "startTime": STR, "completionTime": STR, "lastReconcileTime": STR})
     pt_spec = obj({"pytorchReplicaSpecs": obj({"Master": REPLICA_SPEC, "Worker": REPLICA_SPEC}),
                    "nprocPerNode": {"x-kubernetes-int-or-string": True}, "runPolicy": run_policy,
                    "elasticPolicy": obj({"minReplicas": INT, "maxReplicas": INT, "rdzvBackend": STR,
@@ -207,13 +171,23 @@ def crds() -> Dict[str, dict]:
                     "sshAuthMountPath": STR}, ["mpiReplicaSpecs"])
     isvc_spec = obj({"predictor": obj({"model": obj({"modelFormat": obj({"name": STR, "version": STR}, ["name"]),
                                                      "storageUri": STR, "runtime": STR, "args": arr(STR),
-                                                     "env": arr(OBJ_ANY), "resources": OBJ_ANY, "image": STR}),
-                                       "containers": arr(OBJ_ANY), "volumes": arr(OBJ_ANY),
+                                                     "command": arr(STR), "env": arr(ENV_VAR),
+                                                     "resources": RESOURCES, "image": STR,
+                                                     "protocolVersion": STR}),
+                                       "containers": arr(container()), "volumes": arr(VOLUME),
                                        "minReplicas": {"type": "integer", "minimum": 0}, "maxReplicas": INT,
-                                       "serviceAccountName": STR, "nodeSelector": OBJ_ANY,
-                                       "tolerations": arr(OBJ_ANY), "affinity": OBJ_ANY})}, ["predictor"])
-    isvc_status = obj({"conditions": CONDITIONS, "url": STR, "address": OBJ_ANY, "components": OBJ_ANY,
-                       "modelStatus": OBJ_ANY})
+                                       "serviceAccountName": STR, "nodeSelector": STR_MAP,
+                                       "tolerations": arr(TOLERATION), "affinity": AFFINITY,
+                                       "annotations": STR_MAP, "labels": STR_MAP})}, ["predictor"])
+    isvc_status = obj({"conditions": CONDITIONS, "url": STR,
+                       "address": obj({"url": STR}),
+                       "components": {"type": "object", "additionalProperties": obj(
+                           {"url": STR, "latestCreatedRevision": STR, "latestReadyRevision": STR,
+                            "address": obj({"url": STR})})},
+                       "modelStatus": obj({"states": obj({"activeModelState": STR, "targetModelState": STR}),
+                                           "transitionStatus": STR, "copies": obj({"failedCopies": INT,
+                                                                                    "totalCopies": INT})}),
+                       "observedGeneration": INT})
     age = [{"name": "Age", "type": "date", "jsonPath": ".metadata.creationTimestamp"}]
     return {
         "kubeflow.org_notebooks.yaml": crd("kubeflow.org", "Notebook", "notebooks", "Namespaced",
@@ -224,7 +198,7 @@ def crds() -> Dict[str, dict]:
                                           [("v1", True, True, prof_spec, prof_status),
                                            ("v1beta1", True, False, prof_spec, prof_status)]),
         "kubeflow.org_poddefaults.yaml": crd("kubeflow.org", "PodDefault", "poddefaults", "Namespaced",
-                                             [("v1alpha1", True, True, pd_spec, OBJ_ANY)]),
+                                             [("v1alpha1", True, True, pd_spec, obj({}))]),
         "kubeflow.org_pvcviewers.yaml": crd("kubeflow.org", "PVCViewer", "pvcviewers", "Namespaced",
                                             [("v1alpha1", True, True, pv_spec, pv_status)], printer=age),
         "tensorboard.kubeflow.org_tensorboards.yaml": crd("tensorboard.kubeflow.org", "Tensorboard", "tensorboards",
@@ -582,7 +556,8 @@ def generate(out_dir: str):
     os.makedirs(os.path.join(out_dir, "crds"), exist_ok=True)
     cs = crds()
     for fn, doc in cs.items():
-        _dump(os.path.join(out_dir, "crds", fn), [doc])
+        # compact: leaf schema nodes as one-line flow mappings ({type: string}), block elsewhere
+        _dump(os.path.join(out_dir, "crds", fn), [doc], flow=None)
     _dump(os.path.join(out_dir, "crds", "kustomization.yaml"),
           [{"apiVersion": "kustomize.config.k8s.io/v1beta1", "kind": "Kustomization", "resources": sorted(cs)}])
     for comp, files in components().items():
@@ -608,10 +583,10 @@ def generate(out_dir: str):
               [dict({"apiVersion": "kustomize.config.k8s.io/v1beta1", "kind": "Kustomization"}, **k)])
 
 
-def _dump(path, docs):
+def _dump(path, docs, flow=False):
     with open(path, "w") as f:
         f.write("# Generated by `python -m service_account_auth_improvements_amd.manifests generate`; do not edit.\n")
-        yaml.safe_dump_all(docs, f, sort_keys=False, width=120)
+        yaml.dump_all(docs, f, Dumper=NoAliasDumper, sort_keys=False, width=120, default_flow_style=flow)
 
 
 # ------------------------------------------------------------------ kustomize-lite
@@ -706,7 +681,7 @@ def main(argv=None):
     if argv[0] == "generate":
         generate(argv[1] if len(argv) > 1 else "manifests")
         return 0
-    yaml.safe_dump_all(build(argv[1]), sys.stdout, sort_keys=False)
+    yaml.dump_all(build(argv[1]), sys.stdout, Dumper=NoAliasDumper, sort_keys=False)
     return 0
 
 

@@ -3,6 +3,7 @@ kind, plural, scope and versions (order, served, storage) match a table transcri
 reference CRD files; the Notebook CRD carries the reference's validation patches and the typed
 PodSpec subset, so the API server rejects invalid Notebooks and accepts what the JWA creates."""
 import copy
+import os
 
 import pytest
 
@@ -16,6 +17,9 @@ from service_account_auth_improvements_amd.controlplane.client import InMemoryCl
 #   components/admission-webhook/manifests/base/crd.yaml:10-16,18,2059-2060
 #   components/pvcviewer-controller/config/crd/bases/kubeflow.org_pvcviewers.yaml:9-15,17,3425-3426
 #   components/tensorboard-controller/config/crd/bases/tensorboard.kubeflow.org_tensorboards.yaml:10-16,18,77-78
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF = os.environ.get("KFAMD_REFERENCE_ROOT", "/root/reference")      # read-only upstream checkout
+
 REFERENCE = [
     ("kubeflow.org_notebooks.yaml", "kubeflow.org", "Notebook", "notebooks", "Namespaced",
      [("v1", True, True), ("v1alpha1", True, False), ("v1beta1", True, False)]),
@@ -92,10 +96,86 @@ def test_valid_notebook_accepted_in_every_served_version(version):
              tolerations=[{"key": "amd.com/gpu", "operator": "Exists", "effect": "NoSchedule"}],
              affinity={"nodeAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": {
                  "nodeSelectorTerms": [{"matchExpressions": [{"key": "gpu", "operator": "In", "values": ["mi355x"]}]}]}}},
-             securityContext={"fsGroup": 100}, someFutureField={"kept": True})
+             securityContext={"fsGroup": 100})
     out = c.create(nb)
     assert out["apiVersion"] == "kubeflow.org/v1"          # stored in the storage version
-    assert out["spec"]["template"]["spec"]["someFutureField"] == {"kept": True}
+    assert out["spec"]["template"]["spec"]["volumes"][0]["emptyDir"] == {"medium": "Memory"}
+
+
+def test_unknown_pod_fields_are_pruned_or_rejected_under_strict_validation():
+    """The PodSpec schema is fully typed (corev1.py): an undeclared field is pruned like
+    kube-apiserver does, and ``fieldValidation=Strict`` (kubectl's default) rejects it -- a
+    misspelt container field is never stored silently as if it meant something."""
+    c = _server()
+    typo = dict(GOOD, imagePullPolicyy="Always")
+    out = c.create(_nb([typo], someFutureField={"x": 1}))
+    assert "imagePullPolicyy" not in out["spec"]["template"]["spec"]["containers"][0]
+    assert "someFutureField" not in out["spec"]["template"]["spec"]
+    srv = c.server
+    with pytest.raises(ApiError) as ei:
+        srv.create(_nb([typo], "v1") | {"metadata": {"name": "nb2", "namespace": "ns1"}}, field_validation="Strict")
+    assert ei.value.code == 422
+    assert 'unknown field "spec.template.spec.containers[0].imagePullPolicyy"' in str(ei.value)
+    # a field the schema declares deep in the tree is kept
+    deep = dict(GOOD, lifecycle={"preStop": {"exec": {"command": ["sleep", "1"]}}},
+                securityContext={"capabilities": {"drop": ["ALL"]}, "seccompProfile": {"type": "RuntimeDefault"}})
+    out = srv.create(_nb([deep], "v1") | {"metadata": {"name": "nb3", "namespace": "ns1"}}, field_validation="Strict")
+    assert out["spec"]["template"]["spec"]["containers"][0]["lifecycle"]["preStop"]["exec"]["command"] == ["sleep", "1"]
+
+
+def _ref_paths(path, kind, version=None):
+    import yaml
+    from service_account_auth_improvements_amd import corev1
+    docs = [d for d in yaml.safe_load_all(open(path)) if d and d.get("kind") == "CustomResourceDefinition"]
+    (crd,) = [d for d in docs if d["spec"]["names"]["kind"] == kind]
+    (v,) = [v for v in crd["spec"]["versions"] if version is None or v["name"] == version]
+    return corev1.paths(v["schema"]["openAPIV3Schema"])
+
+
+def _repo_paths(fname, version):
+    from service_account_auth_improvements_amd import corev1
+    crd = manifests.crds()[fname]
+    (v,) = [v for v in crd["spec"]["versions"] if v["name"] == version]
+    return corev1.paths(v["schema"]["openAPIV3Schema"])
+
+
+def test_every_reference_schema_path_is_typed_here():
+    """Walk every property path of the reference Notebook (v1) and PodDefault CRDs: each must be
+    declared in this repo's schema of the same version -- none is hidden behind
+    x-kubernetes-preserve-unknown-fields, and there is no allow-list."""
+    if not os.path.isdir(REF):
+        pytest.skip("reference checkout not present")
+    nb_ref = _ref_paths(os.path.join(REF, "components/notebook-controller/config/crd/bases/kubeflow.org_notebooks.yaml"),
+                        "Notebook", "v1")
+    nb = _repo_paths("kubeflow.org_notebooks.yaml", "v1")
+    assert len(nb_ref) > 900 and nb_ref - nb == set(), sorted(nb_ref - nb)[:20]
+    pd_ref = _ref_paths(os.path.join(REF, "components/admission-webhook/manifests/base/crd.yaml"), "PodDefault")
+    pd = _repo_paths("kubeflow.org_poddefaults.yaml", "v1alpha1")
+    assert len(pd_ref) > 600 and pd_ref - pd == set(), sorted(pd_ref - pd)[:20]
+
+
+def test_generated_crds_are_alias_free_and_fully_structural():
+    text = "".join(open(os.path.join(ROOT, "manifests", "crds", f)).read()
+                   for f in os.listdir(os.path.join(ROOT, "manifests", "crds")))
+    assert "&id" not in text and "*id" not in text
+    for fn, crd in manifests.crds().items():
+        for v in crd["spec"]["versions"]:
+            bad = _preserve_paths(v["schema"]["openAPIV3Schema"])
+            # the only free-form node: a Profile plugin's spec (runtime.RawExtension upstream)
+            assert bad <= {".spec.plugins[].spec"}, (fn, v["name"], sorted(bad))
+
+
+def _preserve_paths(s, pre=""):
+    out = set()
+    if s.get("x-kubernetes-preserve-unknown-fields"):
+        out.add(pre)
+    for k, v in (s.get("properties") or {}).items():
+        out |= _preserve_paths(v, f"{pre}.{k}")
+    if isinstance(s.get("items"), dict):
+        out |= _preserve_paths(s["items"], pre + "[]")
+    if isinstance(s.get("additionalProperties"), dict):
+        out |= _preserve_paths(s["additionalProperties"], pre + "{}")
+    return out
 
 
 @pytest.mark.parametrize("containers,extra,why", [
