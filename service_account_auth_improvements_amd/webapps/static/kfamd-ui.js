@@ -23,6 +23,12 @@
   function header(title, extra) {
     return el("header", {}, el("h1", {}, title), extra);
   }
+  // delete through the common-lib confirm dialog (the reference's DELETE / CANCEL dialog)
+  function confirmDelete(kind, name, doDelete) {
+    return KF.confirmDialog({ title: "Delete " + kind + " " + name + "?",
+                              message: "Warning: All data in this " + kind.toLowerCase() + " will be lost.",
+                              accept: "DELETE", applying: "DELETING", onAccept: doDelete });
+  }
   // (re-)render the page of the current hash; the hashchange listener is registered once per app
   function router(pages) {
     if (!pages._go) {
@@ -42,24 +48,32 @@
     var main = el("main"), headerExtra = el("span");
     root.append(header("Notebooks", headerExtra), main);
     api("GET", "api/config").then(function (j) { config = j.config || {}; }, function (e) { snack(e.message, true); })
-      .then(function () { return KF.namespaceSelect(function (v) { ns = v; router(pages); }); })
+      .then(function () { return KF.namespaceSelect(function (v) { ns = v; router(pages); }, { all: true }); })
       .then(function (s) { sel = s; ns = s.value; headerExtra.replaceChildren(sel); router(pages); });
 
     var pages = {
       index: function () {
         if (poller) poller.stop();
         var list = el("div");
-        main.replaceChildren(el("div", {}, el("a", { href: "#/new" }, el("button", {}, "+ New notebook"))), list);
+        main.replaceChildren(KF.titleToolbar("Notebooks", el("a", { href: "#/new" }, el("button", {}, "+ New notebook"))), list);
         poller = KF.poll(function () {
           if (!ns) return [];
-          return api("GET", "api/namespaces/" + ns + "/notebooks").then(function (j) {
-            var nbs = j.notebooks;
+          var all = ns === KF.ALL_NS;
+          // all namespaces: the union of every namespace's list (the reference frontend does
+          // the same over its namespace list)
+          var nsList = all ? (sel && sel.namespaces) || [] : [ns];
+          return Promise.all(nsList.map(function (n) {
+            return api("GET", "api/namespaces/" + n + "/notebooks", null, { quiet: all }).then(function (j) { return j.notebooks || []; },
+                                                                                    function () { return []; });
+          })).then(function (parts) {
+            var nbs = [].concat.apply([], parts);
             list.replaceChildren(KF.table([
               ["Status", function (n) { return KF.status(n.status); }, function (n) { return n.status.phase; }],
               ["Name", function (n) { return el("a", { href: "#/details/" + n.namespace + "/" + n.name }, n.name); },
                function (n) { return n.name; }],
+            ].concat(all ? [["Namespace", function (n) { return n.namespace; }, function (n) { return n.namespace; }]] : [], [
               ["Type", function (n) { return n.serverType || "jupyter"; }],
-              ["Age", function (n) { return L.age(n.age); }, function (n) { return n.age; }],
+              ["Age", function (n) { return KF.dateTime(n.age); }, function (n) { return n.age; }],
               ["Image", function (n) { return n.shortImage; }],
               ["GPUs", function (n) { return (n.gpus && n.gpus.message) || "-"; }],
               ["CPU", function (n) { return n.cpu; }], ["Memory", function (n) { return n.memory; }],
@@ -67,10 +81,12 @@
               ["", function (n) {
                 return [el("a", { href: "/notebook/" + n.namespace + "/" + n.name + "/", target: "_blank" },
                            el("button", { disabled: n.status.phase !== "ready" }, "Connect")),
-                        el("button", { onclick: function () { act("PATCH", n.name, { stopped: n.status.phase !== "stopped" }); } },
+                        el("button", { onclick: function () { act("PATCH", n.name, { stopped: n.status.phase !== "stopped" }, n.namespace); } },
                            n.status.phase === "stopped" ? "Start" : "Stop"),
-                        el("button", { onclick: function () { if (confirm("Delete " + n.name + "?")) act("DELETE", n.name); } }, "Delete")];
-              }]], nbs, { empty: "No notebooks in this namespace." }));
+                        el("button", { "data-cy": "delete", onclick: function () {
+                          confirmDelete("Notebook", n.name, function () { return act("DELETE", n.name, undefined, n.namespace); });
+                        } }, "Delete")];
+              }]]), nbs, { empty: "No notebooks in this namespace.", sortBy: "Name" }));
             return nbs;
           });
         });
@@ -79,9 +95,9 @@
       details: function (dns, name) { if (poller) poller.stop(); notebookDetails(dns || ns, name); }
     };
 
-    function act(method, name, body) {
-      return api(method, "api/namespaces/" + ns + "/notebooks/" + name, body)
-        .then(function () { if (poller) poller.reset(); }, function (e) { snack(e.message, true); });
+    function act(method, name, body, where) {
+      return api(method, "api/namespaces/" + (where || ns) + "/notebooks/" + name, body)
+        .then(function () { if (poller) poller.reset(); });
     }
 
     // ------------------------------------------------------------ new notebook form
@@ -90,7 +106,7 @@
       var v = function (f, d) { return L.cfgValue(config, f, d); };
       var vendorsInstalled = [], pvcs = [], poddefaults = [];
       var f = el("form", { class: "card", novalidate: true });
-      main.replaceChildren(back("Notebooks"), el("h2", {}, "New notebook"), f);
+      main.replaceChildren(KF.titleToolbar("New notebook", null, "#/"), f);
       Promise.all([api("GET", "api/gpus").then(function (j) { vendorsInstalled = j.vendors || []; }, function () {}),
                    api("GET", "api/namespaces/" + ns + "/pvcs").then(function (j) { pvcs = j.pvcs || []; }, function () {}),
                    api("GET", "api/namespaces/" + ns + "/poddefaults").then(function (j) { poddefaults = j.poddefaults || []; }, function () {})])
@@ -128,10 +144,18 @@
         }));
         // workspace volume
         var wsType = el("select", { disabled: ro("workspaceVolume") }, opt("new", "New volume"), opt("existing", "Existing volume"), opt("none", "None"));
-        var wsName = el("input", { placeholder: "{notebook-name}-workspace" }), wsSize = el("input", { value: "5Gi" });
+        var wsTpl = ((((v("workspaceVolume", {}) || {}).newPvc || {}).metadata || {}).name) || "{notebook-name}-workspace";
+        var wsDirty = false;
+        var wsName = el("input", { "data-cy": "volume name input", value: wsTpl.replace("{notebook-name}", ""),
+                                   oninput: function () { wsDirty = true; wsHeader.textContent = wsName.value; } });
+        var wsHeader = el("span", { "data-cy": "volume name header" }, wsName.value);
+        name.addEventListener("input", function () {
+          if (!wsDirty) { wsName.value = wsTpl.replace("{notebook-name}", name.value); wsHeader.textContent = wsName.value; }
+        });
+        var wsSize = el("input", { value: "5Gi" });
         var wsMount = el("input", { value: "/home/jovyan" });
         var wsExisting = el("select", {}, pvcs.map(function (p) { return opt(p.name, p.name + " (" + p.size + ")"); }));
-        var wsBox = el("div");
+        var wsBox = el("div", { "data-cy": "workspace volume" });
         function wsRender() {
           wsBox.replaceChildren.apply(wsBox, wsType.value === "new" ? ["name ", wsName, " size ", wsSize, " mount ", wsMount]
             : wsType.value === "existing" ? ["claim ", wsExisting, " mount ", wsMount] : []);
@@ -144,17 +168,23 @@
           dvList.replaceChildren.apply(dvList, datavols.map(function (d, i) {
             var t = el("select", { onchange: function (ev) { d.type = ev.target.value; dvRender(); } },
                        opt("new", "New", d.type === "new"), opt("existing", "Existing", d.type === "existing"));
+            var mount = el("input", { value: d.mount, "data-cy": "mount path",
+                                      oninput: function (ev) { d.mount = ev.target.value; d.mountDirty = true; } });
+            // a new data volume mounts at /home/jovyan/<name> until its mount path is edited
+            var follow = function (v) { d.name = v; if (!d.mountDirty) { d.mount = "/home/jovyan/" + v; mount.value = d.mount; } };
             var nm = d.type === "existing"
-              ? el("select", { onchange: function (ev) { d.name = ev.target.value; } }, pvcs.map(function (p) { return opt(p.name, p.name, p.name === d.name); }))
-              : el("input", { value: d.name, placeholder: "volume name", oninput: function (ev) { d.name = ev.target.value; } });
-            if (d.type === "existing" && !d.name && pvcs.length) d.name = pvcs[0].name;
-            return el("div", { class: "dv" }, t, " ", nm,
+              ? el("select", { "data-cy": "volume name input", onchange: function (ev) { follow(ev.target.value); } },
+                   pvcs.map(function (p) { return opt(p.name, p.name, p.name === d.name); }))
+              : el("input", { value: d.name, placeholder: "volume name", "data-cy": "volume name input",
+                              oninput: function (ev) { follow(ev.target.value); } });
+            if (d.type === "existing" && !d.name && pvcs.length) follow(pvcs[0].name);
+            return el("div", { class: "dv" + (i === datavols.length - 1 ? " last" : ""), "data-cy": "data volumes" }, t, " ", nm,
               d.type === "new" ? [" size ", el("input", { value: d.size, size: 6, oninput: function (ev) { d.size = ev.target.value; } })] : null,
-              " mount ", el("input", { value: d.mount, oninput: function (ev) { d.mount = ev.target.value; } }),
+              " mount ", mount,
               el("button", { type: "button", onclick: function () { datavols.splice(i, 1); dvRender(); } }, "✖"));
           }));
         }
-        var addDv = el("button", { type: "button", disabled: ro("dataVolumes"), onclick: function () {
+        var addDv = el("button", { type: "button", "data-cy": "add new volume", disabled: ro("dataVolumes"), onclick: function () {
           datavols.push({ type: "new", name: "", size: "10Gi", mount: "/home/jovyan/data-" + (datavols.length + 1) }); dvRender();
         } }, "+ Add volume");
         // scheduling + configurations
@@ -177,11 +207,11 @@
           KF.field("CPU request / limit", [cpu, " / ", cpuLimit]),
           KF.field("Memory request / limit", [mem, " / ", memLimit]),
           KF.field("GPUs", [gpuNum, " ", gpuVendor]),
-          KF.field("Workspace volume", [wsType, " ", wsBox]),
+          KF.field(["Workspace volume ", wsHeader], [wsType, " ", wsBox]),
           KF.field("Data volumes", [dvList, addDv]),
           KF.field("Affinity", aff), KF.field("Tolerations", tol),
           KF.field("Configurations", cfgBoxes.length ? cfgBoxes : el("span", { class: "muted" }, "no PodDefaults in this namespace")),
-          KF.field("Shared memory (/dev/shm)", shm),
+          KF.field(["Shared memory (/dev/shm)", KF.helpPopover("Mounts an in-memory /dev/shm: PyTorch DataLoader workers and RCCL use it.")], shm),
           KF.field("Environment", env),
           [el("span"), el("div", {}, errBox, el("button", { type: "submit" }, "Launch"), el("a", { href: "#/" }, el("button", { type: "button" }, "Cancel")))]));
         f.onsubmit = function (ev) {
@@ -214,7 +244,10 @@
       var title = el("h2", {}, name), st = el("span");
       main.replaceChildren(back("Notebooks"), el("div", {}, title, " ", st,
         el("a", { href: "/notebook/" + dns + "/" + name + "/", target: "_blank" }, el("button", {}, "Connect")),
-        el("button", { onclick: function () { act("DELETE", name).then(function () { location.hash = "#/"; }); } }, "Delete")),
+        el("button", { "data-cy": "delete", onclick: function () {
+          confirmDelete("Notebook", name, function () { return act("DELETE", name, undefined, dns); })
+            .then(function (ok) { if (ok) location.hash = "#/"; });
+        } }, "Delete")),
         KF.tabs([
           ["Overview", function () {
             return api("GET", p).then(function (j) {
@@ -224,9 +257,13 @@
                 ["Status", KF.status(nb.processed_status)], ["Server type", o.serverType], ["Image", o.image],
                 ["Creator", o.creator], ["CPU (request / limit)", o.cpu + " / " + (o.cpuLimit || "-")],
                 ["Memory (request / limit)", o.memory + " / " + (o.memoryLimit || "-")],
-                ["GPUs", o.gpus.join(", ") || "none"], ["Configurations", o.configurations.join(", ")],
-                ["Environment", o.environment.join(", ")], ["Tolerations / affinity", o.tolerations + " / " + (o.affinity ? "set" : "none")],
-                ["Age", L.age(nb.metadata.creationTimestamp)]]),
+                ["GPUs", o.gpus.length ? o.gpus : ["none"], "amd.com/gpu devices allocated to the notebook's pod"],
+                ["Configurations", o.configurations, "PodDefaults applied by label"],
+                ["Tolerations / affinity", o.tolerations + " / " + (o.affinity ? "set" : "none")],
+                ["Age", KF.dateTime(nb.metadata.creationTimestamp)]]),
+                el("h4", {}, "Environment"),
+                KF.variablesGroupsTable([{ name: "container", variables: o.environment.map(function (e) {
+                  var i = e.indexOf("="); return [e.slice(0, i), e.slice(i + 1)]; }) }]),
                 el("h4", {}, "Volumes"),
                 KF.table([["Name", function (x) { return x.name; }], ["Source", function (x) { return x.source; }],
                           ["Mount path", function (x) { return x.mount; }]], o.volumes),
@@ -294,10 +331,11 @@
                 return [p.viewer.status === "ready" && p.viewer.url ? el("a", { href: p.viewer.url, target: "_blank" }, el("button", {}, "Browse"))
                   : el("button", { onclick: function () { api("POST", "api/namespaces/" + ns + "/viewers", { name: p.name })
                       .then(function () { poller.reset(); }, function (e) { snack(e.message, true); }); } }, "Open viewer"),
-                  el("button", { onclick: function () { if (confirm("Delete " + p.name + "?"))
-                    api("DELETE", "api/namespaces/" + ns + "/pvcs/" + p.name).then(function () { poller.reset(); },
-                                                                                   function (e) { snack(e.message, true); }); } }, "Delete")];
-              }]], pvcs, { empty: "No volumes in this namespace." }));
+                  el("button", { "data-cy": "delete", onclick: function () {
+                    confirmDelete("Volume", p.name, function () {
+                      return api("DELETE", "api/namespaces/" + ns + "/pvcs/" + p.name).then(function () { poller.reset(); });
+                    }); } }, "Delete")];
+              }]], pvcs, { empty: "No volumes in this namespace.", sortBy: "Name" }));
             return pvcs;
           });
         });
@@ -373,10 +411,11 @@
             ["Status", function (t) { return KF.status(t.status); }],
             ["Name", function (t) { return el("a", { href: "/tensorboard/" + t.namespace + "/" + t.name + "/", target: "_blank" }, t.name); }, function (t) { return t.name; }],
             ["Logs", function (t) { return t.logspath; }], ["Age", function (t) { return L.age(t.age); }],
-            ["", function (t) { return el("button", { onclick: function () { if (confirm("Delete " + t.name + "?"))
-              api("DELETE", "api/namespaces/" + ns + "/tensorboards/" + t.name).then(function () { poller.reset(); },
-                                                                                   function (e) { snack(e.message, true); }); } }, "Delete"); }]],
-            tbs, { empty: "No TensorBoards in this namespace." }));
+            ["", function (t) { return el("button", { "data-cy": "delete", onclick: function () {
+              confirmDelete("TensorBoard", t.name, function () {
+                return api("DELETE", "api/namespaces/" + ns + "/tensorboards/" + t.name).then(function () { poller.reset(); });
+              }); } }, "Delete"); }]],
+            tbs, { empty: "No TensorBoards in this namespace.", sortBy: "Name" }));
           return tbs;
         });
       });
@@ -384,11 +423,17 @@
   }
 
   // ==================================================================== Central dashboard (T2/T3)
+  // Routes (centraldashboard-angular app-routing.module.ts): #/ home, #/_/<app path> the app in
+  // the iframe -- a path holding "{ns}" is resolved to the selected namespace, or, with no
+  // namespace to pick, redirected to #/namespace-needed (guards/iframe.guard.ts) --, #/manage
+  // contributors, anything else the 404 page.  Failed calls go through the error interceptor
+  // (KF.api: "[status] log" snack).
   function dashboard() {
-    var j = function (p) { return fetch(new URL(p, KF.base)).then(function (r) { return r.json(); }); };
+    var j = function (p, quiet) { return api("GET", p, null, { quiet: quiet }); };
     Promise.all([j("api/workgroup/env-info"), j("api/workgroup/exists"),
-                 j("api/dashboard-links").catch(function () { return { menuLinks: [] }; })]).then(function (r) {
+                 j("api/dashboard-links", true).catch(function () { return { menuLinks: [] }; })]).then(function (r) {
       var env = r[0], exists = r[1], links = r[2];
+      var nss = (env.namespaces || []).map(function (b) { return b.namespace; });
       var nsSel = el("select", {}, (env.namespaces || []).map(function (b) {
         return el("option", { value: b.namespace }, b.namespace + " (" + b.role + ")");
       }));
@@ -396,39 +441,56 @@
       var post = function () {
         if (frame.contentWindow) frame.contentWindow.postMessage({ type: "namespace-selected", value: nsSel.value }, "*");
       };
-      nsSel.addEventListener("change", function () { post(); home(); });
+      nsSel.addEventListener("change", function () { post(); go(); });
       frame.addEventListener("load", post);
       window.addEventListener("message", function (ev) {          // library.js protocol
         if (ev.data && ev.data.type === "iframe-connected") post();
       });
-      var main = el("div");
-      var nav = el("nav", {}, el("a", { href: "#", onclick: function (ev) { ev.preventDefault(); home(); } }, "Home"),
-        (links.menuLinks || []).map(function (l) {
-          return el("a", { href: "#", onclick: function (ev) {
-            ev.preventDefault(); frame.src = l.link + "?ns=" + nsSel.value; main.replaceChildren(frame);
-          } }, l.text);
-        }),
-        el("a", { href: "#", onclick: function (ev) { ev.preventDefault(); manage(); } }, "Manage contributors"));
+      var main = el("div", { class: "dash-main" });
+      var nav = el("nav", {}, el("a", { href: "#/" }, "Home"),
+        (links.menuLinks || []).map(function (l) { return el("a", { href: "#/_" + l.link }, l.text); }),
+        el("a", { href: "#/manage" }, "Manage contributors"));
       root.append(header("Kubeflow on MI355X", [nsSel, el("span", {}, env.user || "")]), el("div", { class: "dash" }, nav, main));
       if (!exists.hasWorkgroup && exists.registrationFlowAllowed && exists.hasAuth) {
         var inp = el("input", { value: exists.user });
         main.replaceChildren(el("div", { class: "card" }, el("h2", {}, "Create your namespace"), inp,
           el("button", { onclick: function () {
-            fetch(new URL("api/workgroup/create", KF.base), { method: "POST", headers: { "Content-Type": "application/json" },
-                                                              body: JSON.stringify({ namespace: inp.value }) })
-              .then(function () { location.reload(); });
+            api("POST", "api/workgroup/create", { namespace: inp.value }).then(function () { location.reload(); });
           } }, "Finish")));
         return;
       }
+      function go() {
+        var h = (location.hash || "#/").slice(1) || "/";
+        if (h === "/" || h === "") return home();
+        if (h === "/manage") return manage();
+        if (h.indexOf("/namespace-needed") === 0) return namespaceNeeded();
+        if (h.indexOf("/_/") === 0) {
+          var path = decodeURIComponent(h.slice(2));
+          if (path.indexOf("{ns}") >= 0) {
+            if (!nss.length) { location.hash = "#/namespace-needed?path=" + encodeURIComponent(path); return; }
+            path = path.split("{ns}").join(nsSel.value);
+          }
+          frame.src = path;
+          return main.replaceChildren(frame);
+        }
+        main.replaceChildren(el("div", { class: "error-page", "data-cy": "not-found" }, el("div", { class: "headline" }, "404"),
+          el("div", {}, "Sorry, ", el("b", {}, h), " is not a valid page."), el("a", { href: "#/" }, "back to home")));
+      }
+      function namespaceNeeded() {
+        main.replaceChildren(el("div", { class: "error-page", "data-cy": "namespace-needed" },
+          el("div", {}, "This page requires a namespace to be selected but no namespaces are currently available."),
+          el("a", { href: "#/" }, "back to home")));
+      }
       function home() {
         var ns = nsSel.value;
-        Promise.all([j("api/activities/" + ns).catch(function () { return []; }),
-                     j("api/metrics/node?interval=Last15m").catch(function () { return []; })]).then(function (r2) {
+        Promise.all([j("api/activities/" + ns, true).catch(function () { return []; }),
+                     j("api/metrics/node?interval=Last15m", true).catch(function () { return []; })]).then(function (r2) {
           var acts = r2[0] || [], pts = Array.isArray(r2[1]) ? r2[1] : [];
           main.replaceChildren(el("div", { style: "padding:16px" }, el("h2", {}, "Recent activity in " + ns),
-            KF.table([["Time", function (e) { return e.lastTimestamp || e.eventTime || ""; }], ["Type", function (e) { return e.type; }],
+            KF.table([["Time", function (e) { return KF.dateTime(e.lastTimestamp || e.eventTime); }], ["Type", function (e) { return e.type; }],
                       ["Object", function (e) { return (e.involvedObject || {}).kind + "/" + (e.involvedObject || {}).name; }],
-                      ["Message", function (e) { return e.message; }]], acts.slice(0, 20), { empty: "No recent activity." }),
+                      ["Message", function (e) { return e.message; }]], (Array.isArray(acts) ? acts : []).slice(0, 20),
+                     { empty: "No recent activity." }),
             el("h2", {}, "Node CPU utilisation (15 min)"),
             KF.table([["Time", function (p) { return new Date(p.timestamp * 1000).toLocaleTimeString(); }],
                       ["Node", function (p) { return p.label; }], ["Value", function (p) { return (100 * p.value).toFixed(1) + " %"; }]],
@@ -440,9 +502,8 @@
         j("api/workgroup/get-contributors/" + ns).catch(function () { return []; }).then(function (users) {
           var who = el("input", { placeholder: "user@example.com" });
           var call = function (m) {
-            return fetch(new URL("api/workgroup/" + (m === "POST" ? "add" : "remove") + "-contributor/" + ns, KF.base),
-                         { method: m, headers: { "Content-Type": "application/json" }, body: JSON.stringify({ contributor: who.value }) })
-              .then(function (r) { return r.ok ? null : r.json().then(function (b) { snack(b.error, true); }); }).then(manage);
+            return api(m, "api/workgroup/" + (m === "POST" ? "add" : "remove") + "-contributor/" + ns, { contributor: who.value })
+              .catch(function () {}).then(manage);
           };
           main.replaceChildren(el("div", { class: "card" }, el("h2", {}, "Contributors of " + ns),
             el("ul", {}, users.map(function (u) { return el("li", {}, u); })), who,
@@ -450,7 +511,8 @@
             el("button", { onclick: function () { call("DELETE"); } }, "Remove")));
         });
       }
-      home();
+      window.addEventListener("hashchange", go);
+      go();
     });
   }
 

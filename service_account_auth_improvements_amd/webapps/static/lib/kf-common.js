@@ -1,7 +1,9 @@
 // kubeflow-common-lib components for the kfamd web UI (DOM side; the logic is kf-logic.js).
 // Reference: crud-web-apps/common/frontend/kubeflow-common-lib/projects/kubeflow/src/lib/
 // {resource-table, status-icon, namespace-select, snack-bar, editor, conditions-table,
-//  logs-viewer, details-list, title-actions-toolbar, services/backend, services/poller}.
+//  logs-viewer, details-list, title-actions-toolbar, confirm-dialog, help-popover, date-time,
+//  variables-groups-table, services/backend, services/poller} and the central dashboard's
+// error interceptor (centraldashboard-angular/frontend/src/app/interceptors).
 (function (root) {
   "use strict";
   var L = root.KFL;
@@ -34,24 +36,123 @@
     return m ? decodeURIComponent(m[1]) : "";
   }
 
-  // backend service: the crud_backend response envelope {success, status, log, <payload>}
-  function api(method, path, body) {
+  // error interceptor (centraldashboard-angular interceptors/error.interceptor.ts): the snack
+  // text for a failed request -- [status] backend log + URL, or "could not connect" -- while the
+  // rejected promise carries the backend's log line itself
+  function backendLog(status, j, statusText) {
+    if (j && j.log) return j.log;
+    if (j && j.error) return typeof j.error === "string" ? j.error : JSON.stringify(j.error);
+    return status + ": " + (statusText || "error");
+  }
+  function snackErrorMessage(e) {
+    if (typeof e === "string") return "An error occurred: " + e;
+    if (e && e.status !== undefined) {
+      if (e.status <= 0) return "Could not connect to the backend.";
+      return "[" + e.status + "] " + e.message + "\n" + (e.url || "");
+    }
+    return (e && e.message) || "Unexpected error encountered";
+  }
+  function HttpError(status, message, url) {
+    var e = new Error(message);
+    e.status = status;
+    e.url = url;
+    return e;
+  }
+
+  // backend service: the crud_backend response envelope {success, status, log, <payload>};
+  // failures go through the error interceptor (snack unless opts.quiet) and reject
+  function api(method, path, body, opts) {
+    opts = opts || {};
     var headers = { "Content-Type": "application/json" };
     if (["GET", "HEAD"].indexOf(method) < 0) headers["X-XSRF-TOKEN"] = cookie("XSRF-TOKEN");
-    return fetch(new URL(path, base), { method: method, headers: headers, credentials: "same-origin",
-                                        body: body ? JSON.stringify(body) : undefined })
+    var url = new URL(path, base);
+    return fetch(url, { method: method, headers: headers, credentials: "same-origin",
+                        body: body ? JSON.stringify(body) : undefined })
       .then(function (r) {
         return r.json().catch(function () { return {}; }).then(function (j) {
-          if (!r.ok || j.success === false) throw new Error(j.log || j.error || r.statusText);
+          if (!r.ok || j.success === false) throw HttpError(r.status || j.status || 500, backendLog(r.status, j, r.statusText), url.href);
           return j;
         });
+      }, function () { throw HttpError(0, "Could not connect to the backend.", url.href); })
+      .catch(function (e) {
+        if (!opts.quiet) snack(snackErrorMessage(e), true);
+        throw e;
       });
   }
 
   function snack(msg, err) {
-    var s = el("div", { class: "snack" + (err ? " err" : ""), role: "status" }, msg);
+    var s = el("div", { class: "snack" + (err ? " err" : ""), role: "status",
+                        "data-cy-snack-status": err ? "ERROR" : "SUCCESS" }, msg);
     document.body.append(s);
     setTimeout(function () { s.remove(); }, 5000);
+  }
+
+  // confirm-dialog (kubeflow-common-lib confirm-dialog): a modal with a title, a message and
+  // accept / cancel; resolves true on accept.  The accept button shows the "applying" text while
+  // opts.onAccept's promise runs; an error there stays in the dialog.
+  function confirmDialog(opts) {
+    return new Promise(function (resolve) {
+      var err = el("div", { class: "err", "data-cy": "dialog-error" });
+      var accept = el("button", { class: "accept", "data-cy": "dialog-accept" }, opts.accept || "DELETE");
+      var cancel = el("button", { "data-cy": "dialog-cancel" }, opts.cancel || "CANCEL");
+      var box = el("div", { class: "dialog-backdrop", role: "dialog", "aria-modal": "true" },
+        el("div", { class: "dialog" }, el("h3", { "data-cy": "dialog-title" }, opts.title || "Are you sure?"),
+          el("p", { "data-cy": "dialog-message" }, opts.message || ""), err, el("div", { class: "actions" }, cancel, accept)));
+      function close(v) { box.remove(); resolve(v); }
+      cancel.addEventListener("click", function () { close(false); });
+      accept.addEventListener("click", function () {
+        if (!opts.onAccept) return close(true);
+        accept.disabled = true;
+        accept.textContent = opts.applying || "DELETING";
+        Promise.resolve().then(opts.onAccept).then(function () { close(true); }, function (e) {
+          accept.disabled = false;
+          accept.textContent = opts.accept || "DELETE";
+          err.textContent = (e && e.message) || String(e);
+        });
+      });
+      document.body.append(box);
+    });
+  }
+
+  // help-popover (kubeflow-common-lib help-popover): a "?" that toggles a short help text
+  function helpPopover(text) {
+    var pop = el("div", { class: "popover", role: "tooltip", hidden: true }, text);
+    var btn = el("button", { type: "button", class: "help", "aria-label": "help", onclick: function () {
+      pop.hidden = !pop.hidden;
+      if (pop.hidden) pop.setAttribute("hidden", ""); else pop.removeAttribute("hidden");
+    } }, "?");
+    pop.hidden = true;
+    return el("span", { class: "help-popover" }, btn, pop);
+  }
+
+  // date-time (kubeflow-common-lib date-time): the relative age, the absolute time on hover
+  function dateTime(ts) {
+    if (!ts) return el("span", { class: "muted" }, "-");
+    var d = new Date(ts);
+    return el("span", { class: "date-time", title: isNaN(d) ? String(ts) : d.toISOString() }, L.age(ts));
+  }
+
+  // title-actions-toolbar (kubeflow-common-lib title-actions-toolbar): back link, title, buttons
+  function titleToolbar(title, actions, backHref) {
+    return el("div", { class: "toolbar title-toolbar" },
+      backHref ? el("a", { href: backHref, class: "back", "aria-label": "back" }, "←") : null,
+      el("h2", { "data-cy-toolbar-title": "" }, title), el("span", { class: "spacer" }), actions || null);
+  }
+
+  // variables-groups-table (kubeflow-common-lib variables-groups-table): groups of
+  // key / value variables (a PodDefault's env, a notebook's configurations)
+  function variablesGroupsTable(groups) {
+    var rows = [];
+    (groups || []).forEach(function (g) {
+      var vars = g.variables || [];
+      if (!vars.length) rows.push(el("tr", {}, el("td", { class: "group" }, g.name), el("td", { colspan: 2, class: "muted" }, "-")));
+      vars.forEach(function (v, i) {
+        rows.push(el("tr", {}, el("td", { class: "group" }, i === 0 ? g.name : ""), el("td", { class: "key" }, v[0]),
+                     el("td", { class: "value" }, v[1] === undefined ? "" : v[1])));
+      });
+    });
+    return el("table", { class: "rt vgt" }, el("thead", {}, el("tr", {}, el("th", {}, "Group"), el("th", {}, "Name"),
+                                                                 el("th", {}, "Value"))), el("tbody", {}, rows));
   }
 
   var ICON = { ready: "✔", waiting: "⏳", warning: "⚠", error: "✖", stopped: "⏹",
@@ -62,10 +163,13 @@
               st.phase || "");
   }
 
-  // resource table: cols = [[title, render(row), sortKey(row)?], ...]; click a sortable header
+  // resource table: cols = [[title, render(row), sortKey(row)?], ...]; click a sortable header;
+  // opts.sortBy = the title of the column sorted (ascending) on first render
   function table(cols, rows, opts) {
     opts = opts || {};
-    var state = { col: -1, dir: 1 };
+    var first = -1;
+    cols.forEach(function (c, i) { if (c[0] === opts.sortBy && c[2]) first = i; });
+    var state = { col: first, dir: 1 };
     var body = el("tbody");
     function render() {
       var rs = rows.slice();
@@ -76,11 +180,11 @@
       body.replaceChildren.apply(body, rs.length ? rs.map(function (r) {
         return el("tr", { onclick: opts.onRow ? function (ev) { if (ev.target.tagName !== "BUTTON" && ev.target.tagName !== "A") opts.onRow(r); } : null,
                           class: opts.onRow ? "clickable" : null },
-                  cols.map(function (c) { return el("td", {}, c[1](r)); }));
+                  cols.map(function (c) { return el("td", { "data-cy-resource-table-row": c[0] }, c[1](r)); }));
       }) : [el("tr", {}, el("td", { colspan: cols.length, class: "empty" }, opts.empty || "No resources found."))]);
     }
     var head = el("tr", {}, cols.map(function (c, i) {
-      return el("th", { class: c[2] ? "sortable" : null, onclick: c[2] ? function () {
+      return el("th", { class: c[2] ? "sortable" : null, "data-cy-table-header-row": c[0], onclick: c[2] ? function () {
         state.dir = state.col === i ? -state.dir : 1; state.col = i; render();
       } : null }, c[0]);
     }));
@@ -104,14 +208,19 @@
              stop: function () { stopped = true; clearTimeout(timer); } };
   }
 
-  function namespaceSelect(onChange) {
+  // namespace-select; opts.all adds the "All namespaces" entry (value ALL_NS)
+  var ALL_NS = "*";
+  function namespaceSelect(onChange, opts) {
+    opts = opts || {};
     var sel = el("select", { id: "ns", "aria-label": "namespace" });
     var qs = new URLSearchParams(location.search).get("ns") || sessionStorage.getItem("kf-ns");
-    return api("GET", "api/namespaces").then(function (j) { return j.namespaces || []; }, function (e) {
-      snack(e.message, true); return [];
+    return api("GET", "api/namespaces").then(function (j) { return j.namespaces || []; }, function () {
+      return [];
     }).then(function (nss) {
+      sel.namespaces = nss.slice();
       nss.forEach(function (n) { sel.append(el("option", { value: n }, n)); });
-      if (qs && nss.indexOf(qs) >= 0) sel.value = qs;
+      if (opts.all) sel.append(el("option", { value: ALL_NS, "data-cy": "all-namespaces" }, "All namespaces"));
+      if (qs && (nss.indexOf(qs) >= 0 || (opts.all && qs === ALL_NS))) sel.value = qs;
       sel.addEventListener("change", function () { sessionStorage.setItem("kf-ns", sel.value); onChange(sel.value); });
       window.addEventListener("message", function (ev) {        // central dashboard iframe protocol
         if (ev.data && ev.data.type === "namespace-selected") { sel.value = ev.data.value; onChange(sel.value); }
@@ -184,9 +293,16 @@
     return box;
   }
 
+  // details-list (kubeflow-common-lib details-list): rows of [key, value, help?]; an array
+  // value renders as chips, an empty one as "-"
   function details(rows) {
     return el("dl", { class: "details" }, rows.map(function (r) {
-      return [el("dt", {}, r[0]), el("dd", {}, r[1] === "" || r[1] === undefined ? "-" : r[1])];
+      var v = r[1];
+      if (Array.isArray(v) && !(v[0] instanceof Node)) {
+        v = v.length ? v.map(function (x) { return el("span", { class: "chip" }, x); }) : "-";
+      }
+      return [el("dt", { "data-cy-details-key": r[0] }, r[0], r[2] ? helpPopover(r[2]) : null),
+              el("dd", { "data-cy-details-value": r[0] }, v === "" || v === undefined || v === null ? "-" : v)];
     }));
   }
 
@@ -212,11 +328,18 @@
     ".code{margin:0;padding:0 8px} pre.logs{max-height:70vh;overflow:auto;background:#111;color:#ddd;margin:0;padding:8px;font-size:12px}",
     ".ln{color:#777;display:inline-block;width:4em} .group h4{margin:8px 0 4px}",
     "nav a{display:block;padding:8px 12px;color:#222;text-decoration:none} nav a:hover{background:#eee}",
-    ".dash{display:grid;grid-template-columns:220px 1fr;height:calc(100vh - 44px)} iframe{border:0;width:100%;height:100%}"
+    ".dash{display:grid;grid-template-columns:220px 1fr;height:calc(100vh - 44px)} iframe{border:0;width:100%;height:100%}",
+    ".dialog-backdrop{position:fixed;inset:0;background:rgba(0,0,0,.35);display:flex;align-items:center;justify-content:center;z-index:10}",
+    ".dialog{background:#fff;padding:16px 20px;min-width:320px;border-radius:4px} .dialog .actions{text-align:right}",
+    ".dialog .accept{color:#c5221f} .help{border-radius:50%;border:1px solid #999;background:#fff;padding:0 6px;margin-left:4px}",
+    ".popover{position:absolute;background:#333;color:#fff;padding:6px 8px;font-size:12px;max-width:320px} .chip{background:#eee;border-radius:10px;padding:1px 8px;margin-right:4px}",
+    ".title-toolbar{display:flex;align-items:center;gap:8px} .title-toolbar .spacer{flex:1} .error-page{padding:32px;text-align:center}"
   ].join("\n");
   document.head.append(el("style", {}, css));
 
   root.KF = { el: el, api: api, snack: snack, status: status, table: table, poll: poll,
-              namespaceSelect: namespaceSelect, tabs: tabs, yamlView: yamlView, conditionsTable: conditionsTable,
-              logsViewer: logsViewer, details: details, field: field, base: base };
+              namespaceSelect: namespaceSelect, ALL_NS: ALL_NS, tabs: tabs, yamlView: yamlView,
+              conditionsTable: conditionsTable, logsViewer: logsViewer, details: details, field: field, base: base,
+              confirmDialog: confirmDialog, helpPopover: helpPopover, dateTime: dateTime, titleToolbar: titleToolbar,
+              variablesGroupsTable: variablesGroupsTable, snackErrorMessage: snackErrorMessage };
 })(self);
