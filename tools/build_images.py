@@ -1,7 +1,13 @@
 """P7: image builder (counterpart of py/kubeflow/kubeflow/cd/*: kaniko build + push per
 component and per notebook image, in dependency order).
 
-  python tools/build_images.py [--registry R] [--tag T] [--push] [--builder docker|kaniko] [--dry-run] [names...]
+  python tools/build_images.py [--registry R] [--tag T] [--push] [--builder docker|kaniko] [--dry-run]
+                               [--platforms linux/amd64,linux/ppc64le,linux/arm64/v8] [names...]
+
+``--platforms`` builds a multi-architecture image with ``docker buildx`` (the reference's
+``make docker-build-multi-arch``).  Only images with no GPU runtime in them may leave amd64
+(``MULTI_ARCH``): the control plane and TensorBoard.  The notebook servers and the ROCm data-plane
+images target MI355X hosts and stay linux/amd64.
 
 Control-plane components share one image (``images/platform``) tagged once per component
 name, since every Deployment runs ``python -m service_account_auth_improvements_amd <component>``.
@@ -55,6 +61,8 @@ IMAGES = {
     "tensorboard": ("images/tensorboard", "images/tensorboard/Dockerfile", {}, []),
 }
 NOTEBOOK_IMAGES = [n for n in IMAGES if n not in ("trainer-rocm", "predictor-rocm", "platform", "tensorboard")]
+MULTI_ARCH = {"platform", "tensorboard"}
+ALL_PLATFORMS = ("linux/amd64", "linux/ppc64le", "linux/arm64/v8")
 
 
 def platform_aliases():
@@ -77,12 +85,30 @@ def order(names):
     return out
 
 
-def commands(names, registry, tag, builder, push):
+def commands(names, registry, tag, builder, push, platforms=None):
     cmds = []
+    plats = [p for p in (platforms or []) if p]
     for n in order(names):
         ctx, df, args, _ = IMAGES[n]
         ref = f"{registry}/{n}:{tag}"
         bargs = [f"{k}={v.format(r=registry, t=tag)}" for k, v in args.items()]
+        if plats and plats != ["linux/amd64"]:
+            if n not in MULTI_ARCH:
+                raise ValueError(f"{n}: notebook and ROCm data-plane images are linux/amd64 only (asked for {','.join(plats)})")
+            bad = [p for p in plats if p not in ALL_PLATFORMS]
+            if bad:
+                raise ValueError(f"unsupported platforms {bad}")
+            c = ["docker", "buildx", "build", "--platform", ",".join(plats), "-f", os.path.join(ROOT, df), "-t", ref]
+            for b in bargs:
+                c += ["--build-arg", b]
+            c.append("--push" if push else "--output=type=cacheonly")
+            cmds.append(c + [os.path.join(ROOT, ctx)])
+            if n == "platform":
+                for alias in platform_aliases():
+                    c = ["docker", "buildx", "imagetools", "create", "-t", f"{registry}/{alias}:{tag}", ref]
+                    if push:
+                        cmds.append(c)
+            continue
         if builder == "kaniko":
             c = ["/kaniko/executor", f"--context=dir://{os.path.join(ROOT, ctx)}",
                  f"--dockerfile={os.path.join(ROOT, df)}", f"--destination={ref}"]
@@ -114,8 +140,9 @@ def main(argv=None):
     ap.add_argument("--builder", choices=["docker", "kaniko"], default="docker")
     ap.add_argument("--push", action="store_true")
     ap.add_argument("--dry-run", action="store_true")
+    ap.add_argument("--platforms", default="", help="comma-separated, e.g. linux/amd64,linux/ppc64le,linux/arm64/v8")
     a = ap.parse_args(argv)
-    for c in commands(a.names, a.registry, a.tag, a.builder, a.push):
+    for c in commands(a.names, a.registry, a.tag, a.builder, a.push, a.platforms.split(",") if a.platforms else None):
         print("+", " ".join(shlex.quote(x) for x in c), flush=True)
         if not a.dry_run:
             subprocess.run(c, check=True)

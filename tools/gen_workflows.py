@@ -7,8 +7,11 @@ Each component gets, triggered by changes under its paths:
 * ``<id>_integration_test.yaml`` -- its image build plan, then ``tools/ci_integration.py <id>``
   against the multi-process cluster (apiserver / controller-manager / kubelet over HTTP), the
   stand-in for the reference's KinD deploy-and-wait jobs;
-* ``<id>_docker_publish.yaml`` -- build and push its image on main.
-Multi-arch image tests are not generated: the images target MI355X hosts (linux/amd64 + ROCm).
+* ``<id>_docker_publish.yaml`` -- build and push its image on main;
+* ``<id>_multi_arch_test.yaml`` -- for the control-plane components (no GPU runtime in their
+  image): build it for linux/amd64, linux/ppc64le and linux/arm64/v8 under QEMU + buildx, as the
+  reference's ``*_multi_arch_test.yaml`` do.  The ROCm notebook / trainer / predictor images
+  target MI355X hosts and stay linux/amd64.
 
   python tools/gen_workflows.py            # (re)write .github/workflows/<id>_*.yaml
   python tools/gen_workflows.py --check    # exit 1 if any generated file is stale
@@ -94,6 +97,20 @@ def workflows():
                 {"name": "build and push",
                  "run": f"python3 tools/build_images.py {image} --registry ghcr.io/${{{{ github.repository_owner }}}} "
                         "--tag ${{ github.sha }} --push"}]}}}
+    for cid, (title, paths, tests, image, integ) in COMPONENTS.items():
+        if image != "platform":
+            continue
+        out[f"{cid}_multi_arch_test.yaml"] = {
+            "name": f"{title} Multi-Arch Build Test",
+            "on": {"pull_request": {"paths": paths + ["images/platform/**"], "branches": ["main"]}},
+            "concurrency": {"group": "${{ github.workflow }}-${{ github.ref }}-${{ github.event.number }}",
+                            "cancel-in-progress": True},
+            "jobs": {"build": {"runs-on": "ubuntu-22.04", "steps": _checkout() + [
+                {"name": "Setup QEMU", "uses": "docker/setup-qemu-action@v3"},
+                {"name": "Setup Docker Buildx", "uses": "docker/setup-buildx-action@v3"},
+                {"name": "Build multi-arch image",
+                 "run": "python3 tools/build_images.py platform --platforms "
+                        "linux/amd64,linux/ppc64le,linux/arm64/v8"}]}}}
     out["example_notebook_servers_publish.yaml"] = {
         "name": "Example Notebook Servers Publish", "on": {"push": {"paths": ["images/**"], "branches": ["main"]}},
         "jobs": {"publish": {"runs-on": "ubuntu-22.04", "steps": _checkout() + [
