@@ -9,12 +9,12 @@
 //  * 256 x 256 output tile per workgroup, 8 waves (2 along M x 4 along N), each wave a
 //    128 x 64 sub-tile = 8 x 4 v_mfma_f32_16x16x32_bf16 accumulators (128 VGPRs).  The
 //    16x16x32 form holds a higher clock than 32x32x16 on random data (guide: DVFS).
-//  * K is staged 32 rows at a time into a 4-deep LDS ring (4 x 32 KB): each stage is four
+//  * K is staged 32 rows at a time into a 5-deep LDS ring (5 x 32 KB = all 160 KB): each stage is four
 //    [32][128 x bf16] images (A lo/hi, B lo/hi) with 256-B rows whose 32-byte blocks are
 //    XOR-permuted by f(row) = (row & 3) | ((row >> 1) & 4): the two 16-lane groups of a
 //    transposed read (rows r..r+3 and r+8..r+11, 16 columns) then hit 8 distinct blocks,
 //    i.e. all 64 banks once, and the per-tile address is base ^ 32 t (one VGPR per tile).
-//  * LDS-DMA (global_load_lds_dwordx4) runs three stages ahead; each stage's data is
+//  * LDS-DMA (global_load_lds_dwordx4) runs four stages ahead; each stage's data is
 //    published by ONE counted vmcnt + s_barrier in the middle of the previous stage, so the
 //    operand reads can run four MFMA groups ahead across the stage seam.
 //  * Operand reads are inline asm with hand-counted lgkmcnt waits (<= 15 in flight): hipcc
@@ -33,6 +33,13 @@
 //  * A 4-wave variant (2 x 2 waves of 128 x 128, 256 accumulators pinned to AGPRs with
 //    inline-asm MFMAs, two-group-ahead operand reads) halves the LDS read rate but ran at
 //    1210 TF vs 1275: at one wave per SIMD every wait/barrier bubble reaches the MFMA pipe.
+//  * Anatomy (round 3, tools/kbench anatomy builds, K = 32768): removing the DMA pieces lifts the
+//    loop from 1273 to 1645 TF, removing the barrier + vmcnt wait to 1383, removing the operand
+//    reads to 1454, all three 1945; pieces that always hit L2 1453.  So the stage fetch is the
+//    cost -- its issue and its memory latency, not LDS bandwidth.  Register staging (global
+//    loads + ds_write_b128 one stage ahead) measured 1220 TF, i.e. worse; a fifth ring buffer
+//    (one more stage of DMA lookahead) +4.6 %; staggering the two halves' DMA issue +1 % alone
+//    and -2 % on top of the fifth buffer (profiles/gemm_dw_r3.md).
 #include "common.h"
 
 using namespace kf;
@@ -42,9 +49,10 @@ typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 
 namespace gm {
 // K rows are staged BK at a time into an NBUF-deep LDS ring (KF_GEMM_NBUF: 4 = 128 KB, 5 = the
-// full 160 KB, DMA one stage further ahead)
+// full 160 KB with the DMA one stage further ahead: 1,316-1,319 vs 1,256-1,262 TF over the
+// step's dW shapes at K = 32768 on one box, bit-identical output; profiles/gemm_dw_r3.md)
 #ifndef KF_GEMM_NBUF
-#define KF_GEMM_NBUF 4
+#define KF_GEMM_NBUF 5
 #endif
 constexpr int BM = 256, BN = 256, BK = 32, NBUF = KF_GEMM_NBUF;
 static_assert(NBUF == 4 || NBUF == 5, "ring depth");
@@ -326,7 +334,7 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_kernel(TnGroup grp, int K) {
 
 static bool tn_shape_ok(const void* A, long lda, const void* B, long ldb, const void* C, long ldc, int M, int N,
                         int K) {
-  if (M % BM || N % BN || K % (NBUF == 4 ? BK * NBUF : BK) || K < BK * NBUF || lda % 8 || ldb % 8 || ldc % 4) return false;
+  if (M % BM || N % BN || K % (NBUF == 4 ? BK * NBUF : BK) || K < BK || lda % 8 || ldb % 8 || ldc % 4) return false;
   return !(((uintptr_t)A | (uintptr_t)B) & 15) && !((uintptr_t)C & 7);
 }
 

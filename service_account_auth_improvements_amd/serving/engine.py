@@ -95,6 +95,7 @@ class Engine:
             from ..parallel.custom_ar import OneShotAllReduce
             self.car = OneShotAllReduce(model.st.tp_group)
         self._graphs: Dict[int, tuple] = {}
+        self._staging: Dict[int, tuple] = {}   # bucket -> (pinned host [3, Bb], device [3, Bb], copy-done event)
 
     # ------------------------------------------------------------------ helpers
     def _logits_full(self, y):
@@ -265,9 +266,22 @@ class Engine:
             raise ValueError(f"decode batch {B} exceeds the largest graph bucket {BUCKETS[-1]}")
         graph, gt, gs, gp, gl, out = self._graph_for(Bb)
         pad = Bb - B
-        host = torch.tensor([tokens + [0] * pad, slots + [self.scratch] * pad, pos + [0] * pad],
-                            dtype=torch.int64).pin_memory()
-        dev_rows = host.to(self.dev, non_blocking=True)
+        # one pinned staging buffer per bucket, reused every step (allocating and pinning a
+        # fresh host tensor per token costs more than the copy); the event keeps the next step
+        # from overwriting it while the previous step's async copy may still read it
+        st = self._staging.get(Bb)
+        if st is None:
+            st = self._staging[Bb] = (torch.empty((3, Bb), dtype=torch.int64).pin_memory(),
+                                      torch.empty((3, Bb), dtype=torch.int64, device=self.dev),
+                                      torch.cuda.Event())
+        host, dev_rows, done = st
+        done.synchronize()
+        h = host.numpy()
+        h[0, :B], h[1, :B], h[2, :B] = tokens, slots, pos
+        if pad:
+            h[0, B:], h[1, B:], h[2, B:] = 0, self.scratch, 0
+        dev_rows.copy_(host, non_blocking=True)
+        done.record()
         gt.copy_(dev_rows[0])
         gs.copy_(dev_rows[1])
         gp.copy_(dev_rows[2])
