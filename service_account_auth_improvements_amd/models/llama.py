@@ -92,6 +92,30 @@ class LlamaConfig:
         return 6 * n_mm + attn
 
 
+def _run(gen):
+    """Drive a generator to completion and return its value."""
+    while True:
+        try:
+            next(gen)
+        except StopIteration as e:
+            return e.value
+
+
+def _interleave(gens):
+    """Alternate independent generators (one step each in turn) until all have returned; the
+    values come back in order.  A step ends where a generator yielded after launching an
+    asynchronous collective, so each one's communication overlaps the others' compute."""
+    out, live = [None] * len(gens), list(range(len(gens)))
+    while live:
+        for k in list(live):
+            try:
+                next(gens[k])
+            except StopIteration as e:
+                out[k] = e.value
+                live.remove(k)
+    return out
+
+
 class _LayerCtx:
     __slots__ = ("h1", "rstd1", "a", "qkv", "o", "o_tok", "lse", "h2", "rstd2", "m", "gu", "s")
 
@@ -371,10 +395,24 @@ class Llama:
 
     # ------------------------------------------------------------------ decoder layer
     def layer_fwd(self, i: int, r: torch.Tensor, d: Optional[torch.Tensor], B: int, S: int):
+        return _run(self._layer_fwd_steps(i, r, d, B, S, interleave=False))
+
+    def _layer_fwd_steps(self, i: int, r: torch.Tensor, d: Optional[torch.Tensor], B: int, S: int,
+                         interleave: bool):
+        """One decoder layer's forward as a generator.  ``interleave=False``: never yields (the
+        TP collectives overlap their own GEMM chunks, :meth:`_row_parallel`).  ``interleave=True``:
+        each TP collective is launched asynchronously and the generator yields right after, so a
+        caller alternating two independent half-batches (:meth:`stage_forward_dual`) runs one
+        half's GEMMs / attention while the other half's reduction is on the wire."""
         cfg = self.cfg
         c = _LayerCtx()
         a, h1, rstd1 = ops.rmsnorm_fwd(r, self.P(f"l{i}.norm1"), cfg.norm_eps, residual=d)
-        qkv = self._col_parallel(a, self.P(f"l{i}.wqkv"))
+        if interleave and self._sp:
+            pend = tp_all_gather_rows(a, self.st, self.tp_comm_chunks, async_op=True)
+            yield
+            qkv = torch.mm(self._finish(pend), self.P(f"l{i}.wqkv").t())
+        else:
+            qkv = self._col_parallel(a, self.P(f"l{i}.wqkv"))
         D, cp = cfg.head_dim, self.cp
         hq, hkv, Sa = self.hq // cp, self.hkv // cp, S * cp
         if cp > 1:   # own tokens x all heads -> all tokens x own head group
@@ -382,12 +420,27 @@ class Llama:
         ops.rope_(qkv, hq + hkv, D, self.cos, self.sin, seq_len=Sa)
         o, lse = attention_fwd(qkv, B, Sa, hq, hkv, D)
         o_tok = cpx.to_tokens(o, B, S, [hq * D], cp, self.cp_group) if cp > 1 else o
-        da = self._row_parallel(o_tok, self.P(f"l{i}.wo"))
+        if interleave:
+            pend = self._reduce_out_async(torch.mm(o_tok, self.P(f"l{i}.wo").t()))
+            yield
+            da = self._finish(pend)
+        else:
+            da = self._row_parallel(o_tok, self.P(f"l{i}.wo"))
         m, h2, rstd2 = ops.rmsnorm_fwd(h1, self.P(f"l{i}.norm2"), cfg.norm_eps, residual=da)
         del da
-        gu = self._col_parallel(m, self.P(f"l{i}.wgu"))
+        if interleave and self._sp:
+            pend = tp_all_gather_rows(m, self.st, self.tp_comm_chunks, async_op=True)
+            yield
+            gu = torch.mm(self._finish(pend), self.P(f"l{i}.wgu").t())
+        else:
+            gu = self._col_parallel(m, self.P(f"l{i}.wgu"))
         s = ops.swiglu_fwd(gu)
-        dm = self._row_parallel(s, self.P(f"l{i}.wd"))
+        if interleave:
+            pend = self._reduce_out_async(torch.mm(s, self.P(f"l{i}.wd").t()))
+            yield
+            dm = self._finish(pend)
+        else:
+            dm = self._row_parallel(s, self.P(f"l{i}.wd"))
         c.h1, c.rstd1, c.a, c.qkv, c.o, c.o_tok, c.lse = h1, rstd1, a, qkv, o, o_tok, lse
         c.h2, c.rstd2, c.m, c.gu, c.s = h2, rstd2, m, gu, s
         return h2, dm, c
@@ -587,6 +640,33 @@ class Llama:
             return loss, ctx
         out = r + d if d is not None else r
         return out, ctx
+
+    def stage_forward_dual(self, halves, B: int, S: int, scale: float):
+        """Forward of two independent half micro-batches ``[(tokens [B*S], labels [B*S]), ...]``
+        (single-stage model) with their layers interleaved at every TP collective: half A's
+        all-reduce (or SP reduce-scatter / all-gather) is on the wire while half B's GEMMs and
+        attention run, and the other way round -- at TP=8 over xGMI each forward reduction costs
+        several times its producing GEMM, so this hides what the chunked form cannot.  Returns
+        [(loss, ctx)] per half; each is then passed to :meth:`stage_backward` like a micro-batch."""
+        assert self.first and self.last, "dual-batch forward needs the whole model on this stage"
+        ctxs, state = [{"layers": [], "tokens": t} for t, _ in halves], []
+        self._wait("embed", "embed")
+        for (t, _), ctx in zip(halves, ctxs):
+            state.append((self.embed_fwd(t), None))
+        for i in self.layers:
+            self._wait_layer(i)
+            res = _interleave([self._layer_fwd_steps(i, r, d, B, S, interleave=True) for r, d in state])
+            state = []
+            for (r, d, c), ctx in zip(res, ctxs):
+                ctx["layers"].append(c)
+                state.append((r, d))
+        self._wait("lm_head", "lm_head")
+        self._wait("final_norm", "final_norm", self.norms)
+        out = []
+        for (r, d), (_, lab), ctx in zip(state, halves, ctxs):
+            loss, ctx["head"] = self.head_fwd(r, d, lab, scale)
+            out.append((loss, ctx))
+        return out
 
     def stage_backward(self, ctx, grad_out: Optional[torch.Tensor], B: int, S: int,
                        accumulate: bool):

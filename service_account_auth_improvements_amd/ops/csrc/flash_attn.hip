@@ -187,14 +187,20 @@ __device__ __forceinline__ bf16x8 fold_const(float c, int hh) {
 //    gone.  (Measured: +10 % over the FMA form; an MFMA row sum instead of the 32 VALU adds
 //    and static younger-half priority were both slower or null.)
 //  * V^T fragments for output block t+1 are read while block t's MFMAs run.
-constexpr int BQ8 = 256, NST = 4, STG = 2 * TILE;   // stage = K tile + V tile (32 KB)
+// K+V ring depth of the forward and dQ kernels (KF_FA_NST: 4 = 128 KB, 5 = all 160 KB of LDS)
+#ifndef KF_FA_NST
+#define KF_FA_NST 4
+#endif
+constexpr int BQ8 = 256, NST = KF_FA_NST, STG = 2 * TILE;   // stage = K tile + V tile (32 KB)
+static_assert(NST * STG <= 163840, "LDS");
 constexpr float FOLD_T = 8.f;                       // tolerated growth of p above 1 (log2)
 
 // wait until stage `next` landed, given that stages up to `last` were issued (4 DMA
 // instructions per wave per stage, retired in order)
 __device__ __forceinline__ void wait_stage(int next, int last) {
   const int ahead = last - next;
-  if (ahead >= 2) vm_wait<8>();
+  if (ahead >= 3) vm_wait<12>();
+  else if (ahead >= 2) vm_wait<8>();
   else if (ahead == 1) vm_wait<4>();
   else vm_wait<0>();
 }

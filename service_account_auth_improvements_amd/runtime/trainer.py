@@ -52,6 +52,10 @@ class TrainConfig:
     # TP forward communication overlap: token chunks per row-/column-parallel projection
     # (models/llama.py _row_parallel / _col_parallel); 1 = one GEMM + one blocking collective
     tp_comm_chunks: int = 4
+    # TP forward: split each micro-batch into two half-batches whose layers are interleaved at
+    # every TP collective (models/llama.py stage_forward_dual); needs an even micro-batch, one
+    # pipeline stage and no recomputation.  Same arithmetic as grad_accum x2 at half the size.
+    tp_dual_batch: bool = True
 
 
 class Trainer:
@@ -81,9 +85,12 @@ class Trainer:
         self.init_times = {"params_alloc_init_s": time.time() - t0}
         t0 = time.time()
         mode = "reduce_scatter" if (tcfg.zero1 and (self.st.dp > 1 or tcfg.force_collectives)) else "allreduce"
+        # dual half-batch TP forward (tp_dual_batch): each micro-batch becomes two accumulated halves
+        self.dual = (self.st.tp > 1 and getattr(tcfg, "tp_dual_batch", False) and tcfg.micro_batch % 2 == 0
+                     and not tcfg.recompute and self.cp == 1)
         self.reducer = GradReducer(self.model.groups, self.st.dp_group, self.st.dp,
                                    bucket_bytes=tcfg.bucket_mb << 20, mode=mode,
-                                   reduce_dtype=tcfg.grad_reduce, grad_accum=tcfg.grad_accum,
+                                   reduce_dtype=tcfg.grad_reduce, grad_accum=tcfg.grad_accum * (2 if self.dual else 1),
                                    force_collectives=tcfg.force_collectives)
         # identical replicas: broadcast from the first rank of this DP group (C2)
         if self.st.dp > 1:
@@ -157,7 +164,23 @@ class Trainer:
         self.reducer.start_step()
         f32acc = self.reducer.fp32_accumulation
         total = None
-        for j, (tok, lab) in enumerate(micro_batches):
+        dual = self.dual and all(t.shape[0] % 2 == 0 for t, _ in micro_batches)
+        if dual:      # every micro-batch as two interleaved halves: 2n backward passes
+            parts = []
+            for tok, lab in micro_batches:
+                Bh, S = tok.shape[0] // 2, tok.shape[1]
+                halves = [(tok[k * Bh:(k + 1) * Bh].reshape(-1), lab[k * Bh:(k + 1) * Bh].reshape(-1)) for k in (0, 1)]
+                parts.append((self.model.stage_forward_dual(halves, Bh, S, scale), Bh, S))
+            nb, j = 2 * n, 0
+            for fwd, Bh, S in parts:
+                for loss, ctx in fwd:
+                    self.model.on_grad_ready = self.reducer.grad_ready if j == nb - 1 else None
+                    self.model.stage_backward(ctx, None, Bh, S, accumulate=j > 0 and not f32acc)
+                    if j < nb - 1:
+                        self.reducer.accumulate_micro(first=j == 0)
+                    total = loss if total is None else total + loss
+                    j += 1
+        for j, (tok, lab) in enumerate([] if dual else micro_batches):
             self.model.on_grad_ready = self.reducer.grad_ready if j == n - 1 else None
             loss = self.model.forward_backward(tok, lab, accumulate=j > 0 and not f32acc, scale=scale)
             if j < n - 1:

@@ -178,7 +178,7 @@ def _chunk_body(rank, world, chunks, sp):
     from service_account_auth_improvements_amd.runtime.trainer import TrainConfig, Trainer
     st = init_distributed(tp=world, pp=1, device="cpu")
     tr = Trainer(TrainConfig(model="tiny", seq_len=32, micro_batch=2, n_layers=2, lr=LR, sequence_parallel=sp,
-                             tp_comm_chunks=chunks), st, full_init=True)
+                             tp_comm_chunks=chunks, tp_dual_batch=False), st, full_init=True)
     assert tr.model.tp_comm_chunks == chunks
     losses = [float(tr.train_step(_batches(tr.mcfg.vocab_size, 1, seed=500 + s))) for s in range(STEPS)]
     return dict(losses=losses, params={s.name: tr.model.P(s.name).float() for g in tr.model.groups
@@ -194,6 +194,35 @@ def test_tp_chunked_forward_overlap_is_bit_identical(sp):
     one = run_ranks(_chunk_body, world=2, args=(1, sp))
     four = run_ranks(_chunk_body, world=2, args=(4, sp))
     for a, b in zip(one, four):
+        assert a["losses"] == b["losses"]
+        for name in a["params"]:
+            assert torch.equal(a["params"][name], b["params"][name]), name
+
+
+def _dual_body(rank, world, dual, sp, mb, accum):
+    from service_account_auth_improvements_amd.parallel.state import init_distributed
+    from service_account_auth_improvements_amd.runtime.trainer import TrainConfig, Trainer
+    st = init_distributed(tp=world, pp=1, device="cpu")
+    tr = Trainer(TrainConfig(model="tiny", seq_len=32, micro_batch=mb, grad_accum=accum, n_layers=2, lr=LR,
+                             sequence_parallel=sp, tp_dual_batch=dual), st, full_init=True)
+    assert tr.dual == dual
+    losses = []
+    for s in range(STEPS):
+        (tok, lab), = _batches(tr.mcfg.vocab_size, 1, B=4, seed=700 + s)
+        mbs = [(tok[k * mb:(k + 1) * mb], lab[k * mb:(k + 1) * mb]) for k in range(4 // mb)]
+        losses.append(float(tr.train_step(mbs)))
+    return dict(losses=losses, params={s.name: tr.model.P(s.name).float() for g in tr.model.groups
+                                       for s in g.specs})
+
+
+@pytest.mark.parametrize("sp", [False, True], ids=["tp2", "tp2+sp"])
+def test_tp_dual_batch_forward_equals_two_accumulated_micro_batches(sp):
+    """The dual half-batch forward (two halves' layers interleaved at every TP collective) is
+    the same arithmetic as grad_accum 2 at half the micro-batch: bit-identical losses and
+    parameters (two ranks: sums of two are order-free)."""
+    dual = run_ranks(_dual_body, world=2, args=(True, sp, 4, 1))
+    acc = run_ranks(_dual_body, world=2, args=(False, sp, 2, 2))
+    for a, b in zip(dual, acc):
         assert a["losses"] == b["losses"]
         for name in a["params"]:
             assert torch.equal(a["params"][name], b["params"][name]), name
