@@ -55,7 +55,9 @@ class TrainConfig:
     # TP forward: split each micro-batch into two half-batches whose layers are interleaved at
     # every TP collective (models/llama.py stage_forward_dual); needs an even micro-batch, one
     # pipeline stage and no recomputation.  Same arithmetic as grad_accum x2 at half the size.
-    tp_dual_batch: bool = True
+    # Off by default: on the 70B TP=8 shard it costs 17 % compute (half-size GEMMs, an fp32
+    # accumulation pass, +33 GiB) -- profiles/llama3_70b_tp8_shard.md.
+    tp_dual_batch: bool = False
 
 
 class Trainer:

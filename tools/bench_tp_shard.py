@@ -42,6 +42,8 @@ def main():
     ap.add_argument("--recompute", action="store_true")
     ap.add_argument("--tp-comm-chunks", type=int, default=4,
                     help="token chunks per TP projection (forward comm/compute overlap; 1 = off)")
+    ap.add_argument("--tp-dual-batch", type=int, default=0,
+                    help="1: split an even micro-batch into two halves interleaved at every TP collective")
     ap.add_argument("--busbw-gbs", type=float, default=300.0,
                     help="assumed RCCL all-reduce bus bandwidth over xGMI for the wire-time estimate")
     a = ap.parse_args()
@@ -56,7 +58,7 @@ def main():
     set_state(st)
     t0 = time.time()
     tr = Trainer(TrainConfig(model=a.model, seq_len=a.seq_len, micro_batch=a.micro_batch, recompute=a.recompute,
-                                 tp_comm_chunks=a.tp_comm_chunks), st)
+                                 tp_comm_chunks=a.tp_comm_chunks, tp_dual_batch=bool(a.tp_dual_batch)), st)
     torch.cuda.synchronize()
     init_s = time.time() - t0
     data = SyntheticData(tr.mcfg.vocab_size, a.micro_batch, a.seq_len, dev, seed=1)
