@@ -93,6 +93,25 @@ def skinny_gemm(x, w, swiglu: bool = False):
     return y.to(x.dtype)
 
 
+def bgemm_ok(x, w, swiglu: bool = False) -> bool:
+    """True when the batched-decode GEMM (ops/csrc/bgemm.hip) takes x [M, K] . w^T."""
+    return (x.is_cuda and 1 <= x.shape[0] <= 256 and x.shape[1] % 256 == 0 and w.shape[0] % 64 == 0
+            and x.stride(1) == 1 and x.stride(0) % 8 == 0 and w.is_contiguous())
+
+
+def bgemm(x, w, swiglu: bool = False, splits: int = 0):
+    """Batched-decode GEMM x[M<=256, K] . w[N, K]^T: the HIP weight-streaming MFMA kernel on
+    the GPU (K split ``splits`` ways, 0 = automatic).  ``swiglu``: w = [gate; up] ->
+    silu(x.gate^T) * (x.up^T)."""
+    if x.is_cuda:
+        return _k().bgemm(x, w, bool(swiglu), int(splits))
+    y = torch.mm(x.float(), w.float().t())
+    if swiglu:
+        F_ = y.shape[1] // 2
+        y = torch.nn.functional.silu(y[:, :F_]) * y[:, F_:]
+    return y.to(x.dtype)
+
+
 def skinny_gemm_norm_ok(x, K: int) -> bool:
     """True when the fused residual+RMSNorm decode GEMM handles these rows."""
     return x.is_cuda and x.shape[0] <= 4 and x.shape[0] * K <= 32768 and K % 256 == 0

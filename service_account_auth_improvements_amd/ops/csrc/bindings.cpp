@@ -47,6 +47,8 @@ int kf_kv_fill(const void*, long, int, int, int, int, int, void*, void*, int, hi
 int kf_embed_fwd(const long*, const void*, void*, int, int, long, long, hipStream_t);
 int kf_embed_bwd(const long*, const long*, const void*, void*, int, int, long, long, int, hipStream_t);
 int kf_skinny_gemm(const void*, long, int, const void*, int, int, void*, long, int, int, hipStream_t);
+int kf_bgemm_splits(int, int, int);
+int kf_bgemm(const void*, long, int, const void*, int, int, void*, long, int, int, int, float*, hipStream_t);
 int kf_gemv(const void*, long, int, const void*, const void*, float, void*, long, const void*, int, int, void*, long,
             int, int, hipStream_t);
 int kf_gemv_norm_rope(const void*, long, int, const void*, const void*, float, void*, long, const void*, int, int,
@@ -449,6 +451,28 @@ at::Tensor skinny_gemm(const at::Tensor& x, const at::Tensor& w, bool swiglu) {
   return y;
 }
 
+// Batched-decode GEMM (17..256 rows): y = x . w^T, or silu(x . gate^T) * (x . up^T) with
+// w = [gate; up] when swiglu.  splits = 0 picks the K split (kf_bgemm_splits); the fp32
+// partials of a split launch live in a workspace from the caching allocator.
+at::Tensor bgemm(const at::Tensor& x, const at::Tensor& w, bool swiglu, int64_t splits) {
+  check_bf16_cuda(x, "x");
+  check_bf16_cuda(w, "w");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && w.dim() == 2 && w.is_contiguous(), "bgemm: 2-D operands");
+  const int64_t M = x.size(0), K = x.size(1), Nw = w.size(0);
+  TORCH_CHECK(w.size(1) == K, "bgemm: K mismatch");
+  TORCH_CHECK(M >= 1 && M <= 256 && K % 256 == 0 && Nw % 64 == 0, "bgemm: needs 1 <= M <= 256, K % 256 == 0, N % 64 == 0");
+  const int64_t N = swiglu ? Nw / 2 : Nw;
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  auto y = at::empty({M, N}, x.options());
+  const int S = splits > 0 ? (int)splits : kf_bgemm_splits((int)M, (int)Nw, (int)K);
+  at::Tensor part;
+  if (S > 1) part = at::empty({(int64_t)S * M * Nw}, x.options().dtype(at::kFloat));
+  check_rc(kf_bgemm(x.data_ptr(), x.stride(0), (int)M, w.data_ptr(), (int)Nw, (int)K, y.data_ptr(), y.stride(0),
+                    swiglu ? 1 : 0, (int)N, S, S > 1 ? part.data_ptr<float>() : nullptr, cur_stream()),
+           "bgemm");
+  return y;
+}
+
 // Decode GEMM with the residual-add + RMSNorm fused in as a prologue:
 //   h = x (+ res);  y = (rmsnorm(h) * nw) . w^T  [SwiGLU epilogue when swiglu].
 // Returns (y, h); h aliases x when res is None.  Needs M <= 8 and M * K <= 32768.
@@ -640,6 +664,7 @@ TORCH_LIBRARY(kfamd, m) {
   m.def("flash_bwd", &flash_bwd);
   m.def("decode_attn", &decode_attn);
   m.def("skinny_gemm", &skinny_gemm);
+  m.def("bgemm(Tensor x, Tensor w, bool swiglu, int splits) -> Tensor", &bgemm);
   m.def("skinny_gemm_norm", &skinny_gemm_norm);
   m.def("transpose_bf16", &transpose_bf16);
   m.def("car_alloc", &car_alloc);

@@ -47,6 +47,13 @@ BUCKETS = (1, 2, 4, 8, 16, 32, 64, 128, 256)
 SKINNY_MAX_ROWS = min(64, int(os.environ.get("KFAMD_SKINNY_MAX_ROWS", "16")))
 SKINNY_MAX_N = 32768          # beyond this (LM head) hipBLASLt streams faster than the MFMA skinny kernel
 GEMV_MAX_ROWS = 4             # ... but not than the VALU GEMV (ops/csrc/gemv.hip) the 1-4 row case takes
+# above SKINNY_MAX_ROWS the narrow projections (N <= 4096: wo, wd) go to the batched-decode GEMM
+# (ops/csrc/bgemm.hip: W streamed into registers, K split over the CUs) up to BGEMM_MAX_ROWS;
+# hipBLASLt's tiles leave most CUs idle there.  The wide ones (wqkv ties, gate/up and the LM
+# head lose) stay on hipBLASLt (profiles/serve_bgemm.md).  KFAMD_BGEMM=0: off.
+BGEMM = os.environ.get("KFAMD_BGEMM", "1") != "0"
+BGEMM_MAX_N = 4096
+BGEMM_MIN_ROWS, BGEMM_MAX_ROWS = 33, 128   # at 32 rows its reduce launch costs more than it saves
 # prompts admitted in one scheduler iteration are prefilled together up to this many tokens
 PREFILL_MAX_TOKENS = int(os.environ.get("KFAMD_PREFILL_MAX_TOKENS", "16384"))
 PREFILL_PAD_RATIO = 1.25      # ... in length groups padded to at most 1.25x
@@ -183,11 +190,19 @@ class Engine:
             return self.car(x)
         return tp_all_reduce(x, self.m.st)
 
+    def _use_bgemm(self, x, w) -> bool:
+        return (BGEMM and max(SKINNY_MAX_ROWS + 1, BGEMM_MIN_ROWS) <= x.shape[0] <= BGEMM_MAX_ROWS
+                and w.shape[0] <= BGEMM_MAX_N
+                and ops.bgemm_ok(x, w))
+
     def _mm(self, x, w):
-        """Decode GEMM: the skinny weight-streaming kernel for small batches on the GPU."""
+        """Decode GEMM: the skinny weight-streaming kernels for small batches on the GPU, the
+        batched-decode GEMM up to 256 rows, hipBLASLt beyond."""
         if x.is_cuda and (x.shape[0] <= GEMV_MAX_ROWS or (
                 x.shape[0] <= SKINNY_MAX_ROWS and w.shape[0] <= SKINNY_MAX_N and w.shape[1] % 256 == 0)):
             return ops.skinny_gemm(x, w)
+        if self._use_bgemm(x, w):
+            return ops.bgemm(x, w)
         return torch.mm(x, w.t())
 
     def _decode_mlp(self, i, h1, da):
@@ -200,6 +215,8 @@ class Engine:
         mm, h2, _ = ops.rmsnorm_fwd(h1, m.P(f"l{i}.norm2"), cfg.norm_eps, residual=da)
         if mm.is_cuda and (mm.shape[0] <= GEMV_MAX_ROWS or (mm.shape[0] <= SKINNY_MAX_ROWS and wgu.shape[1] % 256 == 0)):
             s = ops.skinny_gemm(mm, wgu, swiglu=True)          # gate/up GEMM + SwiGLU in one kernel
+        elif mm.is_cuda and self._use_bgemm(mm, wgu):
+            s = ops.bgemm(mm, wgu, swiglu=True)
         else:
             s = ops.swiglu_fwd(torch.mm(mm, wgu.t()))
         return h2, self._tp_ar(self._mm(s, m.P(f"l{i}.wd")))

@@ -225,3 +225,37 @@ def test_decode_attn_repeated_calls_stable():
     assert torch.equal(o, first)
     ref = _ref_decode(qkv, kc, vc, slots, lens, 32)
     assert (first.float().cpu() - ref).abs().max().item() < 2e-2
+
+
+@pytest.mark.parametrize("M", [17, 32, 64, 65, 128, 129, 200, 256])
+@pytest.mark.parametrize("swiglu", [False, True], ids=["plain", "swiglu"])
+def test_bgemm_matches_fp32(M, swiglu):
+    """Batched-decode GEMM (ops/csrc/bgemm.hip) vs an fp32 reference, every MT bucket and its
+    M padding, each K split (the fp32 partials + reduce launch included)."""
+    from service_account_auth_improvements_amd import ops
+    g = torch.Generator(device="cpu").manual_seed(M + 1000 * swiglu)
+    K, Nw = 2048, 512
+    x = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+    w = (torch.randn(Nw, K, generator=g) * 0.05).to(DEV, torch.bfloat16)
+    ref = torch.mm(x.float(), w.float().t())
+    if swiglu:
+        ref = torch.nn.functional.silu(ref[:, :Nw // 2]) * ref[:, Nw // 2:]
+    for S in (0, 1, 2, 4, 8):
+        y = ops.bgemm(x, w, swiglu=swiglu, splits=S)
+        torch.cuda.synchronize()
+        err = ((y.float() - ref).abs().max() / ref.abs().max()).item()
+        assert err < 1e-2, (S, err)
+
+
+def test_bgemm_decode_shapes_and_strided_rows():
+    """The Llama-3-8B decode projections at batch 128, and X rows with a stride (a view)."""
+    from service_account_auth_improvements_amd import ops
+    g = torch.Generator(device="cpu").manual_seed(7)
+    for N, K in ((6144, 4096), (4096, 4096), (4096, 14336)):
+        xb = torch.randn(128, K + 64, generator=g).to(DEV, torch.bfloat16)
+        x = xb[:, :K]                                   # row stride K + 64
+        w = (torch.randn(N, K, generator=g) * 0.02).to(DEV, torch.bfloat16)
+        y = ops.bgemm(x, w)
+        ref = torch.mm(x.float(), w.float().t())
+        err = ((y.float() - ref).abs().max() / ref.abs().max()).item()
+        assert err < 1e-2, (N, K, err)
