@@ -181,7 +181,7 @@ def main():
     st = init_distributed(tp=a.tp, pp=a.pp)
     world = st.world_size
     if a.zero1 is None:
-        a.zero1 = (st.dp > 1 or a.force_collectives) and a.pp == 1
+        a.zero1 = st.dp > 1 or a.force_collectives
     if a.micro_batch <= 0:
         big = (st.device.type == "cuda" and torch.cuda.get_device_properties(st.device).total_memory >= 280e9
                and a.model == "llama3-8b" and a.seq_len // (st.dp if a.cp else 1) <= 8192 and a.tp == 1

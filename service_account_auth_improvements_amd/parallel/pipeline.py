@@ -8,8 +8,9 @@ stage pair has a direct link, so a stage hop is a single point-to-point transfer
 Schedule (non-interleaved 1F1B): stage r runs ``pp - r - 1`` warm-up forwards, then
 alternates one forward / one backward, then drains the remaining backwards.  Send and
 receive of opposite directions are posted together through ``batch_isend_irecv`` so no
-ordering of blocking calls can deadlock.  Only ``pp - r`` micro-batches of activations
-are ever alive on stage r.
+ordering of blocking calls can deadlock; send-only groups are left in flight behind the next
+micro-batch's compute (:class:`P2P`).  Only ``pp - r`` micro-batches of activations are ever
+alive on stage r.  With ``zero1`` every stage's DP group shards its optimizer state (ZeRO-1).
 """
 from __future__ import annotations
 
@@ -36,18 +37,41 @@ def stage_layers(n_layers: int, pp: int, rank: int) -> range:
 
 
 class P2P:
+    """Stage-boundary point-to-point transfers.  A group that only SENDS is not waited for: the
+    compute stream goes on with the next micro-batch while the activation (or its gradient)
+    is on the wire -- at micro-batch 4 x 8k tokens a boundary tensor is 268 MB, several ms on
+    one xGMI link.  Its tensor is kept alive until :meth:`flush` (end of the step).  Receives
+    are waited for (a stream dependency under RCCL) before their data is used.  Every group
+    pairs with one posted by the peer in the same order, and a receive is never posted ahead
+    of a send the peer needs first: RCCL runs P2P groups in order on one stream."""
+
     def __init__(self, st: ParallelState, shape, dtype, device):
         self.st, self.shape, self.dtype, self.device = st, shape, dtype, device
         # gloo (the one-GPU rehearsal backend) moves send/recv payloads without ordering them
         # against the HIP stream, so GPU tensors are staged through host memory there; RCCL
         # orders its own stream against the compute stream.
         self._host = torch.device(device).type == "cuda" and dist.get_backend() == "gloo"
+        self._inflight: list = []       # (works, tensors) of send-only groups not yet waited for
+        self.sends_deferred = 0         # send-only groups left in flight (tests)
 
     def _buf(self):
         return torch.empty(self.shape, dtype=self.dtype, device=self.device)
 
+    def flush(self):
+        """Wait for every deferred send (before the optimizer step reuses any buffer)."""
+        for works, _ in self._inflight:
+            for w in works:
+                w.wait()
+        self._inflight.clear()
+
     def _run(self, ops):
         if not ops:
+            return
+        if all(op.op is dist.isend for op in ops):
+            if self._host:
+                ops = [dist.P2POp(dist.isend, op.tensor.cpu(), op.peer) for op in ops]
+            self._inflight.append((dist.batch_isend_irecv(ops), [op.tensor for op in ops]))
+            self.sends_deferred += 1
             return
         copies = []
         if self._host:
@@ -159,6 +183,7 @@ def one_f_one_b(model: Llama, p2p: P2P, micro_batches: List[Tuple[torch.Tensor, 
         p2p.send_backward(bwd(g))
     if on_last_backward is not None:
         on_last_backward(False)
+    p2p.flush()
     for lv in losses:
         total = lv if total is None else total + lv
     return total
@@ -185,17 +210,32 @@ class PipelineTrainer:
         if self.st.tp > 1:
             self.model.tp_comm_chunks = getattr(tcfg, "tp_comm_chunks", self.model.tp_comm_chunks)
         assert not getattr(tcfg, "context_parallel", False), "context parallelism is not combined with PP"
-        self.model.allocate()
+        zero1 = getattr(tcfg, "zero1", False)
+        force = getattr(tcfg, "force_collectives", False)
+        self.model.allocate(pad_to=st.dp * 64 if zero1 else 1)
+        # ZeRO-1 per stage: each DP replica group of a stage reduce-scatters its gradients, owns
+        # 1/dp of the stage's AdamW state and all-gathers the updated parameters, which the next
+        # step's forward waits for bucket by bucket (as the flat DP trainer does)
+        mode = "reduce_scatter" if zero1 and (st.dp > 1 or force) else "allreduce"
         self.reducer = GradReducer(self.model.groups, st.dp_group, st.dp,
-                                   bucket_bytes=tcfg.bucket_mb << 20,
+                                   bucket_bytes=tcfg.bucket_mb << 20, mode=mode,
                                    reduce_dtype=getattr(tcfg, "grad_reduce", "bf16"),
-                                   grad_accum=tcfg.grad_accum)
+                                   grad_accum=tcfg.grad_accum, force_collectives=force)
+        if st.dp > 1:       # identical replicas of this stage: broadcast from its first DP rank (C2)
+            self.reducer.broadcast_params(st.rank - st.dp_rank * st.tp)
+        shard = None
+        if mode == "reduce_scatter":
+            shard = {g.name: self.reducer.shard_ranges(g, st.dp_rank) for g in self.model.groups}
         self.opt = FlatAdamW(self.model.groups,
                              AdamWConfig(lr=tcfg.lr, weight_decay=tcfg.weight_decay,
                                          max_grad_norm=tcfg.max_grad_norm),
+                             shard_ranges=shard, dp_group=st.dp_group,
                              norm_groups=[st.pp_group] if st.pp > 1 else None,
                              tp_sharded={"matrices": st.tp_group} if st.tp > 1 else None,
                              grad_view=self.reducer.grad_view)
+        self.overlap_allgather = mode == "reduce_scatter" and getattr(tcfg, "overlap_allgather", True)
+        if self.overlap_allgather:
+            self.model.param_wait = self.reducer.wait_params
         T = tcfg.micro_batch * tcfg.seq_len
         if self.model.sequence_parallel and st.tp > 1:
             T //= st.tp                     # stages exchange this rank's block of token rows
@@ -209,7 +249,24 @@ class PipelineTrainer:
         ntok = sum(t.numel() for t, _ in micro_batches)
         self.reducer.start_step()
         loss = one_f_one_b(self.model, self.p2p, micro_batches, 1.0 / ntok, self._hook, reducer=self.reducer)
+        self.reducer.wait_all_params()     # a bucket the forward never read (padding) must land too
         self.reducer.finish()
         self.opt.step(grad_scale=1.0 / self.st.dp)
+        self.reducer.all_gather_params(overlap=self.overlap_allgather)
         self.step_idx += 1
         return loss
+
+    def sync_params(self):
+        """Complete in-flight ZeRO-1 parameter gathers (before checkpoint, eval or host reads)."""
+        self.reducer.wait_all_params()
+
+    def reduced_grads(self, group) -> torch.Tensor:
+        """fp32 copy of the DP-summed gradient of a flat group as the optimizer saw it (ZeRO-1:
+        this rank's shards only, NaN elsewhere)."""
+        r = self.reducer
+        if r.mode == "reduce_scatter" and r.enabled:
+            out = torch.full((group.numel,), float("nan"), device=group.grads.device)
+            for lo, hi in r.shard_ranges(group, self.st.dp_rank):
+                out[lo:hi] = r.grad_view(group, lo, hi).float()
+            return out
+        return r.grad_view(group, 0, group.numel).float().clone()

@@ -1,4 +1,4 @@
-"""4-rank (gloo) training on 2-D process meshes -- dp2 x tp2, dp2 x pp2, tp2 x pp2 -- against one
+"""4-rank (gloo) training on 2-D process meshes -- dp2 x tp2, dp2 x pp2 (ZeRO-1 per stage), tp2 x pp2 -- against one
 process running the same global batch, plus the fp32 DP gradient reduction and fp32 micro-batch
 accumulation against exact (float64) sums.
 
@@ -25,7 +25,7 @@ def _mesh_body(rank, world, tp, pp, n_micro, grad_reduce, sp=False):
     from service_account_auth_improvements_amd.runtime.trainer import TrainConfig, Trainer
     st = init_distributed(tp=tp, pp=pp, device="cpu")
     tcfg = TrainConfig(model="tiny", seq_len=32, micro_batch=2, grad_accum=n_micro, n_layers=4, lr=LR,
-                       zero1=st.dp > 1 and pp == 1, bucket_mb=1, grad_reduce=grad_reduce, sequence_parallel=sp)
+                       zero1=st.dp > 1, bucket_mb=1, grad_reduce=grad_reduce, sequence_parallel=sp)
     tr = PipelineTrainer(tcfg, st, full_init=True) if pp > 1 else Trainer(tcfg, st, full_init=True)
     losses = []
     for step in range(STEPS):
@@ -36,7 +36,10 @@ def _mesh_body(rank, world, tp, pp, n_micro, grad_reduce, sp=False):
     if hasattr(tr, "sync_params"):
         tr.sync_params()
     params = {s.name: tr.model.P(s.name).float().clone() for g in tr.model.groups for s in g.specs}
-    return dict(losses=losses, params=params, coords=(st.dp_rank, st.tp_rank, st.pp_rank), dp=st.dp)
+    deferred = tr.p2p.sends_deferred if pp > 1 else 0
+    zero1 = tr.reducer.mode == "reduce_scatter"
+    return dict(losses=losses, params=params, coords=(st.dp_rank, st.tp_rank, st.pp_rank), dp=st.dp,
+                deferred=deferred, zero1=zero1)
 
 
 def _reference(n_batches_per_step, n_layers=4):
@@ -60,6 +63,10 @@ def test_2d_mesh_training_matches_single_process(tp, pp, sp):
     n_micro = 2
     res = run_ranks(_mesh_body, world=world, args=(tp, pp, n_micro, "fp32", sp), timeout=600)
     ref, ref_losses = _reference(dp * n_micro)
+    # PP: send-only P2P groups are left in flight behind compute; dp > 1: ZeRO-1 on every stage
+    if pp > 1:
+        assert all(r["deferred"] > 0 for r in res), [r["deferred"] for r in res]
+    assert all(r["zero1"] == (dp > 1) for r in res)
     # every (dp, tp, pp) coordinate appears exactly once
     assert sorted(r["coords"] for r in res) == sorted((d, t, p) for d in range(dp) for t in range(tp)
                                                      for p in range(pp))
