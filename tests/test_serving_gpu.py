@@ -28,7 +28,10 @@ def _ref_decode(q2d, kc, vc, slots, lengths, Hq):
 
 @pytest.mark.parametrize("B,Hq,Hkv,Lmax,lens", [
     (1, 32, 8, 256, [1]), (3, 32, 8, 1024, [1000, 17, 512]), (8, 8, 8, 4096, [4096, 1, 100, 2049, 3000, 64, 65, 7]),
-    (2, 16, 2, 8192, [8192, 5000]), (4, 4, 4, 128, [128, 3, 64, 100])])
+    (2, 16, 2, 8192, [8192, 5000]), (4, 4, 4, 128, [128, 3, 64, 100]),
+    # one-pass streaming kernel (chunks >= 256 keys): ragged lengths, tails, an empty split
+    (32, 32, 8, 4096, [4096, 1, 17, 255, 256, 257, 1000, 3071] * 4),
+    (8, 64, 8, 16384, [16384, 9000, 1, 300, 5000, 16383, 2048, 7]), (16, 16, 2, 2048, [2048, 1500] * 8)])
 def test_decode_attn(B, Hq, Hkv, Lmax, lens):
     assert _ext.load()
     g = torch.Generator(device="cpu").manual_seed(B * 7 + Lmax)
