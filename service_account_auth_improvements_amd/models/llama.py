@@ -641,32 +641,45 @@ class Llama:
         out = r + d if d is not None else r
         return out, ctx
 
-    def stage_forward_dual(self, halves, B: int, S: int, scale: float):
-        """Forward of two independent half micro-batches ``[(tokens [B*S], labels [B*S]), ...]``
-        (single-stage model) with their layers interleaved at every TP collective: half A's
-        all-reduce (or SP reduce-scatter / all-gather) is on the wire while half B's GEMMs and
-        attention run, and the other way round -- at TP=8 over xGMI each forward reduction costs
-        several times its producing GEMM, so this hides what the chunked form cannot.  Returns
-        [(loss, ctx)] per half; each is then passed to :meth:`stage_backward` like a micro-batch."""
-        assert self.first and self.last, "dual-batch forward needs the whole model on this stage"
-        ctxs, state = [{"layers": [], "tokens": t} for t, _ in halves], []
+    def stage_forward_dual(self, tokens, labels, B: int, S: int, scale: float):
+        """Forward of one micro-batch ``tokens``/``labels`` [B*S] (single-stage model, TP > 1,
+        no SP, B even) as two half-batches whose layers are interleaved at every TP collective:
+        half A's all-reduce is on the wire while half B's GEMMs and attention run, and the other
+        way round -- at TP=8 over xGMI each forward reduction costs several times its producing
+        GEMM, so this hides what the chunked form cannot.  The halves' saved activations are then
+        concatenated into ONE full-batch context (rows in batch order) and the head runs once, so
+        the caller does one :meth:`stage_backward` as for the plain forward: no second backward,
+        no extra gradient accumulation.  Returns (loss placeholder, ctx)."""
+        assert self.first and self.last and not self._sp and B % 2 == 0
+        Bh, T = B // 2, B * S
+        half = T // 2
         self._wait("embed", "embed")
-        for (t, _), ctx in zip(halves, ctxs):
-            state.append((self.embed_fwd(t), None))
+        state = [(self.embed_fwd(tokens[:half]), None), (self.embed_fwd(tokens[half:]), None)]
+        ctx = {"layers": [], "tokens": tokens}
         for i in self.layers:
             self._wait_layer(i)
-            res = _interleave([self._layer_fwd_steps(i, r, d, B, S, interleave=True) for r, d in state])
-            state = []
-            for (r, d, c), ctx in zip(res, ctxs):
-                ctx["layers"].append(c)
-                state.append((r, d))
+            res = _interleave([self._layer_fwd_steps(i, r, d, Bh, S, interleave=True) for r, d in state])
+            (r0, d0, c0), (r1, d1, c1) = res
+            c = _LayerCtx()
+            for f in _LayerCtx.__slots__:
+                x0, x1 = getattr(c0, f), getattr(c1, f)
+                if f == "o_tok" and x0 is c0.o:
+                    setattr(c, f, None)           # aliases o (set below)
+                else:
+                    setattr(c, f, torch.cat([x0, x1], 0))
+            if c.o_tok is None:
+                c.o_tok = c.o
+            del c0, c1, res
+            ctx["layers"].append(c)
+            state = [(r0, d0), (r1, d1)]
+        (r0, d0), (r1, d1) = state
+        r = torch.cat([r0, r1], 0)
+        d = torch.cat([d0, d1], 0) if d0 is not None else None
+        del state, r0, r1, d0, d1
         self._wait("lm_head", "lm_head")
         self._wait("final_norm", "final_norm", self.norms)
-        out = []
-        for (r, d), (_, lab), ctx in zip(state, halves, ctxs):
-            loss, ctx["head"] = self.head_fwd(r, d, lab, scale)
-            out.append((loss, ctx))
-        return out
+        loss, ctx["head"] = self.head_fwd(r, d, labels, scale)
+        return loss, ctx
 
     def stage_backward(self, ctx, grad_out: Optional[torch.Tensor], B: int, S: int,
                        accumulate: bool):

@@ -53,10 +53,8 @@ class TrainConfig:
     # (models/llama.py _row_parallel / _col_parallel); 1 = one GEMM + one blocking collective
     tp_comm_chunks: int = 4
     # TP forward: split each micro-batch into two half-batches whose layers are interleaved at
-    # every TP collective (models/llama.py stage_forward_dual); needs an even micro-batch, one
-    # pipeline stage and no recomputation.  Same arithmetic as grad_accum x2 at half the size.
-    # Off by default: on the 70B TP=8 shard it costs 17 % compute (half-size GEMMs, an fp32
-    # accumulation pass, +33 GiB) -- profiles/llama3_70b_tp8_shard.md.
+    # every TP collective, then one full-batch backward (models/llama.py stage_forward_dual);
+    # needs an even micro-batch, one pipeline stage, no recomputation and no SP.
     tp_dual_batch: bool = False
 
 
@@ -87,12 +85,12 @@ class Trainer:
         self.init_times = {"params_alloc_init_s": time.time() - t0}
         t0 = time.time()
         mode = "reduce_scatter" if (tcfg.zero1 and (self.st.dp > 1 or tcfg.force_collectives)) else "allreduce"
-        # dual half-batch TP forward (tp_dual_batch): each micro-batch becomes two accumulated halves
+        # dual half-batch TP forward (tp_dual_batch, models/llama.py stage_forward_dual)
         self.dual = (self.st.tp > 1 and getattr(tcfg, "tp_dual_batch", False) and tcfg.micro_batch % 2 == 0
-                     and not tcfg.recompute and self.cp == 1)
+                     and not tcfg.recompute and self.cp == 1 and not tcfg.sequence_parallel)
         self.reducer = GradReducer(self.model.groups, self.st.dp_group, self.st.dp,
                                    bucket_bytes=tcfg.bucket_mb << 20, mode=mode,
-                                   reduce_dtype=tcfg.grad_reduce, grad_accum=tcfg.grad_accum * (2 if self.dual else 1),
+                                   reduce_dtype=tcfg.grad_reduce, grad_accum=tcfg.grad_accum,
                                    force_collectives=tcfg.force_collectives)
         # identical replicas: broadcast from the first rank of this DP group (C2)
         if self.st.dp > 1:
@@ -167,24 +165,15 @@ class Trainer:
         f32acc = self.reducer.fp32_accumulation
         total = None
         dual = self.dual and all(t.shape[0] % 2 == 0 for t, _ in micro_batches)
-        if dual:      # every micro-batch as two interleaved halves: 2n backward passes
-            parts = []
-            for tok, lab in micro_batches:
-                Bh, S = tok.shape[0] // 2, tok.shape[1]
-                halves = [(tok[k * Bh:(k + 1) * Bh].reshape(-1), lab[k * Bh:(k + 1) * Bh].reshape(-1)) for k in (0, 1)]
-                parts.append((self.model.stage_forward_dual(halves, Bh, S, scale), Bh, S))
-            nb, j = 2 * n, 0
-            for fwd, Bh, S in parts:
-                for loss, ctx in fwd:
-                    self.model.on_grad_ready = self.reducer.grad_ready if j == nb - 1 else None
-                    self.model.stage_backward(ctx, None, Bh, S, accumulate=j > 0 and not f32acc)
-                    if j < nb - 1:
-                        self.reducer.accumulate_micro(first=j == 0)
-                    total = loss if total is None else total + loss
-                    j += 1
-        for j, (tok, lab) in enumerate([] if dual else micro_batches):
+        for j, (tok, lab) in enumerate(micro_batches):
             self.model.on_grad_ready = self.reducer.grad_ready if j == n - 1 else None
-            loss = self.model.forward_backward(tok, lab, accumulate=j > 0 and not f32acc, scale=scale)
+            if dual:      # two interleaved half-batches forward, one full-batch backward
+                B, S = tok.shape
+                loss, ctx = self.model.stage_forward_dual(tok.reshape(-1), lab.reshape(-1), B, S, scale)
+                self.model.stage_backward(ctx, None, B, S, accumulate=j > 0 and not f32acc)
+                del ctx
+            else:
+                loss = self.model.forward_backward(tok, lab, accumulate=j > 0 and not f32acc, scale=scale)
             if j < n - 1:
                 self.reducer.accumulate_micro(first=j == 0)
             total = loss if total is None else total + loss

@@ -206,30 +206,26 @@ def test_tp_chunked_forward_overlap_is_bit_identical(sp):
             assert torch.equal(a["params"][name], b["params"][name]), name
 
 
-def _dual_body(rank, world, dual, sp, mb, accum):
+def _dual_body(rank, world, dual):
     from service_account_auth_improvements_amd.parallel.state import init_distributed
     from service_account_auth_improvements_amd.runtime.trainer import TrainConfig, Trainer
     st = init_distributed(tp=world, pp=1, device="cpu")
-    tr = Trainer(TrainConfig(model="tiny", seq_len=32, micro_batch=mb, grad_accum=accum, n_layers=2, lr=LR,
-                             sequence_parallel=sp, tp_dual_batch=dual), st, full_init=True)
+    tr = Trainer(TrainConfig(model="tiny", seq_len=32, micro_batch=4, n_layers=2, lr=LR, tp_dual_batch=dual), st,
+                 full_init=True)
     assert tr.dual == dual
-    losses = []
-    for s in range(STEPS):
-        (tok, lab), = _batches(tr.mcfg.vocab_size, 1, B=4, seed=700 + s)
-        mbs = [(tok[k * mb:(k + 1) * mb], lab[k * mb:(k + 1) * mb]) for k in range(4 // mb)]
-        losses.append(float(tr.train_step(mbs)))
+    losses = [float(tr.train_step(_batches(tr.mcfg.vocab_size, 1, B=4, seed=700 + s))) for s in range(STEPS)]
     return dict(losses=losses, params={s.name: tr.model.P(s.name).float() for g in tr.model.groups
                                        for s in g.specs})
 
 
-@pytest.mark.parametrize("sp", [False, True], ids=["tp2", "tp2+sp"])
-def test_tp_dual_batch_forward_equals_two_accumulated_micro_batches(sp):
-    """The dual half-batch forward (two halves' layers interleaved at every TP collective) is
-    the same arithmetic as grad_accum 2 at half the micro-batch: bit-identical losses and
-    parameters (two ranks: sums of two are order-free)."""
-    dual = run_ranks(_dual_body, world=2, args=(True, sp, 4, 1))
-    acc = run_ranks(_dual_body, world=2, args=(False, sp, 2, 2))
-    for a, b in zip(dual, acc):
-        assert a["losses"] == b["losses"]
+def test_tp_dual_batch_forward_matches_plain_forward():
+    """The dual half-batch forward (two halves' layers interleaved at every TP collective, their
+    saved activations concatenated for ONE full-batch backward) computes the same step as the
+    plain forward: same losses, parameters equal to fp32 GEMM-blocking noise."""
+    dual = run_ranks(_dual_body, world=2, args=(True,))
+    plain = run_ranks(_dual_body, world=2, args=(False,))
+    for a, b in zip(dual, plain):
+        for x, y in zip(a["losses"], b["losses"]):
+            assert abs(x - y) <= 1e-5 * abs(y), (a["losses"], b["losses"])
         for name in a["params"]:
-            assert torch.equal(a["params"][name], b["params"][name]), name
+            assert torch.allclose(a["params"][name], b["params"][name], rtol=0, atol=1e-6), name

@@ -4,9 +4,9 @@
 # isolates what chunking / half-batch interleaving costs in GEMM efficiency).
 set -o pipefail
 export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
-O=gpurun_out/r3tp
+O=gpurun_out/${TP_OUT:-r3tp2}
 mkdir -p $O
-for cfg in "1 0" "4 0" "1 1" "4 0" "1 0" "1 1"; do
+for cfg in ${TP_CFGS:-"4 0" "4 1" "4 0" "4 1"}; do
   set -- $cfg
   echo "=== chunks=$1 dual=$2" >> $O/all.log
   timeout -k 10 300 python -u tools/bench_tp_shard.py --seq-len 4096 --micro-batch 4 --steps 4 --warmup 2 \
