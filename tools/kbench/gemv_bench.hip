@@ -7,6 +7,7 @@
 
 #include <cstdio>
 #include <vector>
+#include <cstdlib>
 
 #define CK(x)                                                                             \
   do {                                                                                    \
@@ -47,7 +48,9 @@ int main(int argc, char** argv) {
   for (const Shape& s : shapes) {
     const long rows = s.swiglu ? 2L * s.N : s.N;
     const long bytes = rows * s.K * 2;
-    const int copies = (int)std::max<long>(1, ((1L << 30) + bytes - 1) / bytes);
+    // GEMV_HOT=1: one copy, re-read every launch (MALL / Infinity-Cache resident)
+    const bool hot = getenv("GEMV_HOT") && atoi(getenv("GEMV_HOT"));
+    const int copies = hot ? 1 : (int)std::max<long>(1, ((1L << 30) + bytes - 1) / bytes);
     std::vector<bf16_t*> W(copies);
     for (auto& p : W) {
       CK(hipMalloc(&p, bytes));
