@@ -392,6 +392,12 @@ def create_app(kube: Client, profiles: ProfilesService, metrics: Optional[Metric
     cm_name = env.get("DASHBOARD_CONFIGMAP", "centraldashboard-config")
     logout_url = env.get("LOGOUT_URL", "/logout")
     pod_ns = env.get("POD_NAMESPACE", "kubeflow")
+    # two frontends on the same API (the reference ships centraldashboard and
+    # centraldashboard-angular): DASHBOARD_FRONTEND=angular serves the second one at "/"; it is
+    # always reachable under /ng/ as well (static/dashboard-ng.js)
+    ng_dir = os.path.join(HERE, "static", "dashboard-ng")
+    if static_dir is None and env.get("DASHBOARD_FRONTEND", "").lower() in ("angular", "ng"):
+        static_dir = ng_dir
     static_dir = static_dir or os.path.join(HERE, "static", "dashboard")
     app = Flask("centraldashboard", static_folder=None)
     platform_cache = {}
@@ -638,6 +644,8 @@ def create_app(kube: Client, profiles: ProfilesService, metrics: Optional[Metric
     def spa(path="index.html"):
         if path.startswith("static/"):         # the shared UI bundle (webapps/static/kfamd-ui.js)
             return send_from_directory(os.path.join(HERE, "static"), path[len("static/"):])
+        if path == "ng" or path.startswith("ng/"):
+            return send_from_directory(ng_dir, "index.html")
         full = os.path.join(static_dir, path)
         if path != "index.html" and os.path.isfile(full):
             return send_from_directory(static_dir, path)

@@ -218,7 +218,7 @@ function makeEnv(opts) {
       Promise.resolve().then(function () { (winListeners.hashchange || []).forEach(function (f) { f({ type: "hashchange" }); }); });
     }
   });
-  var store = {};
+  var store = {}, lstore = opts.localStorage || {};
   var window = {
     document: document, location: loc,
     addEventListener: function (t, f) { (winListeners[t] = winListeners[t] || []).push(f); },
@@ -249,6 +249,9 @@ function makeEnv(opts) {
     Blob: function (parts, o) { this.parts = parts; this.type = (o || {}).type; },
     sessionStorage: { getItem: function (k) { return store[k] === undefined ? null : store[k]; },
                       setItem: function (k, v) { store[k] = String(v); } },
+    localStorage: { getItem: function (k) { return lstore[k] === undefined ? null : lstore[k]; },
+                    setItem: function (k, v) { lstore[k] = String(v); },
+                    removeItem: function (k) { delete lstore[k]; } },
     navigator: { clipboard: { writeText: function () { return Promise.resolve(); } } },
     fetch: function (url, init) { init = init || {}; return respond(init.method || "GET", String(url), init.body); },
     setTimeout: function (f, ms) { timers.push({ f: f, ms: ms }); return timers.length; },
@@ -259,6 +262,7 @@ function makeEnv(opts) {
   Object.keys(ctx).forEach(function (k) { if (!(k in window)) window[k] = ctx[k]; });
   global.__shim = { location: loc };
   return { ctx: ctx, document: document, window: window, app: app, requests: requests, timers: timers, posted: posted,
+           localStorage: lstore,
            winListeners: winListeners,
            message: function (data) { (winListeners.message || []).forEach(function (f) { f({ data: data }); }); } };
 }

@@ -118,6 +118,17 @@ def test_dashboard_serves_spa(dash):
     assert b"kfamd web UI" in app.get("/static/kfamd-ui.js").data
     assert b'data-app="dashboard"' in app.get("/").data
     assert b'data-app="dashboard"' in app.get("/some/client/route").data
+    # the second frontend (centraldashboard-angular behaviour) is always under /ng/ ...
+    assert b'data-app="dashboard-ng"' in app.get("/ng/").data
+    assert b"centraldashboard-angular" in app.get("/static/dashboard-ng.js").data
+
+
+def test_dashboard_frontend_switch():
+    """DASHBOARD_FRONTEND=angular serves the second frontend at "/" (the reference deploys either)."""
+    app = dashboard.create_app(InMemoryClient(APIServer()), None, None,
+                               env={"DASHBOARD_FRONTEND": "angular"}).test_client()
+    assert b'data-app="dashboard-ng"' in app.get("/").data
+    assert b'data-app="dashboard-ng"' in app.get("/_/jupyter/").data
 
 
 # ------------------------------------------------------------------ Stackdriver + provider factory

@@ -23,7 +23,7 @@ def out():
     return json.loads(r.stdout)
 
 
-@pytest.mark.parametrize("f", ["kfamd-ui.js", "lib/kf-common.js", "lib/kf-logic.js"])
+@pytest.mark.parametrize("f", ["kfamd-ui.js", "dashboard-ng.js", "lib/kf-common.js", "lib/kf-logic.js"])
 def test_js_sources_parse(f):
     r = subprocess.run(["node", "--check", os.path.join(STATIC, f)], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stderr
@@ -232,3 +232,52 @@ def test_dashboard_routes_guard_and_404(pages):
     assert d["noNamespaceHash"].startswith("#/namespace-needed?path=")        # no namespace: redirected
     assert d["namespaceNeeded"].startswith("This page requires a namespace to be selected")
     assert d["snacks"][0][0] == "ERROR" and d["snacks"][0][1].startswith("[500] KFAM is down")
+
+
+# ------------------------------------------------------------------ second dashboard frontend (T3)
+@pytest.fixture(scope="module")
+def ng():
+    r = subprocess.run(["node", os.path.join(ROOT, "tests", "js", "dashboard_ng.js")], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    return json.loads(r.stdout)
+
+
+def test_ng_namespace_resolution_and_persistence(ng):
+    """namespace.service.ts: owned namespace first time, written back as ?ns and stored per user;
+    the stored choice beats ownership, the query beats the stored choice, and a disabled
+    "All namespaces" in the query falls back."""
+    f = ng["first"]
+    assert f["hash"] == "#/?ns=kubeflow-user" and f["selected"] == "kubeflow-user" and f["home"]
+    assert f["stored"] == '"kubeflow-user"'
+    assert f["options"][0] == ["All namespaces", True]          # disabled outside the allowed apps
+    assert ng["restored"] == {"hash": "#/?ns=team-b", "selected": "team-b"}
+    assert ng["queryWins"] == {"hash": "#/?ns=kubeflow-user", "selected": "kubeflow-user"}
+    assert ng["allNsHome"]["selected"] == "team-b"
+    assert f["build"].startswith("Build version v1.8-mi355x")
+
+
+def test_ng_menu_links_and_all_namespaces(ng):
+    menu = dict(ng["first"]["menu"])
+    assert menu["Notebooks"] == "#/_/jupyter/?ns=kubeflow-user"
+    assert menu["Runs"] == "#/_/pipeline/#/runs?ns=kubeflow-user"     # link's own ?ns={ns} resolved, fragment kept
+    assert ng["first"]["quick"][0] == "#/_/jupyter/new?ns=kubeflow-user"
+    assert ng["jupyter"]["options"][0] == ["All namespaces", False]   # allowed for jupyter
+    assert ng["allNs"]["last"] == {"type": "all-namespaces"} and "ns=All+namespaces" in ng["allNs"]["hash"]
+
+
+def test_ng_iframe_wrapper_protocol_and_mirroring(ng):
+    assert ng["jupyter"]["src"] == "/jupyter/?ns=team-b" and ng["jupyter"]["stored"] == '"team-b"'
+    assert ng["connected"] == [{"type": "namespace-selected", "value": "team-b"}]
+    sw = ng["switched"]
+    assert sw["hash"] == "#/_/jupyter/?ns=kubeflow-user" and sw["sameFrame"]
+    assert sw["messages"] == [{"type": "namespace-selected", "value": "kubeflow-user"}]
+    # the app navigated inside the iframe: the dashboard URL follows, with ?ns added
+    assert ng["mirrored"]["hash"] == "#/_/jupyter/new?ns=kubeflow-user"
+
+
+def test_ng_guard_404_and_error_interceptor(ng):
+    assert ng["guard"]["page"] and ng["guard"]["hash"].startswith("#/namespace-needed?path=")
+    assert ng["noNs"]["page"] and ng["noNs"]["after"].startswith("#/namespace-needed")
+    assert ng["notFound"]["page"] and "/no-such-page" in ng["notFound"]["text"]
+    assert ng["error"] == [["ERROR", "[500] kfam unreachable\nhttp://localhost/app/api/workgroup/env-info"]]
