@@ -191,7 +191,8 @@ class Engine:
         return tp_all_reduce(x, self.m.st)
 
     def _use_bgemm(self, x, w) -> bool:
-        return (BGEMM and max(SKINNY_MAX_ROWS + 1, BGEMM_MIN_ROWS) <= x.shape[0] <= BGEMM_MAX_ROWS
+        # measured at TP=1 (a TP shard's K of 512-1792 leaves too few K stages to split)
+        return (BGEMM and self.m.tp == 1 and max(SKINNY_MAX_ROWS + 1, BGEMM_MIN_ROWS) <= x.shape[0] <= BGEMM_MAX_ROWS
                 and w.shape[0] <= BGEMM_MAX_N
                 and ops.bgemm_ok(x, w))
 
