@@ -42,15 +42,55 @@ def _events(path: str) -> list:
         return []
 
 
+def _vram_used(root: str = "/sys/class/drm") -> dict:
+    """Per-card VRAM bytes in use, read from amdgpu's sysfs (no HIP call, so the measuring
+    process stays off the GPU).  Empty when the node exposes no such files."""
+    out = {}
+    try:
+        names = sorted(n for n in os.listdir(root) if n.startswith("card") and n[4:].isdigit())
+    except OSError:
+        return out
+    for n in names:
+        try:
+            with open(os.path.join(root, n, "device", "mem_info_vram_used")) as f:
+                out[n] = int(f.read().strip())
+        except (OSError, ValueError):
+            pass
+    return out
+
+
+def wait_device_release(base: dict, held: dict, n_devices: int = 1, timeout: float = 15.0,
+                        slack: int = 1 << 30, root: str = "/sys/class/drm", poll: float = 0.05) -> float:
+    """After a job's processes have exited, wait until the driver has given back the device
+    memory they held.  The amdgpu driver tears a process's buffers down after the process is
+    reaped; a next job that allocates during that teardown stalls for seconds in its first
+    large allocations (seen as 2-3 s outliers in ``optimizer_state`` / the first step).
+    Only the job's ``n_devices`` cards are watched: those whose usage rose most (by > 4 GiB)
+    while the job ran (``held`` vs ``base``), so other tenants' cards on a shared node do not
+    delay the loop.  Returns the seconds waited."""
+    rise = sorted(((v - base.get(c, v), c) for c, v in held.items()), reverse=True)[:n_devices]
+    ours = [c for d, c in rise if d > 4 * slack]
+    t0 = time.time()
+    while ours and time.time() - t0 < timeout:
+        now = _vram_used(root)
+        if all(now.get(c, 0) <= base.get(c, 0) + slack for c in ours):
+            break
+        time.sleep(poll)
+    return time.time() - t0
+
+
 def measure(jobs: int = 3, model: str = "llama3-8b", gpus: int = 1, nodes: int = 1, seq_len: int = 8192,
             micro_batch: int = 1, layers: Optional[int] = None, device: str = "cuda", kind: str = "pytorchjob",
-            processes: bool = True, gap: float = 0.0, timeout: float = 300.0, port_base: int = 29700,
+            processes: bool = True, gap: float = 0.0, release_wait: Optional[bool] = None,
+            timeout: float = 300.0, port_base: int = 29700,
             log: Callable[[str], None] = lambda s: print(s, file=sys.stderr, flush=True)) -> dict:
     """Submit ``jobs`` jobs one after another; returns p50 / p90 / min and the breakdown."""
     from .cluster import LocalCluster, ProcessCluster
     from .controlplane import training
     from .native import build_native
     build_native()
+    if release_wait is None:
+        release_wait = os.environ.get("KFAMD_CRD_RELEASE_WAIT", "1") != "0"
     tmp = tempfile.mkdtemp(prefix="crd2step-")
     events = os.path.join(tmp, "events.jsonl")
     env = {"KFAMD_EVENTS_FILE": events, "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS", "4")}
@@ -90,6 +130,7 @@ def measure(jobs: int = 3, model: str = "llama3-8b", gpus: int = 1, nodes: int =
                 if not gpus:
                     job["spec"]["nprocPerNode"] = "1"
                 rank0_pod = f"{name}-master-0"
+            base = _vram_used() if release_wait else {}
             t0 = time.time()
             client.create(job)
             t_running = None
@@ -105,6 +146,7 @@ def measure(jobs: int = 3, model: str = "llama3-8b", gpus: int = 1, nodes: int =
                 fs = [e for e in evs if e["event"] == "first_step" and e.get("rank") == 0]
                 if fs:
                     first = fs[0]
+                    held = _vram_used() if release_wait else {}
                     break
                 time.sleep(0.01)
             if first is None:
@@ -120,7 +162,6 @@ def measure(jobs: int = 3, model: str = "llama3-8b", gpus: int = 1, nodes: int =
                          "model_init": ie["ts"] - dr, "init_to_first_step": first["ts"] - ie["ts"],
                          "params_alloc_init": ie.get("params_alloc_init_s", 0.0),
                          "optimizer_state": ie.get("optimizer_state_s", 0.0)})
-            log(json.dumps({"crd_job": name, **{k: round(v, 3) for k, v in rows[-1].items()}}))
             # the job ends after its step; wait for it (and its pods' processes) so the devices
             # are free for the next job and for whatever runs after this measurement
             while time.time() < deadline:
@@ -129,6 +170,9 @@ def measure(jobs: int = 3, model: str = "llama3-8b", gpus: int = 1, nodes: int =
                 if any(c["type"] in ("Succeeded", "Failed") and c["status"] == "True" for c in conds):
                     break
                 time.sleep(0.05)
+            if release_wait:
+                rows[-1]["device_release"] = wait_device_release(base, held, n_devices=max(1, gpus * nodes))
+            log(json.dumps({"crd_job": name, **{k: round(v, 3) for k, v in rows[-1].items()}}))
     finally:
         cl.stop()
     tot = sorted(r["total"] for r in rows)
@@ -139,4 +183,5 @@ def measure(jobs: int = 3, model: str = "llama3-8b", gpus: int = 1, nodes: int =
             "min_s": round(tot[0], 3), "max_s": round(tot[-1], 3),
             "per_job_s": [round(r["total"], 3) for r in rows],
             "cluster_up_s": round(t_up, 2),
+            "device_release_wait_s": [round(r.get("device_release", 0.0), 3) for r in rows],
             "breakdown_p50_s": {k: round(statistics.median(r[k] for r in rows), 3) for k in BREAKDOWN}}

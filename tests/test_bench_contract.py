@@ -121,3 +121,35 @@ def test_auto_micro_batch_memory_plan():
         assert bench._auto_micro_batch(dp, False, "fp32", True) == 3      # fp32 all-reduce staging
     assert bench._auto_micro_batch(1, True, "fp32", True) == 3            # one-rank rehearsal
     assert bench._auto_micro_batch(1, False, "fp32", False, grad_accum=4) == 3
+
+
+def test_crd_device_release_wait_watches_only_our_cards(tmp_path):
+    """The between-jobs wait reads amdgpu's sysfs VRAM counters and only waits for cards whose
+    usage the job raised (other tenants' cards never delay the loop)."""
+    import threading
+    import time
+    from service_account_auth_improvements_amd import crdbench
+
+    gib = 1 << 30
+
+    def card(n, used):
+        d = tmp_path / f"card{n}" / "device"
+        d.mkdir(parents=True, exist_ok=True)
+        (d / "mem_info_vram_used").write_text(str(used))
+
+    card(0, 1 * gib)
+    card(1, 50 * gib)
+    (tmp_path / "renderD128").mkdir()
+    base = crdbench._vram_used(str(tmp_path))
+    assert base == {"card0": gib, "card1": 50 * gib}
+    card(0, 90 * gib)     # our job holds card0; card1 is another tenant that also grows a lot
+    card(1, 60 * gib)
+    held = crdbench._vram_used(str(tmp_path))
+    threading.Timer(0.3, lambda: card(0, int(1.5 * gib))).start()
+    t0 = time.time()
+    waited = crdbench.wait_device_release(base, held, timeout=5.0, root=str(tmp_path), poll=0.01)
+    assert 0.25 < waited < 2.0 and time.time() - t0 < 2.0
+    # nothing of ours held -> no wait at all; a card that never drains -> bounded by timeout
+    assert crdbench.wait_device_release(base, base, root=str(tmp_path)) < 0.05
+    card(0, 90 * gib)
+    assert 0.2 <= crdbench.wait_device_release(base, held, timeout=0.2, root=str(tmp_path), poll=0.01) < 1.0
