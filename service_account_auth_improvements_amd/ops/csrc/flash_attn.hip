@@ -87,6 +87,20 @@ __device__ __forceinline__ void glds4(const void* g, char* lds) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
                                    (__attribute__((address_space(3))) void*)lds, 4, 0, 0);
 }
+// One LDS-DMA wave-instruction (16 B per lane) from a wave-uniform panel base (SGPRs) plus a
+// 32-bit lane byte offset, landing at the wave-uniform LDS byte address `lds` (m0)
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ const char* uniform_ptr(const char* p) {
+  const uint64_t v = (uint64_t)p;
+  return (const char*)(((uint64_t)__builtin_amdgcn_readfirstlane((u32)(v >> 32)) << 32) |
+                       (u32)__builtin_amdgcn_readfirstlane((u32)v));
+}
+__device__ __forceinline__ void dma_sv(const char* base, u32 off, u32 lds) {
+  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2"
+               :
+               : "s"(__builtin_amdgcn_readfirstlane(lds)), "v"(off), "s"(uniform_ptr(base))
+               : "memory", "m0");
+}
 // Stage `nrows` rows of 128 bf16 (global row stride ld) into the swizzled image at `tile`.
 // Wave-instruction i fills LDS bytes [1024 i, 1024 i + 1024) = rows 4i..4i+3; lane L of it
 // writes physical chunk L%16 of row 4i + L/16 and therefore fetches logical chunk
@@ -157,6 +171,48 @@ __device__ __forceinline__ void lgkm_wait_tie(bf16x8* f) {
   asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]) : "i"(N) : "memory");
 }
 __device__ __forceinline__ void barrier() { asm volatile("s_barrier" ::: "memory"); }
+// Inline-asm LDS reads with an immediate offset (the per-lane part in one VGPR); the caller
+// waits for them with counted, register-tying lgkmcnt waits (lgkm_tie*)
+template <int OFF>
+__device__ __forceinline__ bf16x8 rd_b128(u32 a) {
+  u32x4 r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF) : "memory");
+  return as_bf16x8(r);
+}
+template <int OFF>
+__device__ __forceinline__ bf16x8 rd_tr2(u32 a0, u32 a1) {
+  u32x2 x, y;
+  asm volatile("ds_read_b64_tr_b16 %0, %2 offset:%4\n\tds_read_b64_tr_b16 %1, %3 offset:%4"
+               : "=&v"(x), "=v"(y)
+               : "v"(a0), "v"(a1), "i"(OFF)
+               : "memory");
+  return as_bf16x8(u32x4{x[0], x[1], y[0], y[1]});
+}
+template <int OFF>
+__device__ __forceinline__ float rd_b32(u32 a) {
+  float r;
+  asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF) : "memory");
+  return r;
+}
+template <int N>
+__device__ __forceinline__ void lgkm_tie1(bf16x8& a) {
+  asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(a) : "i"(N) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void lgkm_tie3(bf16x8& a, bf16x8& b, bf16x8& c) {
+  asm volatile("s_waitcnt lgkmcnt(%3)" : "+v"(a), "+v"(b), "+v"(c) : "i"(N) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void lgkm_tie_f2(float& a, float& b) {
+  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "i"(N) : "memory");
+}
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>());
+    static_for<I + 1, N>(f);
+  }
+}
 template <int N>
 __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory"); }
 // Row constant folded into an MFMA chain as one extra k-chunk: A holds a ones column at
@@ -410,12 +466,30 @@ __global__ __launch_bounds__(256) void flash_bwd_pre_kernel(const bf16_t* __rest
 // come out of the MFMA chains with both row constants folded in (hi/lo bf16 split, no
 // accumulator-initialising moves), so dS^T = exp2(c S') * dP' per element; dQ^T += K^T dS^T
 // with the K^T fragments read (inline asm, counted waits) one output block ahead.
+// 1 = K/V row fragments by inline asm, KF_FA_DQ_QP k-steps ahead; 0 = compiler-scheduled
+#ifndef KF_FA_DQ_PIPE
+#define KF_FA_DQ_PIPE 1
+#endif
+#ifndef KF_FA_DQ_QP
+#define KF_FA_DQ_QP 1
+#endif
+constexpr int QP = KF_FA_DQ_QP;
+// lane id from v_mbcnt in asm volatile: recomputed where used, never kept live in a VGPR
+__device__ __forceinline__ u32 lane_id_opaque() {
+  u32 x;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(x));
+  return x;
+}
+template <int N>
+__device__ __forceinline__ void lgkm_tie2(bf16x8& a, bf16x8& b) {
+  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "i"(N) : "memory");
+}
 template <bool CAUSAL>
 __global__ __launch_bounds__(512, 1) void flash_bwd_dq_kernel(
     const bf16_t* __restrict__ qkv, long ld, const bf16_t* __restrict__ dout, long lddo,
     const float* __restrict__ lse, const float* __restrict__ delta, bf16_t* __restrict__ dqkv,
     long lddq, int B, int S, int Hq, int Hkv, float scale_log2, float scale) {
-  __shared__ __attribute__((aligned(16))) char smem[NST * STG];
+  __shared__ __attribute__((aligned(1024))) char smem[NST * STG];
   const int nqb = (S + BQ8 - 1) / BQ8, G = Hq / Hkv;
   int lid = xcd_remap(blockIdx.x, B * Hq * nqb);
   const int g = lid % G;
@@ -445,11 +519,31 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dq_kernel(
   float dl = delta[((long)b * Hq + h) * S + qc];
   const bf16_t* kp = qkv + (long)b * S * ld + (long)(Hq + hkv) * D;
   const bf16_t* vp = qkv + (long)b * S * ld + (long)(Hq + Hkv + hkv) * D;
+#if KF_FA_DQ_PIPE
+  // wave w fills rows 4w.. and 4w+32.. of the K and V images: SGPR panel base + one 32-bit lane
+  // offset shared by K and V (same row stride; rows 32 apart share the chunk swizzle)
+  u32 dma_kv;
+  {
+    const int row = 4 * w + (l >> 4), ch = (l & 15) ^ swz_x(row);
+    dma_kv = (u32)((row * ld + ch * 8) * 2);
+  }
+  const u32 lds_w = lds_addr(smem) + 1024 * w;
+  auto stage = [&](int j) {
+    const u32 st = lds_w + (j % NST) * STG;
+    const char* kb_ = reinterpret_cast<const char*>(kp + (long)j * BK * ld);
+    const char* vb_ = reinterpret_cast<const char*>(vp + (long)j * BK * ld);
+    dma_sv(kb_, dma_kv, st);
+    dma_sv(kb_ + 64 * ld, dma_kv, st + 8192);
+    dma_sv(vb_, dma_kv, st + TILE);
+    dma_sv(vb_ + 64 * ld, dma_kv, st + TILE + 8192);
+  };
+#else
   auto stage = [&](int j) {
     char* st = smem + (j % NST) * STG;
     stage_rows(kp + (long)j * BK * ld, ld, st, BK, w, 8, l);
     stage_rows(vp + (long)j * BK * ld, ld, st + TILE, BK, w, 8, l);
   };
+#endif
   const int ntiles = CAUSAL ? min(S, qb * BQ8 + BQ8) / BK : S / BK;
   for (int j = 0; j < NST - 1 && j < ntiles; ++j) stage(j);
   // retire the register loads before the loop (see the forward)
@@ -473,6 +567,53 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dq_kernel(
       const char* Vs = Ks + TILE;
       const bool need_mask = CAUSAL && (k0 + BK - 1 > qmin_w);
       bf16x8 sf[2][2];
+#if KF_FA_DQ_PIPE
+      // K and V row fragments by inline asm, QP k-steps ahead across both 32-key halves
+      // (the compiler-scheduled form waited lgkmcnt(0) before every MFMA pair); this tile's
+      // lane base is opaque so the 16 XOR-ed addresses are formed next to their reads
+      // rematerialised from the lane id per tile (a long-lived copy spilled, and its reload
+      // waited vmcnt(0) -- i.e. for every DMA stage in flight)
+      const u32 ln = lane_id_opaque(), lr_ = ln & 31;
+      const u32 a_t = (lds_addr(smem) + (u32)((j % NST) * STG)) + lr_ * 256 + 16 * ((ln >> 5) ^ swz_x(lr_));
+      bf16x8 fk[QP + 1], fv[QP + 1];
+      auto rdS = [&](auto ic) {
+        constexpr int i = decltype(ic)::value, kt = i >> 3, ks = i & 7, sl = i % (QP + 1);
+        fk[sl] = rd_b128<8192 * kt>(a_t ^ (32 * ks));
+        fv[sl] = rd_b128<TILE + 8192 * kt>(a_t ^ (32 * ks));
+      };
+      static_for<0, QP>([&](auto ic) { rdS(ic); });
+      f32x16 s, dp;
+      static_for<0, 16>([&](auto ic) {
+        constexpr int i = decltype(ic)::value, kt = i >> 3, ks = i & 7, sl = i % (QP + 1);
+        if constexpr (ks == 0) {
+          s = mfma32(ones, lse_b, f32x16{});
+          dp = mfma32(ones, dl_b, f32x16{});
+        }
+        if constexpr (i + QP < 16) rdS(std::integral_constant<int, i + QP>());
+        lgkm_tie2<2 * (i + QP < 16 ? QP : 15 - i)>(fk[sl], fv[sl]);
+        s = mfma32(fk[sl], qf[ks], s);
+        dp = mfma32(fv[sl], df[ks], dp);
+        if constexpr (ks == 7) {
+          if (need_mask) {
+            const int ln = (int)lane_id_opaque(), qq = qmin_w + (ln & 31), h4 = 4 * (ln >> 5);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int key = k0 + 32 * kt + (r & 3) + 8 * (r >> 2) + h4;
+              s[r] = key > qq ? -INFINITY : s[r];
+            }
+          }
+#pragma unroll
+          for (int r = 0; r < 16; ++r) s[r] = __builtin_amdgcn_exp2f(s[r] * scale_log2) * dp[r];   // dS^T (unscaled)
+#pragma unroll
+          for (int ss = 0; ss < 2; ++ss) {
+            u32x4 u;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) u[e] = pack2(s[8 * ss + 2 * e], s[8 * ss + 2 * e + 1]);
+            sf[kt][ss] = as_bf16x8(u);
+          }
+        }
+      });
+#else
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
         f32x16 s = mfma32(ones, lse_b, f32x16{}), dp = mfma32(ones, dl_b, f32x16{});
@@ -498,6 +639,7 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dq_kernel(
           sf[kt][ss] = as_bf16x8(u);
         }
       }
+#endif
       const u32 kbase = lds_addr(Ks);
       bf16x8 kf[2][4];
       auto k_read = [&](int t, bf16x8* f) {
@@ -552,6 +694,18 @@ constexpr int OFF_Q = 32768;                   // [2][32 x 256 B]
 constexpr int OFF_DO = OFF_Q + 16384;          // [2][32 x 256 B]
 constexpr int OFF_LD = OFF_DO + 16384;         // [2][lse 32 f32 | delta 32 f32]
 constexpr int SMEM = OFF_LD + 512;             // 66048 B -> 2 workgroups per CU
+// 1 = software-pipelined iteration (inline-asm LDS reads, counted waits); 0 = compiler-scheduled
+#ifndef KF_FA_DKDV_PIPE
+#define KF_FA_DKDV_PIPE 1
+#endif
+// read-ahead of the pipelined iteration: S/dP k-steps (3 row reads each) and dV/dK fragments
+#ifndef KF_FA_DKDV_PA
+#define KF_FA_DKDV_PA 1
+#endif
+#ifndef KF_FA_DKDV_PT
+#define KF_FA_DKDV_PT 3
+#endif
+constexpr int PA = KF_FA_DKDV_PA, PT = KF_FA_DKDV_PT;
 
 __host__ __device__ inline int n_chunks(int kb, int S, bool causal) {
   const int q0 = causal ? kb * BKV : 0;
@@ -565,7 +719,7 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
     const float* __restrict__ lse, const float* __restrict__ delta, float* __restrict__ dk_acc,
     float* __restrict__ dv_acc, int B, int S, int Hq, int Hkv, float scale, int items_per_head) {
   using namespace fb;
-  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
   const int G = Hq / Hkv;
   const int lid = xcd_remap(blockIdx.x, B * Hkv * items_per_head);
   int item = lid % items_per_head;
@@ -596,13 +750,34 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
   bf16x8 vf[8];  // B operand of dP = dO V^T: V[key][16ks + 8hh .. +8]
 #pragma unroll
   for (int ks = 0; ks < 8; ++ks) vf[ks] = as_bf16x8(ld16(vp + (long)(kw0 + lr) * ld + 16 * ks + 8 * hh));
+#if KF_FA_DKDV_PIPE
+  const u32 sbase = lds_addr(smem);
+  u32 dma_q, dma_do;   // byte offset of this lane's 16-B piece of row 4w + l/16 in a Q / dO panel
+  {
+    const int row = 4 * w + (l >> 4), ch = (l & 15) ^ swz_x(row);
+    dma_q = (u32)((row * ld + ch * 8) * 2);
+    dma_do = (u32)((row * lddo + ch * 8) * 2);
+  }
+#endif
 
   auto stage = [&](int it, int buf) {
     const int hq = it / ntq, qt = it - hq * ntq;
     const int h = hkv * G + hq;
     const int q0 = qs + qt * QT;
+#if KF_FA_DKDV_PIPE
+    // wave w fills rows 4w.. and 4w+16.. of the Q and dO images: SGPR panel base + one 32-bit
+    // lane offset per tensor (rows 16 apart share the lane's chunk swizzle)
+    const char* qb_ = reinterpret_cast<const char*>(qkv + (rowB + q0) * ld + (long)h * D);
+    const char* db_ = reinterpret_cast<const char*>(dout + (rowB + q0) * lddo + (long)h * D);
+    const u32 lq = sbase + OFF_Q + buf * 8192 + 1024 * w, ldo_ = sbase + OFF_DO + buf * 8192 + 1024 * w;
+    dma_sv(qb_, dma_q, lq);
+    dma_sv(qb_ + 32 * ld, dma_q, lq + 4096);
+    dma_sv(db_, dma_do, ldo_);
+    dma_sv(db_ + 32 * lddo, dma_do, ldo_ + 4096);
+#else
     stage_rows(qkv + (rowB + q0) * ld + (long)h * D, ld, smem + OFF_Q + buf * 8192, QT, w, 4, l);
     stage_rows(dout + (rowB + q0) * lddo + (long)h * D, lddo, smem + OFF_DO + buf * 8192, QT, w, 4, l);
+#endif
     if (w == 0) {
       // lse/delta select from an opaque lane id: hoisted, the per-lane 64-bit pointer lived
       // across the loop and was the kernel's only scratch spill
@@ -622,6 +797,109 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
   if (niter > 0) stage(0, 0);
   wait_dma_barrier();
   const bf16x8 ones = fold_ones(hh);
+#if KF_FA_DKDV_PIPE
+  // Software-pipelined iteration.  Every LDS read is inline asm with an immediate buffer
+  // offset and a counted, register-tying wait: the compiler-scheduled form issued each
+  // operand right before its MFMA behind an lgkmcnt(0) (one read latency exposed per MFMA)
+  // and waited vmcnt(0) for the NEXT tile's DMA before the transposed reads.
+  //  * S/dP chain: Q, K and dO row fragments two k-steps ahead (3-slot ring);
+  //  * dV^T/dK^T chain: the 16 transposed fragments (dO^T, then Q^T) three ahead (4-slot ring),
+  //    the first three issued before the softmax VALU work.
+  // Lane address parts: smem is 1024-aligned, so the k-step / column-block terms are XORs that
+  // never carry (row chunk 2ks+hh -> a_row ^ 32ks; transposed column block t -> a_tr ^ 64t).
+  const u32 a_row0 = sbase + lr * 256 + 16 * (hh ^ swz_x(lr));
+  const u32 a_k0 = a_row0 + 8192 * w + OFF_K;
+  const u32 a_ls = sbase + OFF_LD + 4 * lr;
+  u32 a_tr[2][2];
+#pragma unroll
+  for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      const int row = 16 * ss + vrow + 8 * hf;
+      a_tr[ss][hf] = sbase + row * 256 + 16 * ((vcol >> 3) ^ swz_x(row)) + 8 * (l & 1);
+    }
+  auto iter = [&](auto curc, int it) {
+    constexpr int CUR = decltype(curc)::value;
+    constexpr int OQ = OFF_Q + CUR * 8192, OD = OFF_DO + CUR * 8192, OL = CUR * 256;
+    const int q0 = qs + (it % ntq) * QT;
+    if (it + 1 < niter) stage(it + 1, CUR ^ 1);
+    // opaque per iteration: keeps the 32 XOR-ed per-read addresses from being hoisted out of
+    // the loop as invariants (they would pin ~30 VGPRs and spill)
+    u32 a_row = a_row0, a_k = a_k0, a_t00 = a_tr[0][0], a_t01 = a_tr[0][1], a_t10 = a_tr[1][0], a_t11 = a_tr[1][1];
+    asm volatile("" : "+v"(a_row), "+v"(a_k), "+v"(a_t00), "+v"(a_t01), "+v"(a_t10), "+v"(a_t11));
+    const u32 a_t[2][2] = {{a_t00, a_t01}, {a_t10, a_t11}};
+    if (!CAUSAL || kw0 <= q0 + QT - 1) {
+      float lse_v = rd_b32<OL>(a_ls), dl_v = rd_b32<OL + 128>(a_ls);
+      bf16x8 fq[PA + 1], fk[PA + 1], fd[PA + 1];
+      auto rdA = [&](auto kc) {
+        constexpr int ks = decltype(kc)::value, sl = ks % (PA + 1);
+        fq[sl] = rd_b128<OQ>(a_row ^ (32 * ks));
+        fk[sl] = rd_b128<0>(a_k ^ (32 * ks));
+        fd[sl] = rd_b128<OD>(a_row ^ (32 * ks));
+      };
+      static_for<0, PA>([&](auto kc) { rdA(kc); });
+      lgkm_tie_f2<3 * PA>(lse_v, dl_v);
+      // row constants -lse/scale and -delta of query row lr folded into the chains
+      f32x16 s = mfma32(fold_const(lse_v * inv_scale, hh), ones, f32x16{});
+      f32x16 dp = mfma32(fold_const(dl_v, hh), ones, f32x16{});
+      static_for<0, 8>([&](auto kc) {
+        constexpr int ks = decltype(kc)::value, sl = ks % (PA + 1);
+        if constexpr (ks + PA < 8) rdA(std::integral_constant<int, ks + PA>());
+        // outstanding after this k-step's reads: the later k-steps already issued
+        lgkm_tie3<3 * (ks + PA < 8 ? PA : 7 - ks)>(fq[sl], fk[sl], fd[sl]);
+        s = mfma32(fq[sl], fk[sl], s);
+        dp = mfma32(fd[sl], vf[ks], dp);
+      });
+      // transposed fragment j: j < 8 -> dO^T (dV), else Q^T (dK); column block t, row half ss
+      bf16x8 ft[PT + 1];
+      auto rdT = [&](auto jc) {
+        constexpr int j = decltype(jc)::value, t = (j & 7) >> 1, ss = j & 1;
+        ft[j % (PT + 1)] = rd_tr2<(j < 8 ? OD : OQ)>(a_t[ss][0] ^ (64 * t), a_t[ss][1] ^ (64 * t));
+      };
+      static_for<0, PT>([&](auto jc) { rdT(jc); });
+      const int key = kw0 + lr;
+      const bool need_mask = CAUSAL && (kw0 + 31 > q0);
+      if (need_mask) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = __builtin_amdgcn_exp2f(s[r] * c);
+          s[r] = key > q0 + (r & 3) + 8 * (r >> 2) + 4 * hh ? 0.f : p;
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[r] = __builtin_amdgcn_exp2f(s[r] * c);
+      }
+      bf16x8 pf[2], sf[2];
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        u32x4 u, v;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          u[i] = pack2(s[8 * ss + 2 * i], s[8 * ss + 2 * i + 1]);
+          v[i] = pack2(s[8 * ss + 2 * i] * dp[8 * ss + 2 * i], s[8 * ss + 2 * i + 1] * dp[8 * ss + 2 * i + 1]);
+        }
+        pf[ss] = as_bf16x8(u);
+        sf[ss] = as_bf16x8(v);
+      }
+      static_for<0, 16>([&](auto jc) {
+        constexpr int j = decltype(jc)::value, t = (j & 7) >> 1, ss = j & 1, sl = j % (PT + 1);
+        if constexpr (j + PT < 16) rdT(std::integral_constant<int, j + PT>());
+        lgkm_tie1<2 * (j + PT < 16 ? PT : 15 - j)>(ft[sl]);
+        if constexpr (j < 8) dV[t] = mfma32(ft[sl], pf[ss], dV[t]);
+        else dK[t] = mfma32(ft[sl], sf[ss], dK[t]);
+      });
+    }
+    wait_dma_barrier();
+  };
+  {
+    int it = 0;
+    for (; it + 1 < niter; it += 2) {
+      iter(std::integral_constant<int, 0>(), it);
+      iter(std::integral_constant<int, 1>(), it + 1);
+    }
+    if (it < niter) iter(std::integral_constant<int, 0>(), it);
+  }
+#else
   for (int it = 0; it < niter; ++it) {
     const int cur = it & 1;
     const int qt = it % ntq;
@@ -685,6 +963,7 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
     }
     wait_dma_barrier();
   }
+#endif
   // ---- chunk partial sums: transpose [d][key] accumulators through LDS, row-contiguous adds
   float* T = reinterpret_cast<float*>(smem);   // [128 keys][128 d] fp32 = 64 KB
   auto flush = [&](const f32x16(&acc)[4], float mul, float* dst_base) {
@@ -751,10 +1030,6 @@ __device__ __forceinline__ float ds_f32(u32 addr) {
   float v;
   asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"(addr) : "memory");
   return v;
-}
-template <int N>
-__device__ __forceinline__ void lgkm_tie1(bf16x8& f) {
-  asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(f) : "i"(N) : "memory");
 }
 __device__ __forceinline__ void drain_mfma() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory"); }
 
