@@ -706,6 +706,29 @@ constexpr int SMEM = OFF_LD + 512;             // 66048 B -> 2 workgroups per CU
 #define KF_FA_DKDV_PT 3
 #endif
 constexpr int PA = KF_FA_DKDV_PA, PT = KF_FA_DKDV_PT;
+// dV/dK fragment order: 0 = column block major (t, then row half ss), 1 = ss major (the first
+// four MFMAs need only the first half of P / dS, so the second half's exp overlaps them)
+#ifndef KF_FA_DKDV_SSMAJOR
+#define KF_FA_DKDV_SSMAJOR 0
+#endif
+// 1 = s_setprio 1 over the MFMA chains, 0 over the softmax VALU and the DMA issue
+#ifndef KF_FA_DKDV_PRIO
+#define KF_FA_DKDV_PRIO 1
+#endif
+// 1 = S chain, then dP chain with the softmax beside it, then dV with dS beside it (see kernel)
+#ifndef KF_FA_DKDV_SPLIT
+#define KF_FA_DKDV_SPLIT 0
+#endif
+template <int J> struct FragJ {
+  static constexpr int t = KF_FA_DKDV_SSMAJOR ? (J & 3) : ((J & 7) >> 1);
+  static constexpr int ss = KF_FA_DKDV_SSMAJOR ? ((J & 7) >> 2) : (J & 1);
+};
+__device__ __forceinline__ void prio(int p) {
+  if (KF_FA_DKDV_PRIO) {
+    if (p) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+  }
+}
 
 __host__ __device__ inline int n_chunks(int kb, int S, bool causal) {
   const int q0 = causal ? kb * BKV : 0;
@@ -760,8 +783,13 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
   }
 #endif
 
+#if KF_FA_DKDV_PIPE
+  // iteration it = (head hq, query tile qt) is carried incrementally (no runtime division)
+  auto stage = [&](int hq, int qt, int buf) {
+#else
   auto stage = [&](int it, int buf) {
     const int hq = it / ntq, qt = it - hq * ntq;
+#endif
     const int h = hkv * G + hq;
     const int q0 = qs + qt * QT;
 #if KF_FA_DKDV_PIPE
@@ -794,10 +822,18 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
   const int vrow = 4 * hh + ((l & 15) >> 2);
   const int vcol = 16 * ((l >> 4) & 1) + 4 * (l & 3);
 
+#if KF_FA_DKDV_PIPE
+  if (niter > 0) stage(0, 0, 0);
+#else
   if (niter > 0) stage(0, 0);
+#endif
   wait_dma_barrier();
   const bf16x8 ones = fold_ones(hh);
 #if KF_FA_DKDV_PIPE
+  int nx_hq = 0, nx_qt = 0;   // (head, tile) of the NEXT iteration to stage
+  auto adv = [&]() {
+    if (++nx_qt == ntq) { nx_qt = 0; ++nx_hq; }
+  };
   // Software-pipelined iteration.  Every LDS read is inline asm with an immediate buffer
   // offset and a counted, register-tying wait: the compiler-scheduled form issued each
   // operand right before its MFMA behind an lgkmcnt(0) (one read latency exposed per MFMA)
@@ -821,14 +857,91 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
   auto iter = [&](auto curc, int it) {
     constexpr int CUR = decltype(curc)::value;
     constexpr int OQ = OFF_Q + CUR * 8192, OD = OFF_DO + CUR * 8192, OL = CUR * 256;
-    const int q0 = qs + (it % ntq) * QT;
-    if (it + 1 < niter) stage(it + 1, CUR ^ 1);
+    const int q0 = qs + nx_qt * QT;   // this iteration's tile (advanced below to the next)
+    adv();
+    if (it + 1 < niter) stage(nx_hq, nx_qt, CUR ^ 1);
     // opaque per iteration: keeps the 32 XOR-ed per-read addresses from being hoisted out of
     // the loop as invariants (they would pin ~30 VGPRs and spill)
     u32 a_row = a_row0, a_k = a_k0, a_t00 = a_tr[0][0], a_t01 = a_tr[0][1], a_t10 = a_tr[1][0], a_t11 = a_tr[1][1];
     asm volatile("" : "+v"(a_row), "+v"(a_k), "+v"(a_t00), "+v"(a_t01), "+v"(a_t10), "+v"(a_t11));
     const u32 a_t[2][2] = {{a_t00, a_t01}, {a_t10, a_t11}};
+#if KF_FA_DKDV_SPLIT
     if (!CAUSAL || kw0 <= q0 + QT - 1) {
+      // S chain, then the dP chain with the softmax of S interleaved, then the dV chain with
+      // dS = P * dP' interleaved, then the dK chain: every VALU phase has MFMAs beside it.
+      // Phase-A read steps: i < 8 -> Q_i, K_i; i >= 8 -> dO_(i-8); PA steps ahead.
+      prio(1);
+      float lse_v = rd_b32<OL>(a_ls), dl_v = rd_b32<OL + 128>(a_ls);
+      bf16x8 fq[PA + 1], fk[PA + 1], fd[PA + 1];
+      auto rdA = [&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        if constexpr (i < 8) {
+          fq[i % (PA + 1)] = rd_b128<OQ>(a_row ^ (32 * i));
+          fk[i % (PA + 1)] = rd_b128<0>(a_k ^ (32 * i));
+        } else {
+          fd[(i - 8) % (PA + 1)] = rd_b128<OD>(a_row ^ (32 * (i - 8)));
+        }
+      };
+      static_for<0, PA>([&](auto ic) { rdA(ic); });
+      lgkm_tie_f2<2 * PA>(lse_v, dl_v);
+      f32x16 s = mfma32(fold_const(lse_v * inv_scale, hh), ones, f32x16{});
+      f32x16 dp = mfma32(fold_const(dl_v, hh), ones, f32x16{});
+      // causal mask as a branch-free compare: element r is dropped when key - (q0 + 4hh) > row(r)
+      const int key = kw0 + lr;
+      const int kd = (CAUSAL && (kw0 + 31 > q0)) ? key - (q0 + 4 * hh) : -64;
+      bf16x8 pf[2], sf[2];
+      u32 pu[8];
+      static_for<0, 16>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        constexpr int cum_i = i < 8 ? 2 * (i + 1) : 16 + (i - 7);   // reads in steps 0..i
+        constexpr int last = (i + PA < 16 ? i + PA : 15);
+        constexpr int cum_l = last < 8 ? 2 * (last + 1) : 16 + (last - 7);
+        if constexpr (i + PA < 16) rdA(std::integral_constant<int, i + PA>());
+        if constexpr (i < 8) {
+          asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(fq[i % (PA + 1)]), "+v"(fk[i % (PA + 1)]) : "i"(cum_l - cum_i) : "memory");
+          s = mfma32(fq[i % (PA + 1)], fk[i % (PA + 1)], s);
+        } else {
+          constexpr int ks = i - 8;
+          lgkm_tie1<cum_l - cum_i>(fd[ks % (PA + 1)]);
+          dp = mfma32(fd[ks % (PA + 1)], vf[ks], dp);
+          // softmax of S rows 2ks, 2ks+1 beside the dP MFMAs
+          constexpr int r0 = 2 * ks, r1 = 2 * ks + 1;
+          constexpr int row0 = (r0 & 3) + 8 * (r0 >> 2), row1 = (r1 & 3) + 8 * (r1 >> 2);
+          const float p0 = __builtin_amdgcn_exp2f(s[r0] * c), p1 = __builtin_amdgcn_exp2f(s[r1] * c);
+          s[r0] = kd > row0 ? 0.f : p0;
+          s[r1] = kd > row1 ? 0.f : p1;
+          pu[ks] = pack2(s[r0], s[r1]);
+        }
+      });
+      pf[0] = as_bf16x8(u32x4{pu[0], pu[1], pu[2], pu[3]});
+      pf[1] = as_bf16x8(u32x4{pu[4], pu[5], pu[6], pu[7]});
+      bf16x8 ft[PT + 1];
+      auto rdT = [&](auto jc) {
+        constexpr int j = decltype(jc)::value, t = FragJ<j>::t, ss = FragJ<j>::ss;
+        ft[j % (PT + 1)] = rd_tr2<(j < 8 ? OD : OQ)>(a_t[ss][0] ^ (64 * t), a_t[ss][1] ^ (64 * t));
+      };
+      static_for<0, PT>([&](auto jc) { rdT(jc); });
+      static_for<0, 16>([&](auto jc) {
+        constexpr int j = decltype(jc)::value, t = FragJ<j>::t, ss = FragJ<j>::ss, sl = j % (PT + 1);
+        if constexpr (j + PT < 16) rdT(std::integral_constant<int, j + PT>());
+        lgkm_tie1<2 * (j + PT < 16 ? PT : 15 - j)>(ft[sl]);
+        if constexpr (j < 8) {
+          dV[t] = mfma32(ft[sl], pf[ss], dV[t]);
+          // dS rows 2j, 2j+1 beside the dV MFMAs
+          pu[j] = pack2(s[2 * j] * dp[2 * j], s[2 * j + 1] * dp[2 * j + 1]);
+          if constexpr (j == 7) {
+            sf[0] = as_bf16x8(u32x4{pu[0], pu[1], pu[2], pu[3]});
+            sf[1] = as_bf16x8(u32x4{pu[4], pu[5], pu[6], pu[7]});
+          }
+        } else {
+          dK[t] = mfma32(ft[sl], sf[ss], dK[t]);
+        }
+      });
+      prio(0);
+    }
+#else
+    if (!CAUSAL || kw0 <= q0 + QT - 1) {
+      prio(1);
       float lse_v = rd_b32<OL>(a_ls), dl_v = rd_b32<OL + 128>(a_ls);
       bf16x8 fq[PA + 1], fk[PA + 1], fd[PA + 1];
       auto rdA = [&](auto kc) {
@@ -853,10 +966,11 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
       // transposed fragment j: j < 8 -> dO^T (dV), else Q^T (dK); column block t, row half ss
       bf16x8 ft[PT + 1];
       auto rdT = [&](auto jc) {
-        constexpr int j = decltype(jc)::value, t = (j & 7) >> 1, ss = j & 1;
+        constexpr int j = decltype(jc)::value, t = FragJ<j>::t, ss = FragJ<j>::ss;
         ft[j % (PT + 1)] = rd_tr2<(j < 8 ? OD : OQ)>(a_t[ss][0] ^ (64 * t), a_t[ss][1] ^ (64 * t));
       };
       static_for<0, PT>([&](auto jc) { rdT(jc); });
+      prio(0);
       const int key = kw0 + lr;
       const bool need_mask = CAUSAL && (kw0 + 31 > q0);
       if (need_mask) {
@@ -881,14 +995,17 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
         pf[ss] = as_bf16x8(u);
         sf[ss] = as_bf16x8(v);
       }
+      prio(1);
       static_for<0, 16>([&](auto jc) {
-        constexpr int j = decltype(jc)::value, t = (j & 7) >> 1, ss = j & 1, sl = j % (PT + 1);
+        constexpr int j = decltype(jc)::value, t = FragJ<j>::t, ss = FragJ<j>::ss, sl = j % (PT + 1);
         if constexpr (j + PT < 16) rdT(std::integral_constant<int, j + PT>());
         lgkm_tie1<2 * (j + PT < 16 ? PT : 15 - j)>(ft[sl]);
         if constexpr (j < 8) dV[t] = mfma32(ft[sl], pf[ss], dV[t]);
         else dK[t] = mfma32(ft[sl], sf[ss], dK[t]);
       });
+      prio(0);
     }
+#endif
     wait_dma_barrier();
   };
   {
