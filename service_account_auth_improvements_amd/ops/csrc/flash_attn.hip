@@ -261,11 +261,25 @@ __device__ __forceinline__ void wait_stage(int next, int last) {
   else vm_wait<0>();
 }
 
+// lane id from v_mbcnt in asm volatile: recomputed where used, never kept live in a VGPR
+__device__ __forceinline__ u32 lane_id_opaque() {
+  u32 x;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(x));
+  return x;
+}
+// 1 = K row fragments by inline asm, KF_FA_FWD_FP steps ahead + SGPR-base DMA; 0 = compiler-scheduled
+#ifndef KF_FA_FWD_PIPE
+#define KF_FA_FWD_PIPE 1
+#endif
+#ifndef KF_FA_FWD_FP
+#define KF_FA_FWD_FP 3
+#endif
+constexpr int FP = KF_FA_FWD_FP;
 template <bool CAUSAL>
 __global__ __launch_bounds__(512, 1) void flash_fwd_kernel(
     const bf16_t* __restrict__ qkv, long ld, bf16_t* __restrict__ out, long ldo,
     float* __restrict__ lse_out, int B, int S, int Hq, int Hkv, float scale_log2) {
-  __shared__ __attribute__((aligned(16))) char smem[NST * STG];
+  __shared__ __attribute__((aligned(1024))) char smem[NST * STG];
   const int nqb = (S + BQ8 - 1) / BQ8, G = Hq / Hkv;
   // logical order [b][hkv][q-block][g]: an XCD's contiguous range shares one K/V panel
   int lid = xcd_remap(blockIdx.x, B * Hq * nqb);
@@ -290,11 +304,29 @@ __global__ __launch_bounds__(512, 1) void flash_fwd_kernel(
   }
   const bf16_t* kp = qkv + (long)b * S * ld + (long)(Hq + hkv) * D;
   const bf16_t* vp = qkv + (long)b * S * ld + (long)(Hq + Hkv + hkv) * D;
+#if KF_FA_FWD_PIPE
+  u32 dma_kv;   // see the dQ kernel: one lane offset for the K and V panels
+  {
+    const int row = 4 * w + (l >> 4), ch = (l & 15) ^ swz_x(row);
+    dma_kv = (u32)((row * ld + ch * 8) * 2);
+  }
+  const u32 lds_w = lds_addr(smem) + 1024 * w;
+  auto stage = [&](int j) {
+    const u32 st = lds_w + (j % NST) * STG;
+    const char* kb_ = reinterpret_cast<const char*>(kp + (long)j * BK * ld);
+    const char* vb_ = reinterpret_cast<const char*>(vp + (long)j * BK * ld);
+    dma_sv(kb_, dma_kv, st);
+    dma_sv(kb_ + 64 * ld, dma_kv, st + 8192);
+    dma_sv(vb_, dma_kv, st + TILE);
+    dma_sv(vb_ + 64 * ld, dma_kv, st + TILE + 8192);
+  };
+#else
   auto stage = [&](int j) {
     char* st = smem + (j % NST) * STG;
     stage_rows(kp + (long)j * BK * ld, ld, st, BK, w, 8, l);
     stage_rows(vp + (long)j * BK * ld, ld, st + TILE, BK, w, 8, l);
   };
+#endif
   const int ntiles = CAUSAL ? min(S, qb * BQ8 + BQ8) / BK : S / BK;
   for (int j = 0; j < NST - 1 && j < ntiles; ++j) stage(j);
 
@@ -322,12 +354,32 @@ __global__ __launch_bounds__(512, 1) void flash_fwd_kernel(
       const char* Ks = smem + (j % NST) * STG;
       const char* Vs = Ks + TILE;
       f32x16 sc[2];   // S'^T = K (c Q)^T - m: key on the accumulator rows, query on the lane
+#if KF_FA_FWD_PIPE
+      // K row fragments by inline asm, FP steps ahead; the two 32-key chains alternate
+      const u32 ln = lane_id_opaque(), lr_ = ln & 31;
+      const u32 a_t = (lds_addr(smem) + (u32)((j % NST) * STG)) + lr_ * 256 + 16 * ((ln >> 5) ^ swz_x(lr_));
+      bf16x8 fk[FP + 1];
+      auto rdK = [&](auto ic) {
+        constexpr int i = decltype(ic)::value, kt = i & 1, ks = i >> 1;
+        fk[i % (FP + 1)] = rd_b128<8192 * kt>(a_t ^ (32 * ks));
+      };
+      static_for<0, FP>([&](auto ic) { rdK(ic); });
+      sc[0] = mfma32(ones, mref, f32x16{});
+      sc[1] = mfma32(ones, mref, f32x16{});
+      static_for<0, 16>([&](auto ic) {
+        constexpr int i = decltype(ic)::value, kt = i & 1, ks = i >> 1;
+        if constexpr (i + FP < 16) rdK(std::integral_constant<int, i + FP>());
+        lgkm_tie1<(i + FP < 16 ? FP : 15 - i)>(fk[i % (FP + 1)]);
+        sc[kt] = mfma32(fk[i % (FP + 1)], qf[ks], sc[kt]);
+      });
+#else
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
         sc[kt] = mfma32(ones, mref, f32x16{});
 #pragma unroll
         for (int ks = 0; ks < 8; ++ks) sc[kt] = mfma32(row_read(Ks, swz(32 * kt + lr, 2 * ks + hh)), qf[ks], sc[kt]);
       }
+#endif
       if (CAUSAL && k0 + BK - 1 > qmin_w) {   // a wave's diagonal tiles only (uniform branch)
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt)
@@ -474,12 +526,6 @@ __global__ __launch_bounds__(256) void flash_bwd_pre_kernel(const bf16_t* __rest
 #define KF_FA_DQ_QP 1
 #endif
 constexpr int QP = KF_FA_DQ_QP;
-// lane id from v_mbcnt in asm volatile: recomputed where used, never kept live in a VGPR
-__device__ __forceinline__ u32 lane_id_opaque() {
-  u32 x;
-  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(x));
-  return x;
-}
 template <int N>
 __device__ __forceinline__ void lgkm_tie2(bf16x8& a, bf16x8& b) {
   asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "i"(N) : "memory");
