@@ -735,11 +735,22 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dq_kernel(
 // Backward: dK / dV
 // ====================================================================================
 namespace fb {
-constexpr int OFF_K = 0;                       // [128 keys x 256 B] = 32 KB
-constexpr int OFF_Q = 32768;                   // [2][32 x 256 B]
+// waves per dK/dV workgroup (32 keys each): 4 = 128 keys, 66 KB LDS, 2 workgroups per CU;
+// 8 = 256 keys, 98 KB, 1 workgroup per CU (the same 2 waves per SIMD) -- every staged Q/dO
+// tile, its DMA issue and its barrier are then shared by twice the MFMA work
+#ifndef KF_FA_DKDV_NW
+#define KF_FA_DKDV_NW 4
+#endif
+constexpr int NWK = KF_FA_DKDV_NW;
+static_assert(NWK == 4 || NWK == 8, "dK/dV waves");
+constexpr int BKVW = 32 * NWK;                 // keys per workgroup
+// the per-iteration buffers sit first so their ds_read immediates (buffer + tile offsets)
+// stay below the 16-bit offset field; K (read through a per-wave VGPR base) follows
+constexpr int OFF_Q = 0;                       // [2][32 x 256 B]
 constexpr int OFF_DO = OFF_Q + 16384;          // [2][32 x 256 B]
 constexpr int OFF_LD = OFF_DO + 16384;         // [2][lse 32 f32 | delta 32 f32]
-constexpr int SMEM = OFF_LD + 512;             // 66048 B -> 2 workgroups per CU
+constexpr int OFF_K = OFF_LD + 512;            // [BKVW keys x 256 B] = 32 / 64 KB (256-B aligned)
+constexpr int SMEM = OFF_K + BKVW * 256;       // 66048 B (2 WG per CU) / 98816 B (1 WG per CU)
 // 1 = software-pipelined iteration (inline-asm LDS reads, counted waits); 0 = compiler-scheduled
 #ifndef KF_FA_DKDV_PIPE
 #define KF_FA_DKDV_PIPE 1
@@ -777,13 +788,13 @@ __device__ __forceinline__ void prio(int p) {
 }
 
 __host__ __device__ inline int n_chunks(int kb, int S, bool causal) {
-  const int q0 = causal ? kb * BKV : 0;
+  const int q0 = causal ? kb * BKVW : 0;
   return (S - q0 + QCH - 1) / QCH;
 }
 }  // namespace fb
 
 template <bool CAUSAL>
-__global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
+__global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kernel(
     const bf16_t* __restrict__ qkv, long ld, const bf16_t* __restrict__ dout, long lddo,
     const float* __restrict__ lse, const float* __restrict__ delta, float* __restrict__ dk_acc,
     float* __restrict__ dv_acc, int B, int S, int Hq, int Hkv, float scale, int items_per_head) {
@@ -794,14 +805,14 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
   int item = lid % items_per_head;
   const int bh = lid / items_per_head;
   const int hkv = bh % Hkv, b = bh / Hkv;
-  const int nkb = S / BKV;
+  const int nkb = S / BKVW;
   int kb = 0;
   for (; kb < nkb; ++kb) {
     const int n = n_chunks(kb, S, CAUSAL);
     if (item < n) break;
     item -= n;
   }
-  const int kv0 = kb * BKV;
+  const int kv0 = kb * BKVW;
   const int qs = (CAUSAL ? kv0 : 0) + item * QCH;
   const int qe = min(S, qs + QCH);
   const int ntq = (qe - qs) / QT;
@@ -815,7 +826,7 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
   const bf16_t* kp = qkv + rowB * ld + (long)(Hq + hkv) * D;
   const bf16_t* vp = qkv + rowB * ld + (long)(Hq + Hkv + hkv) * D;
 
-  stage_rows(kp + (long)kv0 * ld, ld, smem + OFF_K, BKV, w, 4, l);
+  stage_rows(kp + (long)kv0 * ld, ld, smem + OFF_K, BKVW, w, NWK, l);
   bf16x8 vf[8];  // B operand of dP = dO V^T: V[key][16ks + 8hh .. +8]
 #pragma unroll
   for (int ks = 0; ks < 8; ++ks) vf[ks] = as_bf16x8(ld16(vp + (long)(kw0 + lr) * ld + 16 * ks + 8 * hh));
@@ -845,9 +856,11 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
     const char* db_ = reinterpret_cast<const char*>(dout + (rowB + q0) * lddo + (long)h * D);
     const u32 lq = sbase + OFF_Q + buf * 8192 + 1024 * w, ldo_ = sbase + OFF_DO + buf * 8192 + 1024 * w;
     dma_sv(qb_, dma_q, lq);
-    dma_sv(qb_ + 32 * ld, dma_q, lq + 4096);
     dma_sv(db_, dma_do, ldo_);
-    dma_sv(db_ + 32 * lddo, dma_do, ldo_ + 4096);
+    if (NWK == 4) {
+      dma_sv(qb_ + 32 * ld, dma_q, lq + 4096);
+      dma_sv(db_ + 32 * lddo, dma_do, ldo_ + 4096);
+    }
 #else
     stage_rows(qkv + (rowB + q0) * ld + (long)h * D, ld, smem + OFF_Q + buf * 8192, QT, w, 4, l);
     stage_rows(dout + (rowB + q0) * lddo + (long)h * D, lddo, smem + OFF_DO + buf * 8192, QT, w, 4, l);
@@ -1127,24 +1140,30 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
     wait_dma_barrier();
   }
 #endif
-  // ---- chunk partial sums: transpose [d][key] accumulators through LDS, row-contiguous adds
+  // ---- chunk partial sums: transpose [d][key] accumulators through LDS, row-contiguous adds,
+  // 128 keys (4 waves' accumulators) per pass
   float* T = reinterpret_cast<float*>(smem);   // [128 keys][128 d] fp32 = 64 KB
   auto flush = [&](const f32x16(&acc)[4], float mul, float* dst_base) {
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+    for (int pass = 0; pass < NWK / 4; ++pass) {
+      if (w / 4 == pass) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int d = 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        const int key = 32 * w + lr;
-        T[key * 128 + (d ^ ((key & 31) << 2))] = acc[t][r] * mul;
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int d = 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hh;
+            const int key = 32 * (w & 3) + lr;
+            T[key * 128 + (d ^ ((key & 31) << 2))] = acc[t][r] * mul;
+          }
       }
-    __syncthreads();
-    float* dst = dst_base + (rowB + kv0) * (long)(Hkv * D) + (long)hkv * D;
-    for (int e = tid; e < BKV * 128; e += 256) {
-      const int key = e >> 7, d = e & 127;
-      atomicAdd(dst + (long)key * Hkv * D + d, T[key * 128 + (d ^ ((key & 31) << 2))]);
+      __syncthreads();
+      float* dst = dst_base + (rowB + kv0 + 128 * pass) * (long)(Hkv * D) + (long)hkv * D;
+      for (int e = tid; e < 128 * 128; e += 64 * NWK) {
+        const int key = e >> 7, d = e & 127;
+        atomicAdd(dst + (long)key * Hkv * D + d, T[key * 128 + (d ^ ((key & 31) << 2))]);
+      }
+      __syncthreads();
     }
-    __syncthreads();
   };
   flush(dK, scale, dk_acc);
   flush(dV, 1.f, dv_acc);
@@ -1490,7 +1509,7 @@ int kf_flash_bwd(const void* qkv, long ld, const void* o, long ldo, const void* 
                  long lddqkv, int B, int S, int Hq, int Hkv, int D_, float scale, int causal,
                  hipStream_t st) {
   using namespace fb;
-  if (D_ != D || S % BKV != 0 || S % BQ != 0 || Hq % Hkv != 0) return 1;
+  if (D_ != D || S % BKVW != 0 || S % BQ != 0 || Hq % Hkv != 0) return 1;
   const int T = B * S;
   const size_t acc_bytes = (size_t)T * Hkv * D * sizeof(float);
   BwdFork* fk = bwd_fork_enabled() ? bwd_fork() : nullptr;
@@ -1518,7 +1537,7 @@ int kf_flash_bwd(const void* qkv, long ld, const void* o, long ldo, const void* 
   if (kv64)
     for (int kb = 0; kb < S / fb2::BKV2; ++kb) items += fb2::n_chunks(kb, S, causal);
   else
-    for (int kb = 0; kb < S / BKV; ++kb) items += n_chunks(kb, S, causal);
+    for (int kb = 0; kb < S / BKVW; ++kb) items += n_chunks(kb, S, causal);
   const int g_kv = B * Hkv * items, g_q = B * Hq * ((S + BQ8 - 1) / BQ8);
   const float sl2 = scale * LOG2E;
   if (kv64) {
@@ -1531,13 +1550,13 @@ int kf_flash_bwd(const void* qkv, long ld, const void* o, long ldo, const void* 
   }
   if (causal) {
     if (!kv64)
-      flash_bwd_dkdv_kernel<true><<<g_kv, 256, 0, skv>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo,
+      flash_bwd_dkdv_kernel<true><<<g_kv, 64 * NWK, 0, skv>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo,
                                                          lse, delta, dk_acc, dv_acc, B, S, Hq, Hkv, scale, items);
     flash_bwd_dq_kernel<true><<<g_q, 512, 0, st>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo, lse,
                                                    delta, (bf16_t*)dqkv, lddqkv, B, S, Hq, Hkv, sl2, scale);
   } else {
     if (!kv64)
-      flash_bwd_dkdv_kernel<false><<<g_kv, 256, 0, skv>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo,
+      flash_bwd_dkdv_kernel<false><<<g_kv, 64 * NWK, 0, skv>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo,
                                                         lse, delta, dk_acc, dv_acc, B, S, Hq, Hkv, scale, items);
     flash_bwd_dq_kernel<false><<<g_q, 512, 0, st>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo, lse,
                                                     delta, (bf16_t*)dqkv, lddqkv, B, S, Hq, Hkv, sl2, scale);

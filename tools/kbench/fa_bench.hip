@@ -57,7 +57,7 @@ int main(int argc, char** argv) {
 
   int items = 0, items64 = 0;
   const int g_q = B * Hq * ((S + BQ8 - 1) / BQ8), g_f = B * Hq * ((S + BQ8 - 1) / BQ8);
-  for (int kb = 0; kb < S / BKV; ++kb) items += fb::n_chunks(kb, S, true);
+  for (int kb = 0; kb < S / fb::BKVW; ++kb) items += fb::n_chunks(kb, S, true);
   for (int kb = 0; kb < S / fb2::BKV2; ++kb) items64 += fb2::n_chunks(kb, S, true);
   const int g_kv64 = B * Hkv * items64, g_kv = B * Hkv * items;
   const char* dkv_env = getenv("KFAMD_FA_DKDV");
@@ -66,7 +66,7 @@ int main(int argc, char** argv) {
     if (use64)
       flash_bwd_dkdv64_kernel<true><<<g_kv64, 256>>>(qkv, ldq, dout, ldo, lse, delta, dk, dv, B, S, Hq, Hkv, scale, items64);
     else
-      flash_bwd_dkdv_kernel<true><<<g_kv, 256>>>(qkv, ldq, dout, ldo, lse, delta, dk, dv, B, S, Hq, Hkv, scale, items);
+      flash_bwd_dkdv_kernel<true><<<g_kv, 64 * fb::NWK>>>(qkv, ldq, dout, ldo, lse, delta, dk, dv, B, S, Hq, Hkv, scale, items);
   };
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
