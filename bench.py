@@ -133,6 +133,8 @@ def main():
                          "fp32 micro-batch accumulation) or bf16 (RCCL bf16 reduce-scatter / all-reduce)")
     ap.add_argument("--tp", type=int, default=1, help="tensor parallel degree (configs[4]: 70B TP=8)")
     ap.add_argument("--pp", type=int, default=1, help="pipeline parallel degree (1F1B)")
+    ap.add_argument("--pp-virtual", type=int, default=1,
+                    help="model chunks per pipeline rank; > 1 = interleaved 1F1B (--grad-accum a multiple of --pp)")
     ap.add_argument("--cp", action="store_true",
                     help="context parallelism (long context): the N data-parallel ranks become ONE group "
                          "sharing the same sequences, 1/N of every sequence's tokens per GPU "
@@ -196,7 +198,7 @@ def main():
                        grad_reduce=a.grad_reduce,
                        n_layers=a.layers, recompute=a.recompute, head_chunk=a.head_chunk,
                        force_collectives=a.force_collectives, sequence_parallel=a.sp,
-                       context_parallel=a.cp)
+                       context_parallel=a.cp, pp_virtual=a.pp_virtual)
     t0 = time.time()
     if a.pp > 1:
         from service_account_auth_improvements_amd.parallel.pipeline import PipelineTrainer
@@ -267,6 +269,7 @@ def main():
                 "grad_reduce": a.grad_reduce,
                 "micro_batch": a.micro_batch,
                 "grad_accum": a.grad_accum,
+                "pp_virtual": a.pp_virtual,
                 "n_layers": tr.mcfg.n_layers,
                 "attention": "hip",
                 "activation_recompute": a.recompute,

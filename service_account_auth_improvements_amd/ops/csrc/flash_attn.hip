@@ -526,6 +526,10 @@ __global__ __launch_bounds__(256) void flash_bwd_pre_kernel(const bf16_t* __rest
 #define KF_FA_DQ_QP 1
 #endif
 constexpr int QP = KF_FA_DQ_QP;
+// 1 = -lse enters through the exp's FMA (per-lane constant); 0 = folded MFMA per 32-key chain
+#ifndef KF_FA_DQ_LSEFMA
+#define KF_FA_DQ_LSEFMA 1
+#endif
 template <int N>
 __device__ __forceinline__ void lgkm_tie2(bf16x8& a, bf16x8& b) {
   asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "i"(N) : "memory");
@@ -596,7 +600,12 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dq_kernel(
 #pragma unroll
   for (int ks = 0; ks < 8; ++ks) asm volatile("" : "+v"(qf[ks]), "+v"(df[ks]));
   asm volatile("" : "+v"(lse_s), "+v"(dl));
-  const bf16x8 ones = fold_ones(hh), lse_b = fold_const(lse_s, hh), dl_b = fold_const(dl, hh);
+  const bf16x8 ones = fold_ones(hh), dl_b = fold_const(dl, hh);
+#if KF_FA_DQ_PIPE
+  const float nlse = KF_FA_DQ_LSEFMA ? -lse_s * scale_log2 : 0.f;
+#else
+  const bf16x8 lse_b = fold_const(lse_s, hh);
+#endif
   f32x16 dq[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) dq[t] = f32x16{};
@@ -632,7 +641,9 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dq_kernel(
       static_for<0, 16>([&](auto ic) {
         constexpr int i = decltype(ic)::value, kt = i >> 3, ks = i & 7, sl = i % (QP + 1);
         if constexpr (ks == 0) {
-          s = mfma32(ones, lse_b, f32x16{});
+          // -lse is a per-LANE constant here (query on the lane): it goes into the exp's FMA
+          // below instead of a folded MFMA; -delta stays folded (dS needs dP' = dP - delta)
+          s = KF_FA_DQ_LSEFMA ? f32x16{} : mfma32(ones, fold_const(lse_s, hh), f32x16{});
           dp = mfma32(ones, dl_b, f32x16{});
         }
         if constexpr (i + QP < 16) rdS(std::integral_constant<int, i + QP>());
@@ -649,7 +660,7 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dq_kernel(
             }
           }
 #pragma unroll
-          for (int r = 0; r < 16; ++r) s[r] = __builtin_amdgcn_exp2f(s[r] * scale_log2) * dp[r];   // dS^T (unscaled)
+          for (int r = 0; r < 16; ++r) s[r] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[r], scale_log2, nlse)) * dp[r];   // dS^T (unscaled)
 #pragma unroll
           for (int ss = 0; ss < 2; ++ss) {
             u32x4 u;

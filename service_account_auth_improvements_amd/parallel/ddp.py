@@ -112,12 +112,13 @@ class GradReducer:
         then writes each micro-batch's gradients fresh, ``accumulate=False``)."""
         return self.fp32 and self.grad_accum > 1
 
-    def accumulate_micro(self, first: bool):
-        """After a NON-final micro-batch's backward: main (=|+=) grads, in fp32."""
+    def accumulate_micro(self, first: bool, groups: Optional[List[FlatGroup]] = None):
+        """After a NON-final micro-batch's backward: main (=|+=) grads, in fp32 (``groups``:
+        only those, e.g. the one pipeline chunk whose backward just ran)."""
         if not self.fp32_accumulation:
             return
         self._accumulated = True
-        for g in self.groups:
+        for g in (self.groups if groups is None else groups):
             ops.grad_accum_(self.main[g.name], g.grads, ops.GRAD_SET if first else ops.GRAD_ADD)
 
     def grad_view(self, group: FlatGroup, lo: int, hi: int) -> torch.Tensor:

@@ -52,10 +52,50 @@ class P2P:
         # orders its own stream against the compute stream.
         self._host = torch.device(device).type == "cuda" and dist.get_backend() == "gloo"
         self._inflight: list = []       # (works, tensors) of send-only groups not yet waited for
+        self._groups: list = []         # interleaved schedule: (group record, tensors) with sends
         self.sends_deferred = 0         # send-only groups left in flight (tests)
 
     def _buf(self):
         return torch.empty(self.shape, dtype=self.dtype, device=self.device)
+
+    # -- interleaved schedule: ring neighbours and tick exchanges (see interleaved_1f1b)
+    @property
+    def ring_next(self) -> int:
+        st = self.st
+        return ((((st.pp_rank + 1) % st.pp) * st.dp + st.dp_rank) * st.tp + st.tp_rank)
+
+    @property
+    def ring_prev(self) -> int:
+        st = self.st
+        return ((((st.pp_rank - 1) % st.pp) * st.dp + st.dp_rank) * st.tp + st.tp_rank)
+
+    def exchange(self, sends, recvs):
+        """Post one group: ``sends`` = [(tensor, peer)], ``recvs`` = [(kind, key, peer)].
+        Returns [(kind, key, peer, handle)]; :meth:`take` waits for a handle and returns its
+        tensor.  Send-only groups are deferred like the 1F1B path's."""
+        ops_ = [dist.P2POp(dist.isend, t.contiguous(), peer) for t, peer in sends]
+        bufs = [(kind, key, peer, self._buf()) for kind, key, peer in recvs]
+        ops_ += [dist.P2POp(dist.irecv, b, peer) for _, _, peer, b in bufs]
+        if not ops_:
+            return []
+        if not bufs or self._host:
+            self._run(ops_)              # gloo + GPU tensors: staged and waited here
+            return [(kind, key, peer, (None, b)) for kind, key, peer, b in bufs]
+        # one record per group, waited at most once (a second wait() on a completed gloo receive
+        # waits for ANOTHER message): by the first take() of one of its tensors, else by flush()
+        grp = {"works": dist.batch_isend_irecv(ops_), "done": False}
+        if sends:
+            self._groups.append((grp, [op.tensor for op in ops_]))
+        return [(kind, key, peer, (grp, b)) for kind, key, peer, b in bufs]
+
+    @staticmethod
+    def take(handle):
+        grp, t = handle
+        if grp is not None and not grp["done"]:
+            for w in grp["works"]:
+                w.wait()
+            grp["done"] = True
+        return t
 
     def flush(self):
         """Wait for every deferred send (before the optimizer step reuses any buffer)."""
@@ -63,6 +103,12 @@ class P2P:
             for w in works:
                 w.wait()
         self._inflight.clear()
+        for grp, _ in self._groups:
+            if not grp["done"]:
+                for w in grp["works"]:
+                    w.wait()
+                grp["done"] = True
+        self._groups.clear()
 
     def _run(self, ops):
         if not ops:
@@ -189,6 +235,178 @@ def one_f_one_b(model: Llama, p2p: P2P, micro_batches: List[Tuple[torch.Tensor, 
     return total
 
 
+# ---------------------------------------------------------------------------------------------
+# Interleaved 1F1B (virtual pipeline stages)
+# ---------------------------------------------------------------------------------------------
+# Each rank holds v layer chunks; chunk c of rank r is virtual stage c*pp + r, so a micro-batch
+# passes every rank v times and the fill/drain bubble shrinks by v.  The per-rank op order is
+# the usual interleaved one (micro-batches in groups of pp, chunk-major inside a group; warm-up
+# 2(pp - r - 1) + (v - 1) pp forwards, then one forward / one backward, then the drain).
+#
+# Transfers: every rank simulates the SAME global timeline -- in each tick a rank runs its next
+# op if that op's inputs were produced in an earlier tick -- and in tick t posts one P2P group:
+# the output it produced in tick t (to the ring neighbour that consumes it) plus receives for
+# what its two neighbours produced in tick t for it.  Both ends of every transfer derive it from
+# the same simulation, so the groups match pairwise and nothing can deadlock.  A received tensor
+# is waited for only when the op that consumes it runs (a stream dependency under RCCL), and
+# send-only groups stay in flight until the end of the step.
+
+
+def interleaved_order(pp: int, v: int, M: int, rank: int) -> List[Tuple[str, int, int]]:
+    """Op list ("F" | "B", micro-batch, chunk) of pipeline rank ``rank``."""
+    assert M % pp == 0, f"interleaved schedule: micro-batches ({M}) must be a multiple of pp ({pp})"
+    N = M * v
+
+    def mb(k):
+        return (k // (pp * v)) * pp + k % pp
+
+    def fchunk(k):
+        return (k // pp) % v
+
+    def bchunk(k):
+        return v - 1 - (k // pp) % v
+
+    warm = N if M == pp else min(N, 2 * (pp - rank - 1) + (v - 1) * pp)
+    ops_: List[Tuple[str, int, int]] = [("F", mb(k), fchunk(k)) for k in range(warm)]
+    for i in range(N - warm):
+        ops_.append(("F", mb(warm + i), fchunk(warm + i)))
+        ops_.append(("B", mb(i), bchunk(i)))
+    ops_ += [("B", mb(k), bchunk(k)) for k in range(N - warm, N)]
+    return ops_
+
+
+def simulate_interleaved(pp: int, v: int, M: int):
+    """Global lockstep timeline: ``ticks[t][r]`` = the op rank r runs in tick t (or None).
+    An op runs once its remote input was produced in an EARLIER tick (a backward also needs
+    its own forward, which always precedes it in the rank's list)."""
+    orders = [interleaved_order(pp, v, M, r) for r in range(pp)]
+    last_vs = pp * v - 1
+    done = {}                     # (kind, m, vs) -> tick
+    pos = [0] * pp
+    ticks = []
+    while any(pos[r] < len(orders[r]) for r in range(pp)):
+        t = len(ticks)
+        row = [None] * pp
+        for r in range(pp):
+            if pos[r] >= len(orders[r]):
+                continue
+            kind, m, c = orders[r][pos[r]]
+            vs = c * pp + r
+            if kind == "F":
+                ok = vs == 0 or done.get(("F", m, vs - 1), t) < t
+            else:
+                ok = done.get(("F", m, vs), t) < t and (vs == last_vs or done.get(("B", m, vs + 1), t) < t)
+            if ok:
+                row[r] = (kind, m, c)
+        if not any(row):
+            raise RuntimeError("interleaved schedule simulation stalled")
+        for r, op in enumerate(row):
+            if op is not None:
+                done[(op[0], op[1], op[2] * pp + r)] = t
+                pos[r] += 1
+        ticks.append(row)
+    return ticks
+
+
+def interleaved_1f1b(chunks: List[Llama], st: ParallelState, p2p: "P2P", micro_batches,
+                     scale: float, on_last_backward=None, reducer=None) -> Optional[torch.Tensor]:
+    """One optimizer step of micro-batches through this rank's ``chunks`` (virtual stages
+    c*pp + pp_rank).  Returns the summed loss on the rank holding the last virtual stage."""
+    pp, v, r = st.pp, len(chunks), st.pp_rank
+    M = len(micro_batches)
+    B, S = micro_batches[0][0].shape
+    last_vs = pp * v - 1
+    ticks = simulate_interleaved(pp, v, M)
+    nxt, prv = p2p.ring_next, p2p.ring_prev
+    acts, grads, ctxs, losses = {}, {}, {}, []
+    n_bwd = [0] * v
+    f32acc = reducer is not None and reducer.fp32_accumulation
+
+    for row in ticks:
+        op = row[r]
+        out = None
+        if op is not None:
+            kind, m, c = op
+            vs = c * pp + r
+            model = chunks[c]
+            if kind == "F":
+                tok, lab = micro_batches[m]
+                inp = tok.reshape(-1) if vs == 0 else p2p.take(acts.pop((m, c)))
+                y, ctx = model.stage_forward(inp, B, S, lab.reshape(-1), scale)
+                ctxs[(m, c)] = ctx
+                if vs == last_vs:
+                    losses.append(y)          # filled in by this micro-batch's head backward
+                else:
+                    out = y
+            else:
+                g = None if vs == last_vs else p2p.take(grads.pop((m, c)))
+                last_of_chunk = n_bwd[c] == M - 1
+                if on_last_backward is not None:
+                    on_last_backward(last_of_chunk, model)
+                gin = model.stage_backward(ctxs.pop((m, c)), g, B, S,
+                                           accumulate=n_bwd[c] > 0 and not f32acc)
+                if reducer is not None and not last_of_chunk:
+                    reducer.accumulate_micro(first=n_bwd[c] == 0, groups=model.groups)
+                if on_last_backward is not None and last_of_chunk:
+                    on_last_backward(False, model)
+                n_bwd[c] += 1
+                out = gin if vs > 0 else None
+        # this tick's transfers (identical derivation on both ends)
+        sends, recvs = [], []
+        if out is not None:
+            kind = op[0]
+            sends.append((out, nxt if kind == "F" else prv))
+        pr, nr = (r - 1) % pp, (r + 1) % pp
+        po, no = row[pr], row[nr]
+        if po is not None and po[0] == "F" and po[2] * pp + pr != last_vs:
+            c_me = po[2] + 1 if r == 0 else po[2]        # rank pp-1 feeds chunk c+1 of rank 0
+            recvs.append(("act", (po[1], c_me), prv))
+        if no is not None and no[0] == "B" and no[2] * pp + nr != 0:
+            c_me = no[2] - 1 if r == pp - 1 else no[2]   # rank 0 feeds chunk c-1 of rank pp-1
+            recvs.append(("grad", (no[1], c_me), nxt))
+        for kind, key, peer, handle in p2p.exchange(sends, [(k, key, peer) for k, key, peer in recvs]):
+            (acts if kind == "act" else grads)[key] = handle
+    p2p.flush()
+    total = None
+    for lv in losses:
+        total = lv if total is None else total + lv
+    return total
+
+
+class _Chunks:
+    """This rank's v virtual-stage models seen as one model: the optimizer and the DP reducer
+    work on all their flat groups (renamed per chunk), P / G look a parameter up by name."""
+
+    def __init__(self, chunks: List[Llama]):
+        self.chunks = chunks
+        self.groups = [g for c in chunks for g in c.groups]
+        self.first = chunks[0].first
+        self.last = chunks[-1].last
+
+    def _owner(self, name):
+        for c in self.chunks:
+            if name in c.mats._index or name in c.norms._index:
+                return c
+        raise KeyError(name)
+
+    def P(self, name):
+        return self._owner(name).P(name)
+
+    def G(self, name):
+        return self._owner(name).G(name)
+
+    def __setattr__(self, key, value):
+        # per-model hooks (param_wait, on_grad_ready, recompute, ...) go to every chunk
+        if key in ("chunks", "groups", "first", "last"):
+            object.__setattr__(self, key, value)
+        else:
+            for c in self.chunks:
+                setattr(c, key, value)
+
+    def __getattr__(self, key):
+        return getattr(self.chunks[0], key)
+
+
 class PipelineTrainer:
     """DP x PP (x TP) training with 1F1B; same optimizer / reducer as the DP trainer."""
 
@@ -202,8 +420,22 @@ class PipelineTrainer:
         if tcfg.seq_len > mcfg.max_seq:
             mcfg = mcfg.with_(max_seq=tcfg.seq_len)
         self.mcfg = mcfg
-        lr = stage_layers(mcfg.n_layers, st.pp, st.pp_rank)
-        self.model = Llama(mcfg, st, layer_range=lr, seed=tcfg.seed, full_init=full_init)
+        self.v = v = max(1, int(getattr(tcfg, "pp_virtual", 1)))
+        if v == 1:
+            lr = stage_layers(mcfg.n_layers, st.pp, st.pp_rank)
+            self.model = Llama(mcfg, st, layer_range=lr, seed=tcfg.seed, full_init=full_init)
+        else:
+            # interleaved schedule: chunk c holds virtual stage c*pp + pp_rank; its flat groups are
+            # renamed per chunk (the reducer and the optimizer key their state by group name)
+            assert st.pp > 1 and mcfg.n_layers >= st.pp * v, "pp_virtual needs pp > 1 and >= pp*v layers"
+            chunks = []
+            for c in range(v):
+                lr = stage_layers(mcfg.n_layers, st.pp * v, c * st.pp + st.pp_rank)
+                m = Llama(mcfg, st, layer_range=lr, seed=tcfg.seed, full_init=full_init)
+                for g in m.groups:
+                    g.name = f"{g.name}.v{c}"
+                chunks.append(m)
+            self.model = _Chunks(chunks)
         self.model.recompute = tcfg.recompute
         self.model.head_chunk = getattr(tcfg, "head_chunk", self.model.head_chunk)
         self.model.sequence_parallel = getattr(tcfg, "sequence_parallel", False)
@@ -212,7 +444,8 @@ class PipelineTrainer:
         assert not getattr(tcfg, "context_parallel", False), "context parallelism is not combined with PP"
         zero1 = getattr(tcfg, "zero1", False)
         force = getattr(tcfg, "force_collectives", False)
-        self.model.allocate(pad_to=st.dp * 64 if zero1 else 1)
+        for m in (self.model.chunks if v > 1 else [self.model]):
+            m.allocate(pad_to=st.dp * 64 if zero1 else 1)
         # ZeRO-1 per stage: each DP replica group of a stage reduce-scatters its gradients, owns
         # 1/dp of the stage's AdamW state and all-gathers the updated parameters, which the next
         # step's forward waits for bucket by bucket (as the flat DP trainer does)
@@ -231,7 +464,8 @@ class PipelineTrainer:
                                          max_grad_norm=tcfg.max_grad_norm),
                              shard_ranges=shard, dp_group=st.dp_group,
                              norm_groups=[st.pp_group] if st.pp > 1 else None,
-                             tp_sharded={"matrices": st.tp_group} if st.tp > 1 else None,
+                             tp_sharded={g.name: st.tp_group for g in self.model.groups
+                                         if g.name.split(".")[0] == "matrices"} if st.tp > 1 else None,
                              grad_view=self.reducer.grad_view)
         self.overlap_allgather = mode == "reduce_scatter" and getattr(tcfg, "overlap_allgather", True)
         if self.overlap_allgather:
@@ -242,13 +476,17 @@ class PipelineTrainer:
         self.p2p = P2P(st, (T, mcfg.hidden), torch.bfloat16, st.device)
         self.step_idx = 0          # optimizer steps taken (restored by load_checkpoint)
 
-    def _hook(self, on: bool):
-        self.model.on_grad_ready = self.reducer.grad_ready if on else None
+    def _hook(self, on: bool, model=None):
+        (model if model is not None else self.model).on_grad_ready = self.reducer.grad_ready if on else None
 
     def train_step(self, micro_batches):
         ntok = sum(t.numel() for t, _ in micro_batches)
         self.reducer.start_step()
-        loss = one_f_one_b(self.model, self.p2p, micro_batches, 1.0 / ntok, self._hook, reducer=self.reducer)
+        if self.v > 1:
+            loss = interleaved_1f1b(self.model.chunks, self.st, self.p2p, micro_batches, 1.0 / ntok, self._hook,
+                                    reducer=self.reducer)
+        else:
+            loss = one_f_one_b(self.model, self.p2p, micro_batches, 1.0 / ntok, self._hook, reducer=self.reducer)
         self.reducer.wait_all_params()     # a bucket the forward never read (padding) must land too
         self.reducer.finish()
         self.opt.step(grad_scale=1.0 / self.st.dp)

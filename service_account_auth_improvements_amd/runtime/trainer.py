@@ -56,6 +56,9 @@ class TrainConfig:
     # every TP collective, then one full-batch backward (models/llama.py stage_forward_dual);
     # needs an even micro-batch, one pipeline stage, no recomputation and no SP.
     tp_dual_batch: bool = False
+    # pipeline: model chunks (virtual stages) per rank; > 1 selects the interleaved 1F1B schedule
+    # (parallel/pipeline.py interleaved_1f1b; micro-batches per step a multiple of pp)
+    pp_virtual: int = 1
 
 
 class Trainer:

@@ -153,3 +153,17 @@ def test_crd_device_release_wait_watches_only_our_cards(tmp_path):
     assert crdbench.wait_device_release(base, base, root=str(tmp_path)) < 0.05
     card(0, 90 * gib)
     assert 0.2 <= crdbench.wait_device_release(base, held, timeout=0.2, root=str(tmp_path), poll=0.01) < 1.0
+
+
+def test_bench_pipeline_interleaved_two_ranks():
+    """``--pp 2 --pp-virtual 2``: the interleaved 1F1B path end to end under torchrun (gloo)."""
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1")
+    args = [x for x in ARGS] + ["--pp", "2", "--pp-virtual", "2", "--grad-accum", "2", "--layers", "4"]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2", *args]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-2000:]
+    (rec,) = _json_lines(r.stdout)
+    assert rec["config"]["parallelism"] == "dp1pp2" and rec["config"]["pp_virtual"] == 2
+    assert rec["config"]["global_batch"] == 2 and rec["value"] > 0
+    assert rec["loss_first"] > 0
