@@ -106,7 +106,7 @@ def test_tensor_parallel_two_ranks_one_gpu_matches_tp1(sp):
     assert ((res[0][1] - norms).abs().max() / norms.abs().max()).item() < 1e-2
 
 
-def _pp_body(rank, world, n_micro):
+def _pp_body(rank, world, n_micro, v=1):
     import os
 
     os.environ["KFAMD_DIST_BACKEND"] = "gloo"
@@ -115,7 +115,8 @@ def _pp_body(rank, world, n_micro):
     from service_account_auth_improvements_amd.runtime.trainer import TrainConfig
 
     st = init_distributed(tp=1, pp=world, device="cuda")
-    tr = PipelineTrainer(TrainConfig(model="small", seq_len=256, lr=0.0, micro_batch=2, n_layers=4), st)
+    tr = PipelineTrainer(TrainConfig(model="small", seq_len=256, lr=0.0, micro_batch=2, n_layers=4,
+                                     pp_virtual=v), st)
     mbs = [(x.to(st.device), y.to(st.device)) for x, y in _batches(tr.mcfg.vocab_size, n_micro, seed=5)]
     loss = tr.train_step(mbs)
     torch.cuda.synchronize()
@@ -123,17 +124,18 @@ def _pp_body(rank, world, n_micro):
     return (float(loss) if loss is not None else None), grads
 
 
-def test_pipeline_two_stages_one_gpu_matches_single_stage():
-    """1F1B over 2 stages (activations / gradients sent between the ranks) == one stage."""
+@pytest.mark.parametrize("n_micro,v", [(3, 1), (4, 2)], ids=["1f1b", "interleaved-v2"])
+def test_pipeline_two_stages_one_gpu_matches_single_stage(n_micro, v):
+    """1F1B (and interleaved 1F1B, 2 chunks per rank) over 2 stages (activations / gradients
+    sent between the ranks) == one stage."""
     from service_account_auth_improvements_amd.parallel.state import ParallelState
     from service_account_auth_improvements_amd.runtime.trainer import TrainConfig, Trainer
 
-    n_micro = 3
     st = ParallelState(device=torch.device("cuda", 0))
     ref = Trainer(TrainConfig(model="small", seq_len=256, lr=0.0, micro_batch=2, n_layers=4), st)
     mbs = [(x.to(st.device), y.to(st.device)) for x, y in _batches(ref.mcfg.vocab_size, n_micro, seed=5)]
     ref_loss = float(ref.train_step(mbs))
-    res = run_ranks(_pp_body, world=2, args=(n_micro,), timeout=300)
+    res = run_ranks(_pp_body, world=2, args=(n_micro, v), timeout=300)
     assert res[0][0] is None and abs(res[1][0] - ref_loss) < 5e-3 * ref_loss
     seen = set()
     for _, grads in res:
