@@ -1,6 +1,6 @@
 """Interleaved 1F1B (virtual pipeline stages, parallel/pipeline.py ``interleaved_1f1b``) on gloo:
-the simulated tick timeline, then pp2 x v2, pp4 x v2 and dp2 x pp2 x v2 (ZeRO-1, fp32 micro-batch
-accumulation) training against one process running the same global batch."""
+the simulated tick timeline, then pp2 x v2, pp4 x v2, dp2 x pp2 x v2 (ZeRO-1, fp32 micro-batch
+accumulation) and tp2 x pp2 x v2 training against one process running the same global batch."""
 import pytest
 import torch
 
@@ -50,11 +50,11 @@ def test_interleaved_order_rejects_partial_groups():
         interleaved_order(4, 2, 6, 0)
 
 
-def _body(rank, world, pp, v, n_micro, dp_steps):
+def _body(rank, world, pp, v, n_micro, dp_steps, tp=1):
     from service_account_auth_improvements_amd.parallel.pipeline import PipelineTrainer
     from service_account_auth_improvements_amd.parallel.state import init_distributed
     from service_account_auth_improvements_amd.runtime.trainer import TrainConfig
-    st = init_distributed(tp=1, pp=pp, device="cpu")
+    st = init_distributed(tp=tp, pp=pp, device="cpu")
     tcfg = TrainConfig(model="tiny", seq_len=32, micro_batch=2, grad_accum=n_micro, n_layers=pp * v, lr=LR,
                        zero1=st.dp > 1, bucket_mb=1, grad_reduce="fp32", pp_virtual=v)
     tr = PipelineTrainer(tcfg, st, full_init=True)
@@ -68,7 +68,7 @@ def _body(rank, world, pp, v, n_micro, dp_steps):
     params = {s.name: tr.model.P(s.name).float().clone() for g in tr.model.groups for s in g.specs}
     names = sorted(g.name for g in tr.model.groups)
     return dict(losses=losses, params=params, coords=(st.dp_rank, st.pp_rank), dp=st.dp, groups=names,
-                deferred=tr.p2p.sends_deferred)
+                deferred=tr.p2p.sends_deferred, tp_rank=st.tp_rank)
 
 
 def _reference(n_layers, n_batches_per_step):
@@ -81,11 +81,14 @@ def _reference(n_layers, n_batches_per_step):
     return tr, losses
 
 
-@pytest.mark.parametrize("world,pp,v,n_micro", [(2, 2, 2, 2), (2, 2, 2, 4), (4, 4, 2, 4), (4, 2, 2, 2)],
-                         ids=["pp2v2m2", "pp2v2m4", "pp4v2m4", "dp2xpp2v2-zero1"])
-def test_interleaved_training_matches_single_process(world, pp, v, n_micro):
-    res = run_ranks(_body, world=world, args=(pp, v, n_micro, STEPS), timeout=600)
-    dp = world // pp
+@pytest.mark.parametrize("world,pp,v,n_micro,tp", [(2, 2, 2, 2, 1), (2, 2, 2, 4, 1), (4, 4, 2, 4, 1), (4, 2, 2, 2, 1),
+                                                   (4, 2, 2, 2, 2)],
+                         ids=["pp2v2m2", "pp2v2m4", "pp4v2m4", "dp2xpp2v2-zero1", "tp2xpp2v2"])
+def test_interleaved_training_matches_single_process(world, pp, v, n_micro, tp):
+    from service_account_auth_improvements_amd.models.llama import Llama
+    from service_account_auth_improvements_amd.parallel.state import ParallelState
+    res = run_ranks(_body, world=world, args=(pp, v, n_micro, STEPS, tp), timeout=600)
+    dp = world // (pp * tp)
     ref, ref_losses = _reference(pp * v, dp * n_micro)
     # each rank holds v chunks (groups renamed per chunk) and left send-only groups in flight
     for r in res:
@@ -98,8 +101,12 @@ def test_interleaved_training_matches_single_process(world, pp, v, n_micro):
         assert abs(got - ref_losses[step]) < 1e-2 * ref_losses[step], (step, got, ref_losses[step])
     seen = set()
     for r in res:
+        sl = Llama(ref.mcfg, ParallelState(tp=tp, tp_rank=r["tp_rank"]), device="cpu", seed=1234,
+                   full_init=True)._tp_slicers() if tp > 1 else {}
         for name, got in r["params"].items():
             want = ref.model.P(name).float()
+            if name in sl:
+                want = sl[name][1](want)
             diff = (got - want).abs()
             assert diff.max().item() <= 2 * LR * STEPS + 1e-3, (r["coords"], name, diff.max().item())
             assert (diff <= 2e-4 + 1e-2 * want.abs()).float().mean().item() > 0.98, (r["coords"], name)
@@ -107,7 +114,7 @@ def test_interleaved_training_matches_single_process(world, pp, v, n_micro):
     assert seen == {s.name for g in ref.model.groups for s in g.specs}
     by = {}
     for r in res:
-        by.setdefault(r["coords"][1], []).append(r["params"])
+        by.setdefault((r["coords"][1], r["tp_rank"]), []).append(r["params"])
     for reps in by.values():
         for other in reps[1:]:
             for name in reps[0]:
