@@ -403,8 +403,15 @@ class _Chunks:
             for c in self.chunks:
                 setattr(c, key, value)
 
+    # settings every chunk shares; anything per chunk (mats, norms, layers, ...) must be reached
+    # through ``chunks`` -- no silent fallback to chunk 0
+    _SHARED = frozenset({"cfg", "st", "tp", "hq", "hkv", "ff", "vl", "device", "head_chunk", "recompute",
+                         "sequence_parallel", "tp_comm_chunks", "cp", "param_wait", "on_grad_ready"})
+
     def __getattr__(self, key):
-        return getattr(self.chunks[0], key)
+        if key in _Chunks._SHARED:
+            return getattr(self.chunks[0], key)
+        raise AttributeError(f"{key!r} is per pipeline chunk: use .chunks[c].{key}")
 
 
 class PipelineTrainer:
