@@ -62,6 +62,8 @@ def main(argv=None):
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--tp", type=int, default=1)
     ap.add_argument("--pp", type=int, default=1)
+    ap.add_argument("--pp-virtual", type=int, default=1,
+                    help="model chunks per pipeline rank (> 1: interleaved 1F1B; --grad-accum a multiple of --pp)")
     ap.add_argument("--zero1", action="store_true")
     ap.add_argument("--sp", action="store_true", help="sequence parallelism on top of --tp (Megatron SP)")
     ap.add_argument("--cp", action="store_true",
@@ -106,7 +108,7 @@ def main(argv=None):
     tcfg = TrainConfig(model=a.model, seq_len=a.seq_len, micro_batch=a.micro_batch, grad_accum=a.grad_accum,
                        zero1=a.zero1, n_layers=a.layers, sequence_parallel=a.sp, context_parallel=a.cp,
                        recompute=a.recompute,
-                       grad_reduce=a.grad_reduce, head_chunk=a.head_chunk)
+                       grad_reduce=a.grad_reduce, head_chunk=a.head_chunk, pp_virtual=a.pp_virtual)
     if a.pp > 1:
         from ..parallel.pipeline import PipelineTrainer
         tr = PipelineTrainer(tcfg, st)

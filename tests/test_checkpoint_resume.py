@@ -75,12 +75,12 @@ def test_zero1_two_ranks_resume_is_bit_identical(tmp_path):
         assert torch.equal(a[k], b[k]), k
 
 
-def _pp_body(rank, world, tmp, phase):
+def _pp_body(rank, world, tmp, phase, v=1):
     from service_account_auth_improvements_amd.runtime import train_entry
     ev = os.path.join(tmp, f"{phase}.r{rank}.events")
     os.environ["KFAMD_EVENTS_FILE"] = ev
     argv = ["--model", "tiny", "--device", "cpu", "--seq-len", "32", "--micro-batch", "2", "--grad-accum", "2",
-            "--pp", "2"]
+            "--pp", "2"] + (["--pp-virtual", str(v), "--layers", str(2 * v)] if v > 1 else [])
     if phase == "full":
         argv += ["--steps", "4", "--save", os.path.join(tmp, "A")]
     elif phase == "p1":
@@ -92,12 +92,14 @@ def _pp_body(rank, world, tmp, phase):
         return [(r["step"], r["loss"]) for r in map(json.loads, f) if r["event"] == "step"]
 
 
-def test_pipeline_two_stages_resume_is_bit_identical(tmp_path):
-    """pp=2 (1F1B, gloo): the resumed run numbers its steps after the checkpoint and
-    ends bit-identical to the uninterrupted one; the last stage's losses continue exactly."""
-    full = run_ranks(_pp_body, world=2, args=(str(tmp_path), "full"))
-    p1 = run_ranks(_pp_body, world=2, args=(str(tmp_path), "p1"))
-    p2 = run_ranks(_pp_body, world=2, args=(str(tmp_path), "p2"))
+@pytest.mark.parametrize("v", [1, 2], ids=["1f1b", "interleaved-v2"])
+def test_pipeline_two_stages_resume_is_bit_identical(tmp_path, v):
+    """pp=2 (1F1B, and interleaved with 2 chunks per rank; gloo): the resumed run numbers its
+    steps after the checkpoint and ends bit-identical to the uninterrupted one; the
+    last stage's losses continue exactly."""
+    full = run_ranks(_pp_body, world=2, args=(str(tmp_path), "full", v))
+    p1 = run_ranks(_pp_body, world=2, args=(str(tmp_path), "p1", v))
+    p2 = run_ranks(_pp_body, world=2, args=(str(tmp_path), "p2", v))
     for r in range(2):
         assert [s for s, _ in p2[r]] == [2, 3]
         assert p1[r] + p2[r] == full[r]
