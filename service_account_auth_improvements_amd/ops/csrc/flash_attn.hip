@@ -194,6 +194,22 @@ __device__ __forceinline__ float rd_b32(u32 a) {
   asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF) : "memory");
   return r;
 }
+template <int OFF>
+__device__ __forceinline__ f32x4 rd_f4(u32 a) {
+  f32x4 r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF) : "memory");
+  return r;
+}
+// transposed pair from one address: rows at OFF and OFF + 4096 (16 rows of 256 B further)
+template <int OFF>
+__device__ __forceinline__ bf16x8 rd_tr2i(u32 a) {
+  u32x2 x, y;
+  asm volatile("ds_read_b64_tr_b16 %0, %2 offset:%3\n\tds_read_b64_tr_b16 %1, %2 offset:%4"
+               : "=&v"(x), "=v"(y)
+               : "v"(a), "i"(OFF), "i"(OFF + 4096)
+               : "memory");
+  return as_bf16x8(u32x4{x[0], x[1], y[0], y[1]});
+}
 template <int N>
 __device__ __forceinline__ void lgkm_tie1(bf16x8& a) {
   asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(a) : "i"(N) : "memory");
@@ -783,6 +799,11 @@ constexpr int PA = KF_FA_DKDV_PA, PT = KF_FA_DKDV_PT;
 #ifndef KF_FA_DKDV_PRIO
 #define KF_FA_DKDV_PRIO 1
 #endif
+// 1 = v_mfma_f32_16x16x32_bf16 form of the pipelined iteration (see the kernel): 16x16 accumulators,
+// the per-row constants enter as the first MFMA's C operand (no fold MFMAs)
+#ifndef KF_FA_DKDV_M16
+#define KF_FA_DKDV_M16 0
+#endif
 // 1 = S chain, then dP chain with the softmax beside it, then dV with dS beside it (see kernel)
 #ifndef KF_FA_DKDV_SPLIT
 #define KF_FA_DKDV_SPLIT 0
@@ -838,9 +859,19 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
   const bf16_t* vp = qkv + rowB * ld + (long)(Hq + Hkv + hkv) * D;
 
   stage_rows(kp + (long)kv0 * ld, ld, smem + OFF_K, BKVW, w, NWK, l);
+#if KF_FA_DKDV_M16
+  // B operand of dP = dO V^T (16x16x32): V[key 16kb + l%16][d 32ks + 8(l/16) .. +8]
+  bf16x8 v16[2][4];
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+      v16[kb][ks] = as_bf16x8(ld16(vp + (long)(kw0 + 16 * kb + (l & 15)) * ld + 32 * ks + 8 * (l >> 4)));
+#else
   bf16x8 vf[8];  // B operand of dP = dO V^T: V[key][16ks + 8hh .. +8]
 #pragma unroll
   for (int ks = 0; ks < 8; ++ks) vf[ks] = as_bf16x8(ld16(vp + (long)(kw0 + lr) * ld + 16 * ks + 8 * hh));
+#endif
 #if KF_FA_DKDV_PIPE
   const u32 sbase = lds_addr(smem);
   u32 dma_q, dma_do;   // byte offset of this lane's 16-B piece of row 4w + l/16 in a Q / dO panel
@@ -886,9 +917,17 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
     }
   };
 
+#if KF_FA_DKDV_M16
+  f32x4 dK4[8][2], dV4[8][2];   // [16-dim block db][16-key block kb]: dK^T / dV^T 16x16 tiles
+#pragma unroll
+  for (int db = 0; db < 8; ++db)
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) { dK4[db][kb] = f32x4{}; dV4[db][kb] = f32x4{}; }
+#else
   f32x16 dK[4], dV[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) { dK[t] = f32x16{}; dV[t] = f32x16{}; }
+#endif
   const int vrow = 4 * hh + ((l & 15) >> 2);
   const int vcol = 16 * ((l >> 4) & 1) + 4 * (l & 3);
 
@@ -924,6 +963,111 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
       const int row = 16 * ss + vrow + 8 * hf;
       a_tr[ss][hf] = sbase + row * 256 + 16 * ((vcol >> 3) ^ swz_x(row)) + 8 * (l & 1);
     }
+#if KF_FA_DKDV_M16
+  // 16x16x32 form.  Lane l: g = l/16, n = l%16.  S = Q K^T and dP = dO V^T as 2 x 2 tiles of 16
+  // queries x 16 keys (D[4g + r][n]: query 16qb + 4g + r, key 16kb + n); the row constants -lse/scale
+  // and -delta of those 4 queries are ONE f32x4 per qb and enter as the first MFMA's C operand.
+  // dV^T / dK^T as 8 x 2 tiles of 16 dims x 16 keys, fed by dO^T / Q^T fragments whose k-slots
+  // 8g..8g+7 are queries {4g..4g+3, 16+4g..16+4g+3} -- the rows the S/dP accumulators hold.
+  // Addresses: row reads chunk 4ks+g of row n (+16 rows per block: immediate 4096) = a ^ 64ks;
+  // transposed reads of rows 4g+q' and 16+4g+q' (immediate 4096), column block db = a ^ 32db.
+  const int g16 = l >> 4, n16 = l & 15;
+  const u32 a_q16 = sbase + n16 * 256 + 16 * (g16 ^ swz_x(n16));
+  const u32 a_k16 = a_q16 + 8192 * w + OFF_K;
+  const int trow = 4 * g16 + ((l & 15) >> 2), tp4 = l & 3;
+  const u32 a_t16 = sbase + trow * 256 + 16 * ((tp4 >> 1) ^ swz_x(trow)) + 8 * (tp4 & 1);
+  const u32 a_l16 = sbase + OFF_LD + 16 * g16;
+  auto iter = [&](auto curc, int it) {
+    constexpr int CUR = decltype(curc)::value;
+    constexpr int OQ = OFF_Q + CUR * 8192, OD = OFF_DO + CUR * 8192, OL = CUR * 256;
+    const int q0 = qs + nx_qt * QT;   // this iteration's tile (advanced below to the next)
+    adv();
+    if (it + 1 < niter) stage(nx_hq, nx_qt, CUR ^ 1);
+    u32 aq = a_q16, ak = a_k16, at = a_t16, al = a_l16;
+    asm volatile("" : "+v"(aq), "+v"(ak), "+v"(at), "+v"(al));
+    if (!CAUSAL || kw0 <= q0 + QT - 1) {
+      prio(1);
+      f32x4 cl[2], cd[2];
+      cl[0] = rd_f4<OL>(al);
+      cl[1] = rd_f4<OL + 64>(al);
+      cd[0] = rd_f4<OL + 128>(al);
+      cd[1] = rd_f4<OL + 192>(al);
+      // half-step h = 2 ks + qb: reads Q[qb], dO[qb] (+ K[0], K[1] when qb == 0), one half-step ahead
+      bf16x8 fq[2], fd[2], fk[2][2];
+      auto rdA = [&](auto hc) {
+        constexpr int h = decltype(hc)::value, ks = h >> 1, qb = h & 1;
+        if constexpr (qb == 0) {
+          fk[ks & 1][0] = rd_b128<0>(ak ^ (64 * ks));
+          fk[ks & 1][1] = rd_b128<4096>(ak ^ (64 * ks));
+        }
+        fq[qb] = rd_b128<OQ + 4096 * qb>(aq ^ (64 * ks));
+        fd[qb] = rd_b128<OD + 4096 * qb>(aq ^ (64 * ks));
+      };
+      rdA(std::integral_constant<int, 0>());
+      asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(cl[0]), "+v"(cl[1]), "+v"(cd[0]), "+v"(cd[1]) :: "memory");
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { cl[qb][r] *= -inv_scale; cd[qb][r] = -cd[qb][r]; }
+      f32x4 sacc[2][2], dacc[2][2];
+      static_for<0, 8>([&](auto hc) {
+        constexpr int h = decltype(hc)::value, ks = h >> 1, qb = h & 1;
+        constexpr int nxt = h + 1 < 8 ? ((h + 1) & 1 ? 2 : 4) : 0;   // reads of half-step h+1
+        if constexpr (h + 1 < 8) rdA(std::integral_constant<int, h + 1>());
+        if constexpr (qb == 0)
+          asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(fq[0]), "+v"(fd[0]), "+v"(fk[ks & 1][0]), "+v"(fk[ks & 1][1])
+                       : "i"(nxt) : "memory");
+        else
+          asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(fq[1]), "+v"(fd[1]) : "i"(nxt) : "memory");
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+          sacc[qb][kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fq[qb], fk[ks & 1][kb], ks == 0 ? cl[qb] : sacc[qb][kb], 0, 0, 0);
+          dacc[qb][kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fd[qb], v16[kb][ks], ks == 0 ? cd[qb] : dacc[qb][kb], 0, 0, 0);
+        }
+      });
+      // transposed fragment j: j < 8 -> dO^T of dim block j (dV), else Q^T of block j - 8 (dK)
+      bf16x8 ft[PT + 1];
+      auto rdT = [&](auto jc) {
+        constexpr int j = decltype(jc)::value, db = j & 7;
+        ft[j % (PT + 1)] = rd_tr2i<(j < 8 ? OD : OQ)>(at ^ (32 * db));
+      };
+      static_for<0, PT>([&](auto jc) { rdT(jc); });
+      prio(0);
+      // P = exp2(c S'), causal mask: key 16kb + n > query 16qb + 4g + r
+      const int kd = (CAUSAL && (kw0 + 31 > q0)) ? kw0 + n16 - q0 - 4 * g16 : -64;
+      bf16x8 pf[2], sf[2];
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        u32x4 u, v;
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+          for (int r = 0; r < 4; r += 2) {
+            float p0 = __builtin_amdgcn_exp2f(sacc[qb][kb][r] * c), p1 = __builtin_amdgcn_exp2f(sacc[qb][kb][r + 1] * c);
+            p0 = kd + 16 * kb > 16 * qb + r ? 0.f : p0;
+            p1 = kd + 16 * kb > 16 * qb + r + 1 ? 0.f : p1;
+            u[2 * qb + r / 2] = pack2(p0, p1);
+            v[2 * qb + r / 2] = pack2(p0 * dacc[qb][kb][r], p1 * dacc[qb][kb][r + 1]);
+          }
+        pf[kb] = as_bf16x8(u);
+        sf[kb] = as_bf16x8(v);
+      }
+      prio(1);
+      static_for<0, 16>([&](auto jc) {
+        constexpr int j = decltype(jc)::value, db = j & 7, sl = j % (PT + 1);
+        if constexpr (j + PT < 16) rdT(std::integral_constant<int, j + PT>());
+        lgkm_tie1<2 * (j + PT < 16 ? PT : 15 - j)>(ft[sl]);
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+          if constexpr (j < 8) dV4[db][kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ft[sl], pf[kb], dV4[db][kb], 0, 0, 0);
+          else dK4[db][kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ft[sl], sf[kb], dK4[db][kb], 0, 0, 0);
+        }
+      });
+      prio(0);
+    }
+    wait_dma_barrier();
+  };
+#else
   auto iter = [&](auto curc, int it) {
     constexpr int CUR = decltype(curc)::value;
     constexpr int OQ = OFF_Q + CUR * 8192, OD = OFF_DO + CUR * 8192, OL = CUR * 256;
@@ -1078,6 +1222,7 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
 #endif
     wait_dma_barrier();
   };
+#endif
   {
     int it = 0;
     for (; it + 1 < niter; it += 2) {
@@ -1154,10 +1299,26 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
   // ---- chunk partial sums: transpose [d][key] accumulators through LDS, row-contiguous adds,
   // 128 keys (4 waves' accumulators) per pass
   float* T = reinterpret_cast<float*>(smem);   // [128 keys][128 d] fp32 = 64 KB
+#if KF_FA_DKDV_M16
+  auto flush = [&](const f32x4(&acc)[8][2], float mul, float* dst_base) {
+#else
   auto flush = [&](const f32x16(&acc)[4], float mul, float* dst_base) {
+#endif
 #pragma unroll
     for (int pass = 0; pass < NWK / 4; ++pass) {
       if (w / 4 == pass) {
+#if KF_FA_DKDV_M16
+#pragma unroll
+        for (int db = 0; db < 8; ++db)
+#pragma unroll
+          for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int d = 16 * db + 4 * (l >> 4) + r;
+              const int key = 32 * (w & 3) + 16 * kb + (l & 15);
+              T[key * 128 + (d ^ ((key & 31) << 2))] = acc[db][kb][r] * mul;
+            }
+#else
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -1166,6 +1327,7 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
             const int key = 32 * (w & 3) + lr;
             T[key * 128 + (d ^ ((key & 31) << 2))] = acc[t][r] * mul;
           }
+#endif
       }
       __syncthreads();
       float* dst = dst_base + (rowB + kv0 + 128 * pass) * (long)(Hkv * D) + (long)hkv * D;
@@ -1176,8 +1338,13 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
       __syncthreads();
     }
   };
+#if KF_FA_DKDV_M16
+  flush(dK4, scale, dk_acc);
+  flush(dV4, 1.f, dv_acc);
+#else
   flush(dK, scale, dk_acc);
   flush(dV, 1.f, dv_acc);
+#endif
 }
 
 // ---- 64 keys per wave, one wave per SIMD (512-register budget) -------------------------
