@@ -291,11 +291,17 @@ __device__ __forceinline__ u32 lane_id_opaque() {
 #define KF_FA_FWD_FP 3
 #endif
 constexpr int FP = KF_FA_FWD_FP;
+// 1 = ping-pong waves (see the forward kernel); ring 5 deep then
+#ifndef KF_FA_FWD_PINGPONG
+#define KF_FA_FWD_PINGPONG 0
+#endif
+constexpr int NSTF = KF_FA_FWD_PINGPONG ? 5 : NST;
+static_assert(NSTF * STG <= 163840, "LDS");
 template <bool CAUSAL>
 __global__ __launch_bounds__(512, 1) void flash_fwd_kernel(
     const bf16_t* __restrict__ qkv, long ld, bf16_t* __restrict__ out, long ldo,
     float* __restrict__ lse_out, int B, int S, int Hq, int Hkv, float scale_log2) {
-  __shared__ __attribute__((aligned(1024))) char smem[NST * STG];
+  __shared__ __attribute__((aligned(1024))) char smem[NSTF * STG];
   const int nqb = (S + BQ8 - 1) / BQ8, G = Hq / Hkv;
   // logical order [b][hkv][q-block][g]: an XCD's contiguous range shares one K/V panel
   int lid = xcd_remap(blockIdx.x, B * Hq * nqb);
@@ -328,7 +334,7 @@ __global__ __launch_bounds__(512, 1) void flash_fwd_kernel(
   }
   const u32 lds_w = lds_addr(smem) + 1024 * w;
   auto stage = [&](int j) {
-    const u32 st = lds_w + (j % NST) * STG;
+    const u32 st = lds_w + (j % NSTF) * STG;
     const char* kb_ = reinterpret_cast<const char*>(kp + (long)j * BK * ld);
     const char* vb_ = reinterpret_cast<const char*>(vp + (long)j * BK * ld);
     dma_sv(kb_, dma_kv, st);
@@ -338,13 +344,17 @@ __global__ __launch_bounds__(512, 1) void flash_fwd_kernel(
   };
 #else
   auto stage = [&](int j) {
-    char* st = smem + (j % NST) * STG;
+    char* st = smem + (j % NSTF) * STG;
     stage_rows(kp + (long)j * BK * ld, ld, st, BK, w, 8, l);
     stage_rows(vp + (long)j * BK * ld, ld, st + TILE, BK, w, 8, l);
   };
 #endif
   const int ntiles = CAUSAL ? min(S, qb * BQ8 + BQ8) / BK : S / BK;
-  for (int j = 0; j < NST - 1 && j < ntiles; ++j) stage(j);
+#if KF_FA_FWD_PINGPONG
+  for (int j = 0; j < NSTF - 2 && j < ntiles; ++j) stage(j);
+#else
+  for (int j = 0; j < NSTF - 1 && j < ntiles; ++j) stage(j);
+#endif
 
   // retire the Q loads HERE (the compiler's wait counts only them, the DMA stays in flight):
   // a first use inside the loop would make hipcc wait vmcnt(0) on every tile
@@ -361,19 +371,26 @@ __global__ __launch_bounds__(512, 1) void flash_fwd_kernel(
   const int vrow = 4 * hh + ((l & 15) >> 2);
   const int vcol = 16 * ((l >> 4) & 1) + 4 * (l & 3);
 
-  wait_stage(0, min(NST - 2, ntiles - 1));
-  barrier();
-  for (int j = 0; j < ntiles; ++j) {
-    if (j + NST - 1 < ntiles) stage(j + NST - 1);   // refills the buffer of tile j-1
-    const int k0 = j * BK;
-    if (live && (!CAUSAL || k0 <= qmax_w)) {
-      const char* Ks = smem + (j % NST) * STG;
-      const char* Vs = Ks + TILE;
-      f32x16 sc[2];   // S'^T = K (c Q)^T - m: key on the accumulator rows, query on the lane
+#if KF_FA_FWD_PINGPONG
+  // Ping-pong: every wave runs the same S chain -> softmax -> PV sequence per tile, but waves 4-7
+  // (the second wave of every SIMD) take the tile's barrier right after their S chain instead of
+  // after the PV, so they run half a tile behind waves 0-3 and one wave of a SIMD is in its VALU
+  // softmax while the other issues MFMAs (with one barrier position, the barrier lines both
+  // waves up on the same phase).  The lagging waves read tile j's V after barrier j, so the ring
+  // is 5 deep with the DMA three tiles ahead (the slot refilled after barrier j is tile j-1's).
+  constexpr int AH = NSTF - 2;
+  const bool lag = __builtin_amdgcn_readfirstlane(w) >= 4;
+#else
+  constexpr int AH = NSTF - 1;
+#endif
+  // S'^T = K (c Q)^T - m of tile j: key on the accumulator rows, query on the lane
+  auto s_chain = [&](int j, f32x16 (&sc)[2]) {
+    const char* Ks = smem + (j % NSTF) * STG;
+    (void)Ks;
 #if KF_FA_FWD_PIPE
       // K row fragments by inline asm, FP steps ahead; the two 32-key chains alternate
       const u32 ln = lane_id_opaque(), lr_ = ln & 31;
-      const u32 a_t = (lds_addr(smem) + (u32)((j % NST) * STG)) + lr_ * 256 + 16 * ((ln >> 5) ^ swz_x(lr_));
+      const u32 a_t = (lds_addr(smem) + (u32)((j % NSTF) * STG)) + lr_ * 256 + 16 * ((ln >> 5) ^ swz_x(lr_));
       bf16x8 fk[FP + 1];
       auto rdK = [&](auto ic) {
         constexpr int i = decltype(ic)::value, kt = i & 1, ks = i >> 1;
@@ -396,6 +413,11 @@ __global__ __launch_bounds__(512, 1) void flash_fwd_kernel(
         for (int ks = 0; ks < 8; ++ks) sc[kt] = mfma32(row_read(Ks, swz(32 * kt + lr, 2 * ks + hh)), qf[ks], sc[kt]);
       }
 #endif
+  };
+  // causal mask, online softmax, O^T += V^T P^T of tile j
+  auto soft_pv = [&](int j, f32x16 (&sc)[2]) {
+    const int k0 = j * BK;
+    const char* Vs = smem + (j % NSTF) * STG + TILE;
       if (CAUSAL && k0 + BK - 1 > qmin_w) {   // a wave's diagonal tiles only (uniform branch)
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt)
@@ -475,9 +497,30 @@ __global__ __launch_bounds__(512, 1) void flash_fwd_kernel(
 #pragma unroll
           for (int ss = 0; ss < 2; ++ss) o[t] = mfma32(vf[t & 1][2 * kt + ss], pf[kt][ss], o[t]);
       }
+      };
+  auto live_tile = [&](int j) { return live && (!CAUSAL || j * BK <= qmax_w); };
+
+  wait_stage(0, min(AH - 1, ntiles - 1));
+  barrier();
+  f32x16 scp[2];
+  for (int j = 0; j < ntiles; ++j) {
+    if (j + AH < ntiles) stage(j + AH);
+    const bool lv = live_tile(j);
+    if (lv) s_chain(j, scp);
+#if KF_FA_FWD_PINGPONG
+    // the lagging waves take tile j's barrier here, between their S chain and their softmax
+    if (lag && j + 1 < ntiles) {
+      wait_stage(j + 1, min(j + AH, ntiles - 1));
+      barrier();
     }
+#endif
+    if (lv) soft_pv(j, scp);
+#if KF_FA_FWD_PINGPONG
+    if (!lag && j + 1 < ntiles) {
+#else
     if (j + 1 < ntiles) {
-      wait_stage(j + 1, min(j + NST - 1, ntiles - 1));
+#endif
+      wait_stage(j + 1, min(j + AH, ntiles - 1));
       barrier();
     }
   }
