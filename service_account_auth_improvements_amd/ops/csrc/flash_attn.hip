@@ -679,7 +679,10 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dq_kernel(
     if (live && (!CAUSAL || k0 <= qmax_w)) {
       const char* Ks = smem + (j % NST) * STG;
       const char* Vs = Ks + TILE;
-      const bool need_mask = CAUSAL && (k0 + BK - 1 > qmin_w);
+      // non-causal: an opaque false keeps the causal loop's shape (folded away, hipcc spilled)
+      int nm = CAUSAL ? (k0 + BK - 1 > qmin_w) : 0;
+      if (!CAUSAL) asm volatile("" : "+v"(nm));
+      const bool need_mask = __builtin_amdgcn_readfirstlane(nm) != 0;
       bf16x8 sf[2][2];
 #if KF_FA_DQ_PIPE
       // K and V row fragments by inline asm, QP k-steps ahead across both 32-key halves
@@ -1229,7 +1232,11 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
       static_for<0, PT>([&](auto jc) { rdT(jc); });
       prio(0);
       const int key = kw0 + lr;
-      const bool need_mask = CAUSAL && (kw0 + 31 > q0);
+      // non-causal: an opaque false keeps the causal loop's shape (with the masked path folded
+      // away hipcc scheduled the loop differently and spilled 12 VGPRs)
+      int nm = CAUSAL ? (kw0 + 31 > q0) : 0;
+      if (!CAUSAL) asm volatile("" : "+v"(nm));
+      const bool need_mask = __builtin_amdgcn_readfirstlane(nm) != 0;
       if (need_mask) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {

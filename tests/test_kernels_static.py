@@ -1,0 +1,48 @@
+"""Static guard, CPU only: every gfx950 kernel of ops/csrc compiles (device code, the build's own
+flags) with no VGPR/SGPR spill and no scratch (private segment 0).  A spill inside a kernel whose
+LDS reads are inline asm is also a hidden ``s_waitcnt vmcnt(0)`` on every reload -- a wait for
+every LDS-DMA stage in flight -- so a register-pressure regression shows up here first."""
+import concurrent.futures as cf
+import os
+import re
+import shutil
+import subprocess
+import tempfile
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "service_account_auth_improvements_amd", "ops", "csrc")
+HIPCC = "/opt/rocm/bin/hipcc" if os.path.exists("/opt/rocm/bin/hipcc") else shutil.which("hipcc")
+
+
+def _kernels(path):
+    from service_account_auth_improvements_amd.ops import _build
+    flags = ["-O3", "-std=c++17", f"--offload-arch={_build.ARCH}", "-ffp-contract=fast", "-munsafe-fp-atomics",
+             *_build.FILE_FLAGS.get(os.path.basename(path), [])]
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "k.s")
+        subprocess.run([HIPCC, *flags, "--cuda-device-only", "-S", "-o", out, path], check=True,
+                       capture_output=True, text=True)
+        text = open(out).read()
+    res = {}
+    for blk in text.split("  - .agpr_count:")[1:]:
+        name = re.search(r"\.name:\s+(\S+)", blk).group(1)
+        res[name] = {k: int(re.search(rf"\.{k}:\s+(\d+)", blk).group(1))
+                     for k in ("vgpr_spill_count", "sgpr_spill_count", "private_segment_fixed_size")}
+    return res
+
+
+@pytest.mark.skipif(HIPCC is None, reason="needs hipcc")
+def test_every_kernel_is_spill_and_scratch_free():
+    files = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hip"))
+    with cf.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
+        results = dict(zip(files, ex.map(_kernels, files)))
+    bad, n = [], 0
+    for f, ks in results.items():
+        for name, v in ks.items():
+            n += 1
+            if any(v.values()):
+                bad.append((os.path.basename(f), name, v))
+    assert n >= 30, n          # every file contributed its kernels
+    assert not bad, bad
