@@ -291,12 +291,9 @@ __device__ __forceinline__ u32 lane_id_opaque() {
 #define KF_FA_FWD_FP 3
 #endif
 constexpr int FP = KF_FA_FWD_FP;
-// 1 = ping-pong waves (see the forward kernel); ring 5 deep then
-#ifndef KF_FA_FWD_PINGPONG
-#define KF_FA_FWD_PINGPONG 0
-#endif
-constexpr int NSTF = KF_FA_FWD_PINGPONG ? 5 : NST;
-static_assert(NSTF * STG <= 163840, "LDS");
+// (measured and removed: ping-pong wave roles -- waves 4-7 taking each tile's barrier after their
+// S chain, 5-deep ring -- 2.31-2.36 vs 2.23-2.25 ms, profiles/fa_fwd_pingpong_ab.txt)
+constexpr int NSTF = NST;   // forward K+V ring depth
 template <bool CAUSAL>
 __global__ __launch_bounds__(512, 1) void flash_fwd_kernel(
     const bf16_t* __restrict__ qkv, long ld, bf16_t* __restrict__ out, long ldo,
@@ -350,11 +347,7 @@ __global__ __launch_bounds__(512, 1) void flash_fwd_kernel(
   };
 #endif
   const int ntiles = CAUSAL ? min(S, qb * BQ8 + BQ8) / BK : S / BK;
-#if KF_FA_FWD_PINGPONG
-  for (int j = 0; j < NSTF - 2 && j < ntiles; ++j) stage(j);
-#else
   for (int j = 0; j < NSTF - 1 && j < ntiles; ++j) stage(j);
-#endif
 
   // retire the Q loads HERE (the compiler's wait counts only them, the DMA stays in flight):
   // a first use inside the loop would make hipcc wait vmcnt(0) on every tile
@@ -371,18 +364,7 @@ __global__ __launch_bounds__(512, 1) void flash_fwd_kernel(
   const int vrow = 4 * hh + ((l & 15) >> 2);
   const int vcol = 16 * ((l >> 4) & 1) + 4 * (l & 3);
 
-#if KF_FA_FWD_PINGPONG
-  // Ping-pong: every wave runs the same S chain -> softmax -> PV sequence per tile, but waves 4-7
-  // (the second wave of every SIMD) take the tile's barrier right after their S chain instead of
-  // after the PV, so they run half a tile behind waves 0-3 and one wave of a SIMD is in its VALU
-  // softmax while the other issues MFMAs (with one barrier position, the barrier lines both
-  // waves up on the same phase).  The lagging waves read tile j's V after barrier j, so the ring
-  // is 5 deep with the DMA three tiles ahead (the slot refilled after barrier j is tile j-1's).
-  constexpr int AH = NSTF - 2;
-  const bool lag = __builtin_amdgcn_readfirstlane(w) >= 4;
-#else
   constexpr int AH = NSTF - 1;
-#endif
   // S'^T = K (c Q)^T - m of tile j: key on the accumulator rows, query on the lane
   auto s_chain = [&](int j, f32x16 (&sc)[2]) {
     const char* Ks = smem + (j % NSTF) * STG;
@@ -507,19 +489,8 @@ __global__ __launch_bounds__(512, 1) void flash_fwd_kernel(
     if (j + AH < ntiles) stage(j + AH);
     const bool lv = live_tile(j);
     if (lv) s_chain(j, scp);
-#if KF_FA_FWD_PINGPONG
-    // the lagging waves take tile j's barrier here, between their S chain and their softmax
-    if (lag && j + 1 < ntiles) {
-      wait_stage(j + 1, min(j + AH, ntiles - 1));
-      barrier();
-    }
-#endif
     if (lv) soft_pv(j, scp);
-#if KF_FA_FWD_PINGPONG
-    if (!lag && j + 1 < ntiles) {
-#else
     if (j + 1 < ntiles) {
-#endif
       wait_stage(j + 1, min(j + AH, ntiles - 1));
       barrier();
     }
@@ -836,27 +807,18 @@ constexpr int SMEM = OFF_K + BKVW * 256;       // 66048 B (2 WG per CU) / 98816 
 #define KF_FA_DKDV_PT 3
 #endif
 constexpr int PA = KF_FA_DKDV_PA, PT = KF_FA_DKDV_PT;
-// dV/dK fragment order: 0 = column block major (t, then row half ss), 1 = ss major (the first
-// four MFMAs need only the first half of P / dS, so the second half's exp overlaps them)
-#ifndef KF_FA_DKDV_SSMAJOR
-#define KF_FA_DKDV_SSMAJOR 0
-#endif
 // 1 = s_setprio 1 over the MFMA chains, 0 over the softmax VALU and the DMA issue
 #ifndef KF_FA_DKDV_PRIO
 #define KF_FA_DKDV_PRIO 1
 #endif
-// 1 = v_mfma_f32_16x16x32_bf16 form of the pipelined iteration (see the kernel): 16x16 accumulators,
-// the per-row constants enter as the first MFMA's C operand (no fold MFMAs)
-#ifndef KF_FA_DKDV_M16
-#define KF_FA_DKDV_M16 0
-#endif
-// 1 = S chain, then dP chain with the softmax beside it, then dV with dS beside it (see kernel)
-#ifndef KF_FA_DKDV_SPLIT
-#define KF_FA_DKDV_SPLIT 0
-#endif
+// (measured and removed: a split S / dP chain with the softmax beside the dP MFMAs, and a
+// v_mfma_f32_16x16x32_bf16 form with the row constants as the first MFMA's C operand --
+// 4.38 and 4.39-4.44 ms vs 4.10-4.21 ms, profiles/fa_dkdv_split_ab.txt, fa_dkdv_mfma16_ab.txt)
+// transposed fragment j of the dV/dK chain: column block t, row half ss (column block major; the
+// row-half-major order measured 8 % slower, profiles/fa_dkdv_prio_ab.txt)
 template <int J> struct FragJ {
-  static constexpr int t = KF_FA_DKDV_SSMAJOR ? (J & 3) : ((J & 7) >> 1);
-  static constexpr int ss = KF_FA_DKDV_SSMAJOR ? ((J & 7) >> 2) : (J & 1);
+  static constexpr int t = (J & 7) >> 1;
+  static constexpr int ss = J & 1;
 };
 __device__ __forceinline__ void prio(int p) {
   if (KF_FA_DKDV_PRIO) {
@@ -905,19 +867,9 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
   const bf16_t* vp = qkv + rowB * ld + (long)(Hq + Hkv + hkv) * D;
 
   stage_rows(kp + (long)kv0 * ld, ld, smem + OFF_K, BKVW, w, NWK, l);
-#if KF_FA_DKDV_M16
-  // B operand of dP = dO V^T (16x16x32): V[key 16kb + l%16][d 32ks + 8(l/16) .. +8]
-  bf16x8 v16[2][4];
-#pragma unroll
-  for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks)
-      v16[kb][ks] = as_bf16x8(ld16(vp + (long)(kw0 + 16 * kb + (l & 15)) * ld + 32 * ks + 8 * (l >> 4)));
-#else
   bf16x8 vf[8];  // B operand of dP = dO V^T: V[key][16ks + 8hh .. +8]
 #pragma unroll
   for (int ks = 0; ks < 8; ++ks) vf[ks] = as_bf16x8(ld16(vp + (long)(kw0 + lr) * ld + 16 * ks + 8 * hh));
-#endif
 #if KF_FA_DKDV_PIPE
   const u32 sbase = lds_addr(smem);
   u32 dma_q, dma_do;   // byte offset of this lane's 16-B piece of row 4w + l/16 in a Q / dO panel
@@ -963,17 +915,9 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
     }
   };
 
-#if KF_FA_DKDV_M16
-  f32x4 dK4[8][2], dV4[8][2];   // [16-dim block db][16-key block kb]: dK^T / dV^T 16x16 tiles
-#pragma unroll
-  for (int db = 0; db < 8; ++db)
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) { dK4[db][kb] = f32x4{}; dV4[db][kb] = f32x4{}; }
-#else
   f32x16 dK[4], dV[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) { dK[t] = f32x16{}; dV[t] = f32x16{}; }
-#endif
   const int vrow = 4 * hh + ((l & 15) >> 2);
   const int vcol = 16 * ((l >> 4) & 1) + 4 * (l & 3);
 
@@ -1009,111 +953,6 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
       const int row = 16 * ss + vrow + 8 * hf;
       a_tr[ss][hf] = sbase + row * 256 + 16 * ((vcol >> 3) ^ swz_x(row)) + 8 * (l & 1);
     }
-#if KF_FA_DKDV_M16
-  // 16x16x32 form.  Lane l: g = l/16, n = l%16.  S = Q K^T and dP = dO V^T as 2 x 2 tiles of 16
-  // queries x 16 keys (D[4g + r][n]: query 16qb + 4g + r, key 16kb + n); the row constants -lse/scale
-  // and -delta of those 4 queries are ONE f32x4 per qb and enter as the first MFMA's C operand.
-  // dV^T / dK^T as 8 x 2 tiles of 16 dims x 16 keys, fed by dO^T / Q^T fragments whose k-slots
-  // 8g..8g+7 are queries {4g..4g+3, 16+4g..16+4g+3} -- the rows the S/dP accumulators hold.
-  // Addresses: row reads chunk 4ks+g of row n (+16 rows per block: immediate 4096) = a ^ 64ks;
-  // transposed reads of rows 4g+q' and 16+4g+q' (immediate 4096), column block db = a ^ 32db.
-  const int g16 = l >> 4, n16 = l & 15;
-  const u32 a_q16 = sbase + n16 * 256 + 16 * (g16 ^ swz_x(n16));
-  const u32 a_k16 = a_q16 + 8192 * w + OFF_K;
-  const int trow = 4 * g16 + ((l & 15) >> 2), tp4 = l & 3;
-  const u32 a_t16 = sbase + trow * 256 + 16 * ((tp4 >> 1) ^ swz_x(trow)) + 8 * (tp4 & 1);
-  const u32 a_l16 = sbase + OFF_LD + 16 * g16;
-  auto iter = [&](auto curc, int it) {
-    constexpr int CUR = decltype(curc)::value;
-    constexpr int OQ = OFF_Q + CUR * 8192, OD = OFF_DO + CUR * 8192, OL = CUR * 256;
-    const int q0 = qs + nx_qt * QT;   // this iteration's tile (advanced below to the next)
-    adv();
-    if (it + 1 < niter) stage(nx_hq, nx_qt, CUR ^ 1);
-    u32 aq = a_q16, ak = a_k16, at = a_t16, al = a_l16;
-    asm volatile("" : "+v"(aq), "+v"(ak), "+v"(at), "+v"(al));
-    if (!CAUSAL || kw0 <= q0 + QT - 1) {
-      prio(1);
-      f32x4 cl[2], cd[2];
-      cl[0] = rd_f4<OL>(al);
-      cl[1] = rd_f4<OL + 64>(al);
-      cd[0] = rd_f4<OL + 128>(al);
-      cd[1] = rd_f4<OL + 192>(al);
-      // half-step h = 2 ks + qb: reads Q[qb], dO[qb] (+ K[0], K[1] when qb == 0), one half-step ahead
-      bf16x8 fq[2], fd[2], fk[2][2];
-      auto rdA = [&](auto hc) {
-        constexpr int h = decltype(hc)::value, ks = h >> 1, qb = h & 1;
-        if constexpr (qb == 0) {
-          fk[ks & 1][0] = rd_b128<0>(ak ^ (64 * ks));
-          fk[ks & 1][1] = rd_b128<4096>(ak ^ (64 * ks));
-        }
-        fq[qb] = rd_b128<OQ + 4096 * qb>(aq ^ (64 * ks));
-        fd[qb] = rd_b128<OD + 4096 * qb>(aq ^ (64 * ks));
-      };
-      rdA(std::integral_constant<int, 0>());
-      asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(cl[0]), "+v"(cl[1]), "+v"(cd[0]), "+v"(cd[1]) :: "memory");
-#pragma unroll
-      for (int qb = 0; qb < 2; ++qb)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) { cl[qb][r] *= -inv_scale; cd[qb][r] = -cd[qb][r]; }
-      f32x4 sacc[2][2], dacc[2][2];
-      static_for<0, 8>([&](auto hc) {
-        constexpr int h = decltype(hc)::value, ks = h >> 1, qb = h & 1;
-        constexpr int nxt = h + 1 < 8 ? ((h + 1) & 1 ? 2 : 4) : 0;   // reads of half-step h+1
-        if constexpr (h + 1 < 8) rdA(std::integral_constant<int, h + 1>());
-        if constexpr (qb == 0)
-          asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(fq[0]), "+v"(fd[0]), "+v"(fk[ks & 1][0]), "+v"(fk[ks & 1][1])
-                       : "i"(nxt) : "memory");
-        else
-          asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(fq[1]), "+v"(fd[1]) : "i"(nxt) : "memory");
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb) {
-          sacc[qb][kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fq[qb], fk[ks & 1][kb], ks == 0 ? cl[qb] : sacc[qb][kb], 0, 0, 0);
-          dacc[qb][kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fd[qb], v16[kb][ks], ks == 0 ? cd[qb] : dacc[qb][kb], 0, 0, 0);
-        }
-      });
-      // transposed fragment j: j < 8 -> dO^T of dim block j (dV), else Q^T of block j - 8 (dK)
-      bf16x8 ft[PT + 1];
-      auto rdT = [&](auto jc) {
-        constexpr int j = decltype(jc)::value, db = j & 7;
-        ft[j % (PT + 1)] = rd_tr2i<(j < 8 ? OD : OQ)>(at ^ (32 * db));
-      };
-      static_for<0, PT>([&](auto jc) { rdT(jc); });
-      prio(0);
-      // P = exp2(c S'), causal mask: key 16kb + n > query 16qb + 4g + r
-      const int kd = (CAUSAL && (kw0 + 31 > q0)) ? kw0 + n16 - q0 - 4 * g16 : -64;
-      bf16x8 pf[2], sf[2];
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb) {
-        u32x4 u, v;
-#pragma unroll
-        for (int qb = 0; qb < 2; ++qb)
-#pragma unroll
-          for (int r = 0; r < 4; r += 2) {
-            float p0 = __builtin_amdgcn_exp2f(sacc[qb][kb][r] * c), p1 = __builtin_amdgcn_exp2f(sacc[qb][kb][r + 1] * c);
-            p0 = kd + 16 * kb > 16 * qb + r ? 0.f : p0;
-            p1 = kd + 16 * kb > 16 * qb + r + 1 ? 0.f : p1;
-            u[2 * qb + r / 2] = pack2(p0, p1);
-            v[2 * qb + r / 2] = pack2(p0 * dacc[qb][kb][r], p1 * dacc[qb][kb][r + 1]);
-          }
-        pf[kb] = as_bf16x8(u);
-        sf[kb] = as_bf16x8(v);
-      }
-      prio(1);
-      static_for<0, 16>([&](auto jc) {
-        constexpr int j = decltype(jc)::value, db = j & 7, sl = j % (PT + 1);
-        if constexpr (j + PT < 16) rdT(std::integral_constant<int, j + PT>());
-        lgkm_tie1<2 * (j + PT < 16 ? PT : 15 - j)>(ft[sl]);
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb) {
-          if constexpr (j < 8) dV4[db][kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ft[sl], pf[kb], dV4[db][kb], 0, 0, 0);
-          else dK4[db][kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ft[sl], sf[kb], dK4[db][kb], 0, 0, 0);
-        }
-      });
-      prio(0);
-    }
-    wait_dma_barrier();
-  };
-#else
   auto iter = [&](auto curc, int it) {
     constexpr int CUR = decltype(curc)::value;
     constexpr int OQ = OFF_Q + CUR * 8192, OD = OFF_DO + CUR * 8192, OL = CUR * 256;
@@ -1125,81 +964,6 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
     u32 a_row = a_row0, a_k = a_k0, a_t00 = a_tr[0][0], a_t01 = a_tr[0][1], a_t10 = a_tr[1][0], a_t11 = a_tr[1][1];
     asm volatile("" : "+v"(a_row), "+v"(a_k), "+v"(a_t00), "+v"(a_t01), "+v"(a_t10), "+v"(a_t11));
     const u32 a_t[2][2] = {{a_t00, a_t01}, {a_t10, a_t11}};
-#if KF_FA_DKDV_SPLIT
-    if (!CAUSAL || kw0 <= q0 + QT - 1) {
-      // S chain, then the dP chain with the softmax of S interleaved, then the dV chain with
-      // dS = P * dP' interleaved, then the dK chain: every VALU phase has MFMAs beside it.
-      // Phase-A read steps: i < 8 -> Q_i, K_i; i >= 8 -> dO_(i-8); PA steps ahead.
-      prio(1);
-      float lse_v = rd_b32<OL>(a_ls), dl_v = rd_b32<OL + 128>(a_ls);
-      bf16x8 fq[PA + 1], fk[PA + 1], fd[PA + 1];
-      auto rdA = [&](auto ic) {
-        constexpr int i = decltype(ic)::value;
-        if constexpr (i < 8) {
-          fq[i % (PA + 1)] = rd_b128<OQ>(a_row ^ (32 * i));
-          fk[i % (PA + 1)] = rd_b128<0>(a_k ^ (32 * i));
-        } else {
-          fd[(i - 8) % (PA + 1)] = rd_b128<OD>(a_row ^ (32 * (i - 8)));
-        }
-      };
-      static_for<0, PA>([&](auto ic) { rdA(ic); });
-      lgkm_tie_f2<2 * PA>(lse_v, dl_v);
-      f32x16 s = mfma32(fold_const(lse_v * inv_scale, hh), ones, f32x16{});
-      f32x16 dp = mfma32(fold_const(dl_v, hh), ones, f32x16{});
-      // causal mask as a branch-free compare: element r is dropped when key - (q0 + 4hh) > row(r)
-      const int key = kw0 + lr;
-      const int kd = (CAUSAL && (kw0 + 31 > q0)) ? key - (q0 + 4 * hh) : -64;
-      bf16x8 pf[2], sf[2];
-      u32 pu[8];
-      static_for<0, 16>([&](auto ic) {
-        constexpr int i = decltype(ic)::value;
-        constexpr int cum_i = i < 8 ? 2 * (i + 1) : 16 + (i - 7);   // reads in steps 0..i
-        constexpr int last = (i + PA < 16 ? i + PA : 15);
-        constexpr int cum_l = last < 8 ? 2 * (last + 1) : 16 + (last - 7);
-        if constexpr (i + PA < 16) rdA(std::integral_constant<int, i + PA>());
-        if constexpr (i < 8) {
-          asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(fq[i % (PA + 1)]), "+v"(fk[i % (PA + 1)]) : "i"(cum_l - cum_i) : "memory");
-          s = mfma32(fq[i % (PA + 1)], fk[i % (PA + 1)], s);
-        } else {
-          constexpr int ks = i - 8;
-          lgkm_tie1<cum_l - cum_i>(fd[ks % (PA + 1)]);
-          dp = mfma32(fd[ks % (PA + 1)], vf[ks], dp);
-          // softmax of S rows 2ks, 2ks+1 beside the dP MFMAs
-          constexpr int r0 = 2 * ks, r1 = 2 * ks + 1;
-          constexpr int row0 = (r0 & 3) + 8 * (r0 >> 2), row1 = (r1 & 3) + 8 * (r1 >> 2);
-          const float p0 = __builtin_amdgcn_exp2f(s[r0] * c), p1 = __builtin_amdgcn_exp2f(s[r1] * c);
-          s[r0] = kd > row0 ? 0.f : p0;
-          s[r1] = kd > row1 ? 0.f : p1;
-          pu[ks] = pack2(s[r0], s[r1]);
-        }
-      });
-      pf[0] = as_bf16x8(u32x4{pu[0], pu[1], pu[2], pu[3]});
-      pf[1] = as_bf16x8(u32x4{pu[4], pu[5], pu[6], pu[7]});
-      bf16x8 ft[PT + 1];
-      auto rdT = [&](auto jc) {
-        constexpr int j = decltype(jc)::value, t = FragJ<j>::t, ss = FragJ<j>::ss;
-        ft[j % (PT + 1)] = rd_tr2<(j < 8 ? OD : OQ)>(a_t[ss][0] ^ (64 * t), a_t[ss][1] ^ (64 * t));
-      };
-      static_for<0, PT>([&](auto jc) { rdT(jc); });
-      static_for<0, 16>([&](auto jc) {
-        constexpr int j = decltype(jc)::value, t = FragJ<j>::t, ss = FragJ<j>::ss, sl = j % (PT + 1);
-        if constexpr (j + PT < 16) rdT(std::integral_constant<int, j + PT>());
-        lgkm_tie1<2 * (j + PT < 16 ? PT : 15 - j)>(ft[sl]);
-        if constexpr (j < 8) {
-          dV[t] = mfma32(ft[sl], pf[ss], dV[t]);
-          // dS rows 2j, 2j+1 beside the dV MFMAs
-          pu[j] = pack2(s[2 * j] * dp[2 * j], s[2 * j + 1] * dp[2 * j + 1]);
-          if constexpr (j == 7) {
-            sf[0] = as_bf16x8(u32x4{pu[0], pu[1], pu[2], pu[3]});
-            sf[1] = as_bf16x8(u32x4{pu[4], pu[5], pu[6], pu[7]});
-          }
-        } else {
-          dK[t] = mfma32(ft[sl], sf[ss], dK[t]);
-        }
-      });
-      prio(0);
-    }
-#else
     if (!CAUSAL || kw0 <= q0 + QT - 1) {
       prio(1);
       float lse_v = rd_b32<OL>(a_ls), dl_v = rd_b32<OL + 128>(a_ls);
@@ -1269,10 +1033,8 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
       });
       prio(0);
     }
-#endif
     wait_dma_barrier();
   };
-#endif
   {
     int it = 0;
     for (; it + 1 < niter; it += 2) {
@@ -1349,26 +1111,10 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
   // ---- chunk partial sums: transpose [d][key] accumulators through LDS, row-contiguous adds,
   // 128 keys (4 waves' accumulators) per pass
   float* T = reinterpret_cast<float*>(smem);   // [128 keys][128 d] fp32 = 64 KB
-#if KF_FA_DKDV_M16
-  auto flush = [&](const f32x4(&acc)[8][2], float mul, float* dst_base) {
-#else
   auto flush = [&](const f32x16(&acc)[4], float mul, float* dst_base) {
-#endif
 #pragma unroll
     for (int pass = 0; pass < NWK / 4; ++pass) {
       if (w / 4 == pass) {
-#if KF_FA_DKDV_M16
-#pragma unroll
-        for (int db = 0; db < 8; ++db)
-#pragma unroll
-          for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int d = 16 * db + 4 * (l >> 4) + r;
-              const int key = 32 * (w & 3) + 16 * kb + (l & 15);
-              T[key * 128 + (d ^ ((key & 31) << 2))] = acc[db][kb][r] * mul;
-            }
-#else
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -1377,7 +1123,6 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
             const int key = 32 * (w & 3) + lr;
             T[key * 128 + (d ^ ((key & 31) << 2))] = acc[t][r] * mul;
           }
-#endif
       }
       __syncthreads();
       float* dst = dst_base + (rowB + kv0 + 128 * pass) * (long)(Hkv * D) + (long)hkv * D;
@@ -1388,13 +1133,8 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
       __syncthreads();
     }
   };
-#if KF_FA_DKDV_M16
-  flush(dK4, scale, dk_acc);
-  flush(dV4, 1.f, dv_acc);
-#else
   flush(dK, scale, dk_acc);
   flush(dV, 1.f, dv_acc);
-#endif
 }
 
 // ---- 64 keys per wave, one wave per SIMD (512-register budget) -------------------------
