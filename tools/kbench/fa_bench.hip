@@ -127,6 +127,27 @@ int main(int argc, char** argv) {
   post();
   CK(hipDeviceSynchronize());
   printf("bwd_total %8.1f us  %6.0f TF(5-product)\n", bwd * 1e3, 5 * mm / (bwd * 1e-3) / 1e12);
+#if KF_FA_STAMPS
+  {  // dK/dV phase shares from the diagnostic stamps of the last dK/dV launch (see flash_attn.hip)
+    static unsigned long long st[1 << 16][8];
+    CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(kf_fa_stamps), sizeof(st)));
+    const char* names[5] = {"dma issue", "S/dP chain", "softmax", "dV/dK chain", "barrier"};
+    double sum[5] = {0, 0, 0, 0, 0}, tot = 0, its = 0, pro = 0, fl = 0, nw = 0;
+    const int waves = std::min(g_kv * fb::NWK, 1 << 16);
+    for (int i = 0; i < waves; ++i) {
+      if (!st[i][5]) continue;
+      its += (double)st[i][5];
+      nw += 1;
+      pro += (double)st[i][6];
+      fl += (double)st[i][7];
+      for (int k = 0; k < 5; ++k) { sum[k] += (double)st[i][k]; tot += (double)st[i][k]; }
+    }
+    printf("dkdv phases (s_memtime, all waves, %.0f iterations):", its);
+    for (int k = 0; k < 5; ++k) printf("  %s %.1f%% (%.0f cyc/it)", names[k], 100 * sum[k] / tot, sum[k] / its);
+    printf("\ndkdv per work item (wave mean): prologue %.0f cyc, loop %.0f cyc, flush %.0f cyc (%.1f / %.1f %% of the wave's time)\n",
+           pro / nw, tot / nw, fl / nw, 100 * pro / (pro + tot + fl), 100 * fl / (pro + tot + fl));
+  }
+#endif
 
   // ---- float64 reference on sampled rows
   auto hq = fetch<uint16_t>(qkv, (size_t)T * ldq), hdo = fetch<uint16_t>(dout, (size_t)T * ldo);
