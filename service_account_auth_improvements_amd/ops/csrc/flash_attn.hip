@@ -52,7 +52,10 @@ constexpr int BK = 64;            // keys per tile (forward / dQ)
 constexpr int TILE = BK * D * 2;  // 16 KB
 constexpr int BKV = 128;          // keys per dK/dV workgroup (4 waves x 32)
 constexpr int QT = 32;            // query rows per dK/dV iteration
-constexpr int QCH = 1024;         // query rows per dK/dV work item (512 / 2048: 6 % / 4 % slower)
+#ifndef KF_FA_QCH
+#define KF_FA_QCH 1024
+#endif
+constexpr int QCH = KF_FA_QCH;    // query rows per dK/dV work item (512 / 2048: 6 % / 4 % slower)
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float LN2 = 0.6931471805599453f;
 
@@ -833,6 +836,24 @@ __host__ __device__ inline int n_chunks(int kb, int S, bool causal) {
 }
 }  // namespace fb
 
+// Diagnostic build only (-DKF_FA_STAMPS=1, tools/kbench): per-wave sums of s_memtime deltas between
+// the iteration's phase boundaries (0 start, 1 after the next tile's DMA issue, 2 after the S/dP
+// chain, 3 after the softmax, 4 after the dV/dK chain, 5 after the barrier), written once per wave
+// by vector stores to kf_fa_stamps; the real kernel compiles no stamp.
+#ifndef KF_FA_STAMPS
+#define KF_FA_STAMPS 0
+#endif
+#if KF_FA_STAMPS
+__device__ unsigned long long kf_fa_stamps[1 << 16][8];
+#define KF_STAMP(i)                                                          \
+  do {                                                                       \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime();           \
+    if ((i) > 0) st_acc[(i) - 1] += now_ - st_prev;                          \
+    st_prev = now_;                                                          \
+  } while (0)
+#else
+#define KF_STAMP(i) ((void)0)
+#endif
 template <bool CAUSAL>
 __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kernel(
     const bf16_t* __restrict__ qkv, long ld, const bf16_t* __restrict__ dout, long lddo,
@@ -840,6 +861,9 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
     float* __restrict__ dv_acc, int B, int S, int Hq, int Hkv, float scale, int items_per_head) {
   using namespace fb;
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+#if KF_FA_STAMPS
+  const unsigned long long st_k0 = __builtin_amdgcn_s_memtime();
+#endif
   const int G = Hq / Hkv;
   const int lid = xcd_remap(blockIdx.x, B * Hkv * items_per_head);
   int item = lid % items_per_head;
@@ -953,12 +977,18 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
       const int row = 16 * ss + vrow + 8 * hf;
       a_tr[ss][hf] = sbase + row * 256 + 16 * ((vcol >> 3) ^ swz_x(row)) + 8 * (l & 1);
     }
+#if KF_FA_STAMPS
+  unsigned long long st_acc[5] = {0, 0, 0, 0, 0}, st_prev = 0;
+  const unsigned long long st_loop0 = __builtin_amdgcn_s_memtime();
+#endif
   auto iter = [&](auto curc, int it) {
     constexpr int CUR = decltype(curc)::value;
     constexpr int OQ = OFF_Q + CUR * 8192, OD = OFF_DO + CUR * 8192, OL = CUR * 256;
     const int q0 = qs + nx_qt * QT;   // this iteration's tile (advanced below to the next)
+    KF_STAMP(0);
     adv();
     if (it + 1 < niter) stage(nx_hq, nx_qt, CUR ^ 1);
+    KF_STAMP(1);
     // opaque per iteration: keeps the 32 XOR-ed per-read addresses from being hoisted out of
     // the loop as invariants (they would pin ~30 VGPRs and spill)
     u32 a_row = a_row0, a_k = a_k0, a_t00 = a_tr[0][0], a_t01 = a_tr[0][1], a_t10 = a_tr[1][0], a_t11 = a_tr[1][1];
@@ -994,6 +1024,7 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
         ft[j % (PT + 1)] = rd_tr2<(j < 8 ? OD : OQ)>(a_t[ss][0] ^ (64 * t), a_t[ss][1] ^ (64 * t));
       };
       static_for<0, PT>([&](auto jc) { rdT(jc); });
+      KF_STAMP(2);
       prio(0);
       const int key = kw0 + lr;
       // non-causal: an opaque false keeps the causal loop's shape (with the masked path folded
@@ -1023,6 +1054,7 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
         pf[ss] = as_bf16x8(u);
         sf[ss] = as_bf16x8(v);
       }
+      KF_STAMP(3);
       prio(1);
       static_for<0, 16>([&](auto jc) {
         constexpr int j = decltype(jc)::value, t = FragJ<j>::t, ss = FragJ<j>::ss, sl = j % (PT + 1);
@@ -1032,8 +1064,10 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
         else dK[t] = mfma32(ft[sl], sf[ss], dK[t]);
       });
       prio(0);
+      KF_STAMP(4);
     }
     wait_dma_barrier();
+    KF_STAMP(5);
   };
   {
     int it = 0;
@@ -1043,6 +1077,9 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
     }
     if (it < niter) iter(std::integral_constant<int, 0>(), it);
   }
+#if KF_FA_STAMPS
+  const unsigned long long st_loop1 = __builtin_amdgcn_s_memtime();
+#endif
 #else
   for (int it = 0; it < niter; ++it) {
     const int cur = it & 1;
@@ -1135,6 +1172,19 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
   };
   flush(dK, scale, dk_acc);
   flush(dV, 1.f, dv_acc);
+#if KF_FA_STAMPS
+  {
+    const unsigned long long st_end = __builtin_amdgcn_s_memtime();
+    const int slot = (blockIdx.x * NWK + w) & ((1 << 16) - 1);
+    // one lane per value (vector stores): 0-4 loop phases, 5 iterations, 6 prologue, 7 flush
+    unsigned long long v = 0;
+    for (int k = 0; k < 5; ++k) v = l == k ? st_acc[k] : v;
+    v = l == 5 ? (unsigned long long)niter : v;
+    v = l == 6 ? st_loop0 - st_k0 : v;
+    v = l == 7 ? st_end - st_loop1 : v;
+    if (l < 8) kf_fa_stamps[slot][l] = v;
+  }
+#endif
 }
 
 // ---- 64 keys per wave, one wave per SIMD (512-register budget) -------------------------
