@@ -79,6 +79,36 @@ def test_swiglu(rows, F):
     assert _rel(ops.swiglu_bwd(gu, d), reference.swiglu_bwd(gu, d)) < 1e-2
 
 
+_SWIGLU_CHILD = """
+import torch
+from service_account_auth_improvements_amd import ops
+from service_account_auth_improvements_amd.ops import _ext, reference
+assert _ext.load()
+torch.manual_seed(2)
+for rows, F in ((17, 14336), (256, 512), (3, 8)):
+    gu = torch.randn(rows, 2 * F, device="cuda:0", dtype=torch.bfloat16) * 3
+    d = torch.randn(rows, F, device="cuda:0", dtype=torch.bfloat16)
+    for got, want in ((ops.swiglu_fwd(gu), reference.swiglu_fwd(gu)),
+                      (ops.swiglu_bwd(gu, d), reference.swiglu_bwd(gu, d))):
+        a, b = got.float(), want.float()
+        assert ((a - b).abs().max() / b.abs().max().clamp_min(1e-6)).item() < 1e-2, (rows, F)
+print("swiglu grid-stride ok")
+"""
+
+
+def test_swiglu_grid_stride_forced():
+    """KFAMD_SWIGLU_2D=0 (read once per process) routes small row counts to the grid-stride kernels."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, KFAMD_SWIGLU_2D="0", PYTHONPATH=root)
+    out = subprocess.run([sys.executable, "-c", _SWIGLU_CHILD], env=env, capture_output=True, text=True,
+                         timeout=110)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert "swiglu grid-stride ok" in out.stdout
+
+
 @pytest.mark.parametrize("T,V", [(16, 128256), (64, 1024), (5, 16032)])
 def test_cross_entropy_fused(T, V):
     torch.manual_seed(3)
