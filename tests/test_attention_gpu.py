@@ -44,14 +44,11 @@ def test_flash_fwd_spiky_scores():
     assert torch.allclose(lse, lse_ref, atol=2e-2, rtol=1e-3)
 
 
-@pytest.mark.parametrize("dkdv", ["32", "64"])
 @pytest.mark.parametrize("B,S,Hq,Hkv,causal", [
     (1, 256, 2, 1, True), (2, 512, 8, 2, True), (1, 1024, 32, 8, True),
     (1, 512, 4, 4, False), (1, 768, 8, 1, True)])
-def test_flash_bwd(B, S, Hq, Hkv, causal, dkdv, monkeypatch):
-    """Both dK/dV kernels (32 keys per wave, the default, and 64 keys per wave, which needs
-    S % 256 == 0 and otherwise falls back to the 32-key kernel) against fp32 autograd."""
-    monkeypatch.setenv("KFAMD_FA_DKDV", dkdv)
+def test_flash_bwd(B, S, Hq, Hkv, causal):
+    """dQ and dK/dV kernels against fp32 autograd."""
     qkv = _qkv(B, S, Hq, Hkv, seed=S + 3 * Hq)
     sc = 1 / math.sqrt(128)
     o, lse = torch.ops.kfamd.flash_fwd(qkv, B, S, Hq, Hkv, 128, sc, causal)
@@ -96,14 +93,13 @@ def test_flash_bwd_stream_fork_ordering():
         assert err < 1e-2, err
 
 
-@pytest.mark.parametrize("b,g,dkdv", [(0, 0, "32"), (1, 5, "64")])
-def test_flash_fwd_bwd_at_bench_shape(b, g, dkdv, monkeypatch):
-    """The bench's exact launch: B=2, S=8192, Hq=32, Hkv=8, causal (64 heavy-first q-blocks, the
-    XCD remap and the dK/dV work-item split as in the training step), checked on one (batch,
-    kv-head) GQA group -- its 4 query heads' O / lse / dQ and the group's dK / dV -- against an
-    fp32 autograd reference of that slice; once per dK/dV kernel."""
-    monkeypatch.setenv("KFAMD_FA_DKDV", dkdv)
-    B, S, Hq, Hkv, D = 2, 8192, 32, 8, 128
+@pytest.mark.parametrize("B,b,g", [(2, 0, 0), (2, 1, 5), (4, 3, 7), (4, 1, 2)])
+def test_flash_fwd_bwd_at_bench_shape(B, b, g):
+    """The bench's exact launch: micro-batch B = 4 (bench.py's default on a 288 GB MI355X; B = 2
+    too), S=8192, Hq=32, Hkv=8, causal -- the grid size, the XCD remap and the dK/dV work-item
+    split all change with B -- checked on one (batch, kv-head) GQA group: its 4 query heads'
+    O / lse / dQ and the group's dK / dV against an fp32 autograd reference of that slice."""
+    S, Hq, Hkv, D = 8192, 32, 8, 128
     G = Hq // Hkv
     sc = 1 / math.sqrt(D)
     qkv = _qkv(B, S, Hq, Hkv, seed=99)
@@ -136,14 +132,12 @@ def test_flash_fwd_bwd_at_bench_shape(b, g, dkdv, monkeypatch):
     assert rel(dqkv[rows, (Hq + Hkv + g) * D:(Hq + Hkv + g + 1) * D].float(), dv_r) < 3e-2
 
 
-@pytest.mark.parametrize("dkdv", ["32", "64"])
-def test_flash_long_context_32k(dkdv, monkeypatch):
+def test_flash_long_context_32k():
     """Long context: S = 32768, causal GQA 8/2, B = 1.  The forward's O / lse and
     the backward's dQ are checked on the LAST 256 query rows of one head (they attend to every
     key), dK / dV on the first 256 keys of one kv-head (every query attends to them), against
     fp32 references over the full key / query range of that slice."""
     assert _ext.load()
-    monkeypatch.setenv("KFAMD_FA_DKDV", dkdv)
     B, S, Hq, Hkv, D = 1, 32768, 8, 2, 128
     G = Hq // Hkv
     sc = 1 / math.sqrt(D)

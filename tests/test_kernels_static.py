@@ -46,3 +46,17 @@ def test_every_kernel_is_spill_and_scratch_free():
                 bad.append((os.path.basename(f), name, v))
     assert n >= 30, n          # every file contributed its kernels
     assert not bad, bad
+
+
+def test_shipped_kernels_carry_no_experiment_knobs():
+    """Kernel-source hygiene: the shipped flash-attention source has no preprocessor knobs or
+    diagnostic stamp code (measured-and-rejected variants live in tools/kbench/flash_attn_lab.hip),
+    and no shipped kernel reads the shader clock."""
+    branch = re.compile(r"^\s*#\s*(if|ifdef|ifndef|elif)\b")
+    with open(os.path.join(CSRC, "flash_attn.hip")) as f:
+        n = sum(1 for line in f if branch.match(line))
+    assert n <= 6, n
+    for f in os.listdir(CSRC):
+        if f.endswith(".hip"):
+            with open(os.path.join(CSRC, f)) as fh:
+                assert "s_memtime" not in fh.read(), f

@@ -1,14 +1,71 @@
 #!/bin/bash
-# One GPU session: gpu tests -> 1-GPU bench -> rocprofv3 kernel stats + summary.
-# Every GPU step has its own time limit; the first failure ends the script.
+# One parameterised GPU session (the only gpurun script; recipes in tools/RECIPES.md):
+#
+#   tools/gpu_session.sh OUTDIR STEP [STEP ...]
+#
+# Steps run in order, each under its own time limit; the first failure (non-zero status, a
+# time limit, an abort or a fault) ends the session, so nothing more touches the GPU after it.
+#   tests[:K_EXPR]          pytest -m gpu (optionally -k K_EXPR)              -> OUTDIR/pytest.log
+#   smoke                   __graft_entry__.smoke()                             -> OUTDIR/smoke.log
+#   bench[:STEPS[:WARMUP]]  python bench.py (+ $BENCH_ARGS)                     -> OUTDIR/bench*.log
+#   prof[:STEPS]            rocprofv3 --kernel-trace --stats of bench.py, per-category summary
+#                                                                               -> OUTDIR/prof/summary.md
+#   kbench:BIN[:A,B,..]     tools/kbench/bin/BIN A B ..                         -> OUTDIR/kbench.txt
+#   pmc:BIN[:A,B,..]        two PMC passes over a kbench binary (tools/kbench/pmc.sh)
+#   tool:SCRIPT[:A,B,..]    python -u tools/SCRIPT A B ..                       -> OUTDIR/SCRIPT.log
+# Counter runs never combine --pmc with trace domains; nothing here sets GPU_MAX_HW_QUEUES.
 set -o pipefail
-export TMPDIR=/tmp
-mkdir -p gpurun_out
-timeout -k 10 420 python -m pytest tests -x -q -m gpu > gpurun_out/pytest_gpu.log 2>&1
-rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 420 python bench.py --steps 8 --warmup 3 > gpurun_out/bench.log 2>&1
-rc=$?; echo "bench rc=$rc"; tail -2 gpurun_out/bench.log; [ $rc -eq 0 ] || exit $rc
-PROF_OUT=gpurun_out/prof_full bash tools/gpu_prof.sh --steps 3 --warmup 2 || exit 1
-f=$(find gpurun_out/prof_full -name "*kernel_stats.csv" | head -1)
-python tools/prof_summary.py "$f" 5 > gpurun_out/prof_full/summary.md
-head -20 gpurun_out/prof_full/summary.md
+export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
+O=${1:?usage: gpu_session.sh OUTDIR STEP...}
+shift
+mkdir -p "$O"
+n=0
+
+fail() { echo "step '$1' failed rc=$2"; [ -f "$3" ] && tail -40 "$3"; exit "$2"; }
+
+for step in "$@"; do
+  n=$((n + 1))
+  IFS=: read -r kind a1 a2 <<< "$step"
+  args=()
+  [ -n "$a2" ] && IFS=, read -r -a args <<< "$a2"
+  echo "=== [$n] $step ($(date +%T))"
+  case "$kind" in
+    tests)
+      log=$O/pytest.log
+      k=(); [ -n "$a1" ] && k=(-k "$a1")
+      timeout -k 10 900 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu tests "${k[@]}" > "$log" 2>&1 \
+        || fail "$step" $? "$log"
+      tail -1 "$log" ;;
+    smoke)
+      log=$O/smoke.log
+      timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$log" 2>&1 || fail "$step" $? "$log"
+      tail -1 "$log" ;;
+    bench)
+      log=$O/bench_$n.log
+      timeout -k 10 700 python -u bench.py --steps "${a1:-20}" --warmup "${a2:-5}" $BENCH_ARGS > "$log" 2>&1 \
+        || fail "$step" $? "$log"
+      tail -1 "$log" | cut -c1-400 ;;
+    prof)
+      log=$O/prof.log
+      timeout -k 10 700 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof" -o run -- \
+        python3 bench.py --steps "${a1:-3}" --warmup 2 --crd-jobs 0 $BENCH_ARGS > "$log" 2>&1 || fail "$step" $? "$log"
+      f=$(find "$O/prof" -name "*kernel_stats.csv" | head -1)
+      python tools/prof_summary.py "$f" "${a1:-3}" > "$O/prof/summary.md" && cp "$f" "$O/prof/kernel_stats.csv"
+      head -18 "$O/prof/summary.md" ;;
+    kbench)
+      log=$O/kbench.txt
+      echo "=== $a1 ${args[*]}" >> "$log"
+      timeout -k 5 120 "tools/kbench/bin/$a1" "${args[@]}" >> "$log" 2>&1 || fail "$step" $? "$log"
+      sed -n '/=== '"$a1"'/,$p' "$log" | tail -12 ;;
+    pmc)
+      bash tools/kbench/pmc.sh "$O/pmc_$n" "$a1" "${args[@]}" || fail "$step" $? ""
+      ;;
+    tool)
+      log=$O/${a1%.py}_$n.log
+      timeout -k 10 600 python -u "tools/$a1" "${args[@]}" > "$log" 2>&1 || fail "$step" $? "$log"
+      grep -v amdgpu.ids "$log" | tail -8 | cut -c1-300 ;;
+    *)
+      echo "unknown step '$step'"; exit 2 ;;
+  esac
+done
+echo "=== session done ($n steps)"

@@ -1,8 +1,8 @@
 // Standalone microbench for the K3 flash-attention kernels (no torch): times the forward and
 // each backward kernel separately with hipEvents at the Llama-3-8B training shape, and checks
 // sampled rows of O, lse, dQ, dK and dV against a float64 CPU reference.  Build variants
-// with -D flags on ops/csrc/flash_attn.hip (tools/kbench/build.sh); run: fa_bench [B S Hq Hkv iters].
-#include "../../service_account_auth_improvements_amd/ops/csrc/flash_attn.hip"
+// with -D flags on flash_attn_lab.hip, a lab copy of ops/csrc/flash_attn.hip (tools/kbench/build.sh); run: fa_bench [B S Hq Hkv iters].
+#include "flash_attn_lab.hip"   // the production kernels plus the measured-and-rejected knobs and stamps
 
 #include <cmath>
 #include <cstdio>

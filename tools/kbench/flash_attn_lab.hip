@@ -41,6 +41,7 @@
 using namespace kf;
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
 typedef __attribute__((ext_vector_type(4))) float f4;
 #define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
 
@@ -51,7 +52,10 @@ constexpr int BK = 64;            // keys per tile (forward / dQ)
 constexpr int TILE = BK * D * 2;  // 16 KB
 constexpr int BKV = 128;          // keys per dK/dV workgroup (4 waves x 32)
 constexpr int QT = 32;            // query rows per dK/dV iteration
-constexpr int QCH = 1024;         // query rows per dK/dV work item (512 / 2048: 6 % / 4 % slower)
+#ifndef KF_FA_QCH
+#define KF_FA_QCH 1024
+#endif
+constexpr int QCH = KF_FA_QCH;    // query rows per dK/dV work item (512 / 2048: 6 % / 4 % slower)
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float LN2 = 0.6931471805599453f;
 
@@ -65,6 +69,17 @@ __device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 __device__ __forceinline__ bf16x8 as_bf16x8(u32x4 v) { return __builtin_bit_cast(bf16x8, v); }
+__device__ __forceinline__ u32x2 tr_read(const char* p) {
+  s16x4 t = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, p));
+  return __builtin_bit_cast(u32x2, t);
+}
+__device__ __forceinline__ bf16x8 tr_pair(const char* base, int o0, int o1) {
+  const u32x2 a = tr_read(base + o0), b = tr_read(base + o1);
+  return as_bf16x8(u32x4{a[0], a[1], b[0], b[1]});
+}
+__device__ __forceinline__ bf16x8 row_read(const char* base, int off) {
+  return as_bf16x8(*reinterpret_cast<const u32x4*>(base + off));
+}
 
 // LDS-DMA of one 16-B piece per lane; `lds` must be wave-uniform (lands at lds + 16*lane)
 __device__ __forceinline__ void glds16(const void* g, char* lds) {
@@ -247,9 +262,11 @@ __device__ __forceinline__ bf16x8 fold_const(float c, int hh) {
 //    gone.  (Measured: +10 % over the FMA form; an MFMA row sum instead of the 32 VALU adds
 //    and static younger-half priority were both slower or null.)
 //  * V^T fragments for output block t+1 are read while block t's MFMAs run.
-// K+V ring depth of the forward and dQ kernels: 4 = 128 KB (5, all 160 KB of LDS, measured the
-// same: profiles/gemm_dw_r3.md)
-constexpr int BQ8 = 256, NST = 4, STG = 2 * TILE;   // stage = K tile + V tile (32 KB)
+// K+V ring depth of the forward and dQ kernels (KF_FA_NST: 4 = 128 KB, 5 = all 160 KB of LDS)
+#ifndef KF_FA_NST
+#define KF_FA_NST 4
+#endif
+constexpr int BQ8 = 256, NST = KF_FA_NST, STG = 2 * TILE;   // stage = K tile + V tile (32 KB)
 static_assert(NST * STG <= 163840, "LDS");
 constexpr float FOLD_T = 8.f;                       // tolerated growth of p above 1 (log2)
 
@@ -269,9 +286,14 @@ __device__ __forceinline__ u32 lane_id_opaque() {
   asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(x));
   return x;
 }
-// K row fragments are read by inline asm FP MFMA steps ahead; tiles staged by SGPR-base DMA
-// (the compiler-scheduled form waited lgkmcnt(0) before every MFMA: profiles/fa_fwd_pipe_ab.txt)
-constexpr int FP = 3;
+// 1 = K row fragments by inline asm, KF_FA_FWD_FP steps ahead + SGPR-base DMA; 0 = compiler-scheduled
+#ifndef KF_FA_FWD_PIPE
+#define KF_FA_FWD_PIPE 1
+#endif
+#ifndef KF_FA_FWD_FP
+#define KF_FA_FWD_FP 3
+#endif
+constexpr int FP = KF_FA_FWD_FP;
 // (measured and removed: ping-pong wave roles -- waves 4-7 taking each tile's barrier after their
 // S chain, 5-deep ring -- 2.31-2.36 vs 2.23-2.25 ms, profiles/fa_fwd_pingpong_ab.txt)
 constexpr int NSTF = NST;   // forward K+V ring depth
@@ -304,6 +326,7 @@ __global__ __launch_bounds__(512, 1) void flash_fwd_kernel(
   }
   const bf16_t* kp = qkv + (long)b * S * ld + (long)(Hq + hkv) * D;
   const bf16_t* vp = qkv + (long)b * S * ld + (long)(Hq + Hkv + hkv) * D;
+#if KF_FA_FWD_PIPE
   u32 dma_kv;   // see the dQ kernel: one lane offset for the K and V panels
   {
     const int row = 4 * w + (l >> 4), ch = (l & 15) ^ swz_x(row);
@@ -319,6 +342,13 @@ __global__ __launch_bounds__(512, 1) void flash_fwd_kernel(
     dma_sv(vb_, dma_kv, st + TILE);
     dma_sv(vb_ + 64 * ld, dma_kv, st + TILE + 8192);
   };
+#else
+  auto stage = [&](int j) {
+    char* st = smem + (j % NSTF) * STG;
+    stage_rows(kp + (long)j * BK * ld, ld, st, BK, w, 8, l);
+    stage_rows(vp + (long)j * BK * ld, ld, st + TILE, BK, w, 8, l);
+  };
+#endif
   const int ntiles = CAUSAL ? min(S, qb * BQ8 + BQ8) / BK : S / BK;
   for (int j = 0; j < NSTF - 1 && j < ntiles; ++j) stage(j);
 
@@ -340,8 +370,9 @@ __global__ __launch_bounds__(512, 1) void flash_fwd_kernel(
   constexpr int AH = NSTF - 1;
   // S'^T = K (c Q)^T - m of tile j: key on the accumulator rows, query on the lane
   auto s_chain = [&](int j, f32x16 (&sc)[2]) {
-    const char* Ks = smem + (j % NSTF) * STG;   // (kept: its removal reorders two SALU ops)
+    const char* Ks = smem + (j % NSTF) * STG;
     (void)Ks;
+#if KF_FA_FWD_PIPE
       // K row fragments by inline asm, FP steps ahead; the two 32-key chains alternate
       const u32 ln = lane_id_opaque(), lr_ = ln & 31;
       const u32 a_t = (lds_addr(smem) + (u32)((j % NSTF) * STG)) + lr_ * 256 + 16 * ((ln >> 5) ^ swz_x(lr_));
@@ -359,6 +390,14 @@ __global__ __launch_bounds__(512, 1) void flash_fwd_kernel(
         lgkm_tie1<(i + FP < 16 ? FP : 15 - i)>(fk[i % (FP + 1)]);
         sc[kt] = mfma32(fk[i % (FP + 1)], qf[ks], sc[kt]);
       });
+#else
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        sc[kt] = mfma32(ones, mref, f32x16{});
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) sc[kt] = mfma32(row_read(Ks, swz(32 * kt + lr, 2 * ks + hh)), qf[ks], sc[kt]);
+      }
+#endif
   };
   // causal mask, online softmax, O^T += V^T P^T of tile j
   auto soft_pv = [&](int j, f32x16 (&sc)[2]) {
@@ -512,9 +551,18 @@ __global__ __launch_bounds__(256) void flash_bwd_pre_kernel(const bf16_t* __rest
 // come out of the MFMA chains with both row constants folded in (hi/lo bf16 split, no
 // accumulator-initialising moves), so dS^T = exp2(c S') * dP' per element; dQ^T += K^T dS^T
 // with the K^T fragments read (inline asm, counted waits) one output block ahead.
-// K/V row fragments by inline asm, QP k-steps ahead; -lse enters through the exp's FMA (a
-// per-lane constant) instead of a folded MFMA per 32-key chain (profiles/fa_dq_lsefma_ab.txt)
-constexpr int QP = 1;
+// 1 = K/V row fragments by inline asm, KF_FA_DQ_QP k-steps ahead; 0 = compiler-scheduled
+#ifndef KF_FA_DQ_PIPE
+#define KF_FA_DQ_PIPE 1
+#endif
+#ifndef KF_FA_DQ_QP
+#define KF_FA_DQ_QP 1
+#endif
+constexpr int QP = KF_FA_DQ_QP;
+// 1 = -lse enters through the exp's FMA (per-lane constant); 0 = folded MFMA per 32-key chain
+#ifndef KF_FA_DQ_LSEFMA
+#define KF_FA_DQ_LSEFMA 1
+#endif
 template <int N>
 __device__ __forceinline__ void lgkm_tie2(bf16x8& a, bf16x8& b) {
   asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "i"(N) : "memory");
@@ -554,6 +602,7 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dq_kernel(
   float dl = delta[((long)b * Hq + h) * S + qc];
   const bf16_t* kp = qkv + (long)b * S * ld + (long)(Hq + hkv) * D;
   const bf16_t* vp = qkv + (long)b * S * ld + (long)(Hq + Hkv + hkv) * D;
+#if KF_FA_DQ_PIPE
   // wave w fills rows 4w.. and 4w+32.. of the K and V images: SGPR panel base + one 32-bit lane
   // offset shared by K and V (same row stride; rows 32 apart share the chunk swizzle)
   u32 dma_kv;
@@ -571,6 +620,13 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dq_kernel(
     dma_sv(vb_, dma_kv, st + TILE);
     dma_sv(vb_ + 64 * ld, dma_kv, st + TILE + 8192);
   };
+#else
+  auto stage = [&](int j) {
+    char* st = smem + (j % NST) * STG;
+    stage_rows(kp + (long)j * BK * ld, ld, st, BK, w, 8, l);
+    stage_rows(vp + (long)j * BK * ld, ld, st + TILE, BK, w, 8, l);
+  };
+#endif
   const int ntiles = CAUSAL ? min(S, qb * BQ8 + BQ8) / BK : S / BK;
   for (int j = 0; j < NST - 1 && j < ntiles; ++j) stage(j);
   // retire the register loads before the loop (see the forward)
@@ -578,7 +634,11 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dq_kernel(
   for (int ks = 0; ks < 8; ++ks) asm volatile("" : "+v"(qf[ks]), "+v"(df[ks]));
   asm volatile("" : "+v"(lse_s), "+v"(dl));
   const bf16x8 ones = fold_ones(hh), dl_b = fold_const(dl, hh);
-  const float nlse = -lse_s * scale_log2;
+#if KF_FA_DQ_PIPE
+  const float nlse = KF_FA_DQ_LSEFMA ? -lse_s * scale_log2 : 0.f;
+#else
+  const bf16x8 lse_b = fold_const(lse_s, hh);
+#endif
   f32x16 dq[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) dq[t] = f32x16{};
@@ -592,11 +652,13 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dq_kernel(
     const int k0 = j * BK;
     if (live && (!CAUSAL || k0 <= qmax_w)) {
       const char* Ks = smem + (j % NST) * STG;
+      const char* Vs = Ks + TILE;
       // non-causal: an opaque false keeps the causal loop's shape (folded away, hipcc spilled)
       int nm = CAUSAL ? (k0 + BK - 1 > qmin_w) : 0;
       if (!CAUSAL) asm volatile("" : "+v"(nm));
       const bool need_mask = __builtin_amdgcn_readfirstlane(nm) != 0;
       bf16x8 sf[2][2];
+#if KF_FA_DQ_PIPE
       // K and V row fragments by inline asm, QP k-steps ahead across both 32-key halves
       // (the compiler-scheduled form waited lgkmcnt(0) before every MFMA pair); this tile's
       // lane base is opaque so the 16 XOR-ed addresses are formed next to their reads
@@ -617,7 +679,7 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dq_kernel(
         if constexpr (ks == 0) {
           // -lse is a per-LANE constant here (query on the lane): it goes into the exp's FMA
           // below instead of a folded MFMA; -delta stays folded (dS needs dP' = dP - delta)
-          s = f32x16{};
+          s = KF_FA_DQ_LSEFMA ? f32x16{} : mfma32(ones, fold_const(lse_s, hh), f32x16{});
           dp = mfma32(ones, dl_b, f32x16{});
         }
         if constexpr (i + QP < 16) rdS(std::integral_constant<int, i + QP>());
@@ -644,6 +706,33 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dq_kernel(
           }
         }
       });
+#else
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        f32x16 s = mfma32(ones, lse_b, f32x16{}), dp = mfma32(ones, dl_b, f32x16{});
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+          s = mfma32(row_read(Ks, swz(32 * kt + lr, 2 * ks + hh)), qf[ks], s);
+          dp = mfma32(row_read(Vs, swz(32 * kt + lr, 2 * ks + hh)), df[ks], dp);
+        }
+        if (need_mask) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = k0 + 32 * kt + (r & 3) + 8 * (r >> 2) + 4 * hh;
+            s[r] = key > q ? -INFINITY : s[r];
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[r] = __builtin_amdgcn_exp2f(s[r] * scale_log2) * dp[r];   // dS^T (unscaled)
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          u32x4 u;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) u[i] = pack2(s[8 * ss + 2 * i], s[8 * ss + 2 * i + 1]);
+          sf[kt][ss] = as_bf16x8(u);
+        }
+      }
+#endif
       const u32 kbase = lds_addr(Ks);
       bf16x8 kf[2][4];
       auto k_read = [&](int t, bf16x8* f) {
@@ -693,9 +782,14 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dq_kernel(
 // Backward: dK / dV
 // ====================================================================================
 namespace fb {
-// waves per dK/dV workgroup (32 keys each): 4 = 128 keys, 66 KB LDS, 2 workgroups per CU (8 waves
-// = 256 keys, 1 workgroup per CU, measured 4.30 vs 4.10-4.21 ms: profiles/fa_dkdv_w8_ab.txt)
-constexpr int NWK = 4;
+// waves per dK/dV workgroup (32 keys each): 4 = 128 keys, 66 KB LDS, 2 workgroups per CU;
+// 8 = 256 keys, 98 KB, 1 workgroup per CU (the same 2 waves per SIMD) -- every staged Q/dO
+// tile, its DMA issue and its barrier are then shared by twice the MFMA work
+#ifndef KF_FA_DKDV_NW
+#define KF_FA_DKDV_NW 4
+#endif
+constexpr int NWK = KF_FA_DKDV_NW;
+static_assert(NWK == 4 || NWK == 8, "dK/dV waves");
 constexpr int BKVW = 32 * NWK;                 // keys per workgroup
 // the per-iteration buffers sit first so their ds_read immediates (buffer + tile offsets)
 // stay below the 16-bit offset field; K (read through a per-wave VGPR base) follows
@@ -703,10 +797,23 @@ constexpr int OFF_Q = 0;                       // [2][32 x 256 B]
 constexpr int OFF_DO = OFF_Q + 16384;          // [2][32 x 256 B]
 constexpr int OFF_LD = OFF_DO + 16384;         // [2][lse 32 f32 | delta 32 f32]
 constexpr int OFF_K = OFF_LD + 512;            // [BKVW keys x 256 B] = 32 / 64 KB (256-B aligned)
-constexpr int SMEM = OFF_K + BKVW * 256;       // 66048 B (2 WG per CU)
-// read-ahead of the software-pipelined iteration: S/dP k-steps (3 row reads each) and dV/dK
-// transposed fragments (a fourth fragment measured no better: profiles/fa_dkdv_pt_ab.txt)
-constexpr int PA = 1, PT = 3;
+constexpr int SMEM = OFF_K + BKVW * 256;       // 66048 B (2 WG per CU) / 98816 B (1 WG per CU)
+// 1 = software-pipelined iteration (inline-asm LDS reads, counted waits); 0 = compiler-scheduled
+#ifndef KF_FA_DKDV_PIPE
+#define KF_FA_DKDV_PIPE 1
+#endif
+// read-ahead of the pipelined iteration: S/dP k-steps (3 row reads each) and dV/dK fragments
+#ifndef KF_FA_DKDV_PA
+#define KF_FA_DKDV_PA 1
+#endif
+#ifndef KF_FA_DKDV_PT
+#define KF_FA_DKDV_PT 3
+#endif
+constexpr int PA = KF_FA_DKDV_PA, PT = KF_FA_DKDV_PT;
+// 1 = s_setprio 1 over the MFMA chains, 0 over the softmax VALU and the DMA issue
+#ifndef KF_FA_DKDV_PRIO
+#define KF_FA_DKDV_PRIO 1
+#endif
 // (measured and removed: a split S / dP chain with the softmax beside the dP MFMAs, and a
 // v_mfma_f32_16x16x32_bf16 form with the row constants as the first MFMA's C operand --
 // 4.38 and 4.39-4.44 ms vs 4.10-4.21 ms, profiles/fa_dkdv_split_ab.txt, fa_dkdv_mfma16_ab.txt)
@@ -716,10 +823,11 @@ template <int J> struct FragJ {
   static constexpr int t = (J & 7) >> 1;
   static constexpr int ss = J & 1;
 };
-// s_setprio 1 over the MFMA chains, 0 over the softmax VALU and the DMA issue
 __device__ __forceinline__ void prio(int p) {
-  if (p) __builtin_amdgcn_s_setprio(1);
-  else __builtin_amdgcn_s_setprio(0);
+  if (KF_FA_DKDV_PRIO) {
+    if (p) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+  }
 }
 
 __host__ __device__ inline int n_chunks(int kb, int S, bool causal) {
@@ -728,6 +836,24 @@ __host__ __device__ inline int n_chunks(int kb, int S, bool causal) {
 }
 }  // namespace fb
 
+// Diagnostic build only (-DKF_FA_STAMPS=1, tools/kbench): per-wave sums of s_memtime deltas between
+// the iteration's phase boundaries (0 start, 1 after the next tile's DMA issue, 2 after the S/dP
+// chain, 3 after the softmax, 4 after the dV/dK chain, 5 after the barrier), written once per wave
+// by vector stores to kf_fa_stamps; the real kernel compiles no stamp.
+#ifndef KF_FA_STAMPS
+#define KF_FA_STAMPS 0
+#endif
+#if KF_FA_STAMPS
+__device__ unsigned long long kf_fa_stamps[1 << 16][8];
+#define KF_STAMP(i)                                                          \
+  do {                                                                       \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime();           \
+    if ((i) > 0) st_acc[(i) - 1] += now_ - st_prev;                          \
+    st_prev = now_;                                                          \
+  } while (0)
+#else
+#define KF_STAMP(i) ((void)0)
+#endif
 template <bool CAUSAL>
 __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kernel(
     const bf16_t* __restrict__ qkv, long ld, const bf16_t* __restrict__ dout, long lddo,
@@ -735,6 +861,9 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
     float* __restrict__ dv_acc, int B, int S, int Hq, int Hkv, float scale, int items_per_head) {
   using namespace fb;
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+#if KF_FA_STAMPS
+  const unsigned long long st_k0 = __builtin_amdgcn_s_memtime();
+#endif
   const int G = Hq / Hkv;
   const int lid = xcd_remap(blockIdx.x, B * Hkv * items_per_head);
   int item = lid % items_per_head;
@@ -765,6 +894,7 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
   bf16x8 vf[8];  // B operand of dP = dO V^T: V[key][16ks + 8hh .. +8]
 #pragma unroll
   for (int ks = 0; ks < 8; ++ks) vf[ks] = as_bf16x8(ld16(vp + (long)(kw0 + lr) * ld + 16 * ks + 8 * hh));
+#if KF_FA_DKDV_PIPE
   const u32 sbase = lds_addr(smem);
   u32 dma_q, dma_do;   // byte offset of this lane's 16-B piece of row 4w + l/16 in a Q / dO panel
   {
@@ -772,11 +902,18 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
     dma_q = (u32)((row * ld + ch * 8) * 2);
     dma_do = (u32)((row * lddo + ch * 8) * 2);
   }
+#endif
 
+#if KF_FA_DKDV_PIPE
   // iteration it = (head hq, query tile qt) is carried incrementally (no runtime division)
   auto stage = [&](int hq, int qt, int buf) {
+#else
+  auto stage = [&](int it, int buf) {
+    const int hq = it / ntq, qt = it - hq * ntq;
+#endif
     const int h = hkv * G + hq;
     const int q0 = qs + qt * QT;
+#if KF_FA_DKDV_PIPE
     // wave w fills rows 4w.. and 4w+16.. of the Q and dO images: SGPR panel base + one 32-bit
     // lane offset per tensor (rows 16 apart share the lane's chunk swizzle)
     const char* qb_ = reinterpret_cast<const char*>(qkv + (rowB + q0) * ld + (long)h * D);
@@ -788,6 +925,10 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
       dma_sv(qb_ + 32 * ld, dma_q, lq + 4096);
       dma_sv(db_ + 32 * lddo, dma_do, ldo_ + 4096);
     }
+#else
+    stage_rows(qkv + (rowB + q0) * ld + (long)h * D, ld, smem + OFF_Q + buf * 8192, QT, w, 4, l);
+    stage_rows(dout + (rowB + q0) * lddo + (long)h * D, lddo, smem + OFF_DO + buf * 8192, QT, w, 4, l);
+#endif
     if (w == 0) {
       // lse/delta select from an opaque lane id: hoisted, the per-lane 64-bit pointer lived
       // across the loop and was the kernel's only scratch spill
@@ -804,9 +945,14 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
   const int vrow = 4 * hh + ((l & 15) >> 2);
   const int vcol = 16 * ((l >> 4) & 1) + 4 * (l & 3);
 
+#if KF_FA_DKDV_PIPE
   if (niter > 0) stage(0, 0, 0);
+#else
+  if (niter > 0) stage(0, 0);
+#endif
   wait_dma_barrier();
   const bf16x8 ones = fold_ones(hh);
+#if KF_FA_DKDV_PIPE
   int nx_hq = 0, nx_qt = 0;   // (head, tile) of the NEXT iteration to stage
   auto adv = [&]() {
     if (++nx_qt == ntq) { nx_qt = 0; ++nx_hq; }
@@ -831,12 +977,18 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
       const int row = 16 * ss + vrow + 8 * hf;
       a_tr[ss][hf] = sbase + row * 256 + 16 * ((vcol >> 3) ^ swz_x(row)) + 8 * (l & 1);
     }
+#if KF_FA_STAMPS
+  unsigned long long st_acc[5] = {0, 0, 0, 0, 0}, st_prev = 0;
+  const unsigned long long st_loop0 = __builtin_amdgcn_s_memtime();
+#endif
   auto iter = [&](auto curc, int it) {
     constexpr int CUR = decltype(curc)::value;
     constexpr int OQ = OFF_Q + CUR * 8192, OD = OFF_DO + CUR * 8192, OL = CUR * 256;
     const int q0 = qs + nx_qt * QT;   // this iteration's tile (advanced below to the next)
+    KF_STAMP(0);
     adv();
     if (it + 1 < niter) stage(nx_hq, nx_qt, CUR ^ 1);
+    KF_STAMP(1);
     // opaque per iteration: keeps the 32 XOR-ed per-read addresses from being hoisted out of
     // the loop as invariants (they would pin ~30 VGPRs and spill)
     u32 a_row = a_row0, a_k = a_k0, a_t00 = a_tr[0][0], a_t01 = a_tr[0][1], a_t10 = a_tr[1][0], a_t11 = a_tr[1][1];
@@ -872,6 +1024,7 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
         ft[j % (PT + 1)] = rd_tr2<(j < 8 ? OD : OQ)>(a_t[ss][0] ^ (64 * t), a_t[ss][1] ^ (64 * t));
       };
       static_for<0, PT>([&](auto jc) { rdT(jc); });
+      KF_STAMP(2);
       prio(0);
       const int key = kw0 + lr;
       // non-causal: an opaque false keeps the causal loop's shape (with the masked path folded
@@ -901,6 +1054,7 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
         pf[ss] = as_bf16x8(u);
         sf[ss] = as_bf16x8(v);
       }
+      KF_STAMP(3);
       prio(1);
       static_for<0, 16>([&](auto jc) {
         constexpr int j = decltype(jc)::value, t = FragJ<j>::t, ss = FragJ<j>::ss, sl = j % (PT + 1);
@@ -910,8 +1064,10 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
         else dK[t] = mfma32(ft[sl], sf[ss], dK[t]);
       });
       prio(0);
+      KF_STAMP(4);
     }
     wait_dma_barrier();
+    KF_STAMP(5);
   };
   {
     int it = 0;
@@ -921,6 +1077,74 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
     }
     if (it < niter) iter(std::integral_constant<int, 0>(), it);
   }
+#if KF_FA_STAMPS
+  const unsigned long long st_loop1 = __builtin_amdgcn_s_memtime();
+#endif
+#else
+  for (int it = 0; it < niter; ++it) {
+    const int cur = it & 1;
+    const int qt = it % ntq;
+    const int q0 = qs + qt * QT;
+    if (it + 1 < niter) stage(it + 1, cur ^ 1);
+    const char* Qs = smem + OFF_Q + cur * 8192;
+    const char* dOs = smem + OFF_DO + cur * 8192;
+    const float* Ls = reinterpret_cast<const float*>(smem + OFF_LD + cur * 256);
+    if (!CAUSAL || kw0 <= q0 + QT - 1) {
+      // row constants -lse/scale and -delta of query row lr folded into the chains
+      f32x16 s = mfma32(fold_const(Ls[lr] * inv_scale, hh), ones, f32x16{});
+      f32x16 dp = mfma32(fold_const(Ls[32 + lr], hh), ones, f32x16{});
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        s = mfma32(row_read(Qs, swz(lr, 2 * ks + hh)), row_read(smem + OFF_K, swz(32 * w + lr, 2 * ks + hh)), s);
+        dp = mfma32(row_read(dOs, swz(lr, 2 * ks + hh)), vf[ks], dp);
+      }
+      const int key = kw0 + lr;
+      const bool need_mask = CAUSAL && (kw0 + 31 > q0);
+      if (need_mask) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = __builtin_amdgcn_exp2f(s[r] * c);
+          s[r] = key > q0 + (r & 3) + 8 * (r >> 2) + 4 * hh ? 0.f : p;
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[r] = __builtin_amdgcn_exp2f(s[r] * c);
+      }
+      bf16x8 pf[2];
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        u32x4 u;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) u[i] = pack2(s[8 * ss + 2 * i], s[8 * ss + 2 * i + 1]);
+        pf[ss] = as_bf16x8(u);
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          const int row = 16 * ss + vrow, col = 32 * t + vcol;
+          dV[t] = mfma32(tr_pair(dOs, swz8(row, col), swz8(row + 8, col)), pf[ss], dV[t]);
+        }
+      bf16x8 sf[2];
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        u32x4 u;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          u[i] = pack2(s[8 * ss + 2 * i] * dp[8 * ss + 2 * i], s[8 * ss + 2 * i + 1] * dp[8 * ss + 2 * i + 1]);
+        sf[ss] = as_bf16x8(u);
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          const int row = 16 * ss + vrow, col = 32 * t + vcol;
+          dK[t] = mfma32(tr_pair(Qs, swz8(row, col), swz8(row + 8, col)), sf[ss], dK[t]);
+        }
+    }
+    wait_dma_barrier();
+  }
+#endif
   // ---- chunk partial sums: transpose [d][key] accumulators through LDS, row-contiguous adds,
   // 128 keys (4 waves' accumulators) per pass
   float* T = reinterpret_cast<float*>(smem);   // [128 keys][128 d] fp32 = 64 KB
@@ -945,6 +1169,273 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
       }
       __syncthreads();
     }
+  };
+  flush(dK, scale, dk_acc);
+  flush(dV, 1.f, dv_acc);
+#if KF_FA_STAMPS
+  {
+    const unsigned long long st_end = __builtin_amdgcn_s_memtime();
+    const int slot = (blockIdx.x * NWK + w) & ((1 << 16) - 1);
+    // one lane per value (vector stores): 0-4 loop phases, 5 iterations, 6 prologue, 7 flush
+    unsigned long long v = 0;
+    for (int k = 0; k < 5; ++k) v = l == k ? st_acc[k] : v;
+    v = l == 5 ? (unsigned long long)niter : v;
+    v = l == 6 ? st_loop0 - st_k0 : v;
+    v = l == 7 ? st_end - st_loop1 : v;
+    if (l < 8) kf_fa_stamps[slot][l] = v;
+  }
+#endif
+}
+
+// ---- 64 keys per wave, one wave per SIMD (512-register budget) -------------------------
+// The 32-key kernel above reads 40 KB of LDS per wave and 32-query iteration (Q and dO row
+// fragments, the K fragments again, Q^T and dO^T transposed fragments) for 32 MFMAs, and its
+// 256 VGPRs spill.  Here each wave owns 64 keys as two 32-key groups: every Q/dO/Q^T/dO^T
+// fragment read feeds BOTH groups' MFMAs (48 KB for 64 MFMAs), V stays in registers, and the
+// 256 dK^T/dV^T accumulator registers go to the AGPR half of the unified 512-entry file
+// (1 workgroup of 4 waves per CU).  Measured (profiles/attention_microbench.txt): no spill
+// and the same speed as the 32-key kernel; phase stamps put both MFMA phases at ~2x their
+// MFMA floor, waiting on LDS-read latency at one wave per SIMD.
+namespace fb2 {
+constexpr int BKV2 = 256;                       // keys per workgroup (4 waves x 64)
+constexpr int OFF_K = 0;                       // [256 keys x 256 B] = 64 KB
+constexpr int OFF_Q = 65536;                   // [2][32 x 256 B]
+constexpr int OFF_DO = OFF_Q + 16384;          // [2][32 x 256 B]
+constexpr int OFF_LD = OFF_DO + 16384;         // [2][lse 32 f32 | delta 32 f32]
+constexpr int SMEM = 131072;                   // the flush transposes [256 keys][128 d] fp32
+
+__host__ __device__ inline int n_chunks(int kb, int S, bool causal) {
+  const int q0 = causal ? kb * BKV2 : 0;
+  return (S - q0 + QCH - 1) / QCH;
+}
+}  // namespace fb2
+
+// acc += a.b with the accumulator pinned to AGPRs: left to itself, hipcc picks the VGPR form
+// of the MFMA and parks the 256 accumulators in AGPRs between uses (~1200 v_accvgpr moves
+// per iteration)
+// (flash_attn.hip is built with -mllvm -amdgpu-mfma-vgpr-form so that the builtin S/dP chains
+// keep their accumulators in VGPRs).  The hazard recognizer does not look inside inline asm,
+// so the waits it would insert are explicit: two wait states before every MFMA (a VALU op may
+// just have written its B operand; the pad fills an MFMA issue gap) and drain_mfma() before
+// the accumulators are read back.
+__device__ __forceinline__ void mfma32_agpr(f32x16& acc, bf16x8 a, bf16x8 b) {
+  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ bf16x8 ds_b128(u32 addr) {
+  u32x4 v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr) : "memory");
+  return as_bf16x8(v);
+}
+__device__ __forceinline__ float ds_f32(u32 addr) {
+  float v;
+  asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"(addr) : "memory");
+  return v;
+}
+__device__ __forceinline__ void drain_mfma() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory"); }
+
+template <bool CAUSAL>
+__global__ __launch_bounds__(256, 1) void flash_bwd_dkdv64_kernel(
+    const bf16_t* __restrict__ qkv, long ld, const bf16_t* __restrict__ dout, long lddo,
+    const float* __restrict__ lse, const float* __restrict__ delta, float* __restrict__ dk_acc,
+    float* __restrict__ dv_acc, int B, int S, int Hq, int Hkv, float scale, int items_per_head) {
+  using namespace fb2;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  const int G = Hq / Hkv;
+  const int lid = xcd_remap(blockIdx.x, B * Hkv * items_per_head);
+  int item = lid % items_per_head;
+  const int bh = lid / items_per_head;
+  const int hkv = bh % Hkv, b = bh / Hkv;
+  const int nkb = S / BKV2;
+  int kb = 0;
+  for (; kb < nkb; ++kb) {
+    const int n = n_chunks(kb, S, CAUSAL);
+    if (item < n) break;
+    item -= n;
+  }
+  const int kv0 = kb * BKV2;
+  const int qs = (CAUSAL ? kv0 : 0) + item * QCH;
+  const int qe = min(S, qs + QCH);
+  const int ntq = (qe - qs) / QT;
+  const int niter = ntq * G;
+
+  const int tid = threadIdx.x, l = tid & 63, lr = l & 31, hh = l >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kw0 = kv0 + 64 * w;
+  const float c = scale * LOG2E, inv_scale = 1.f / scale;
+  const long rowB = (long)b * S;
+  const bf16_t* kp = qkv + rowB * ld + (long)(Hq + hkv) * D;
+  const bf16_t* vp = qkv + rowB * ld + (long)(Hq + Hkv + hkv) * D;
+
+  stage_rows(kp + (long)kv0 * ld, ld, smem + OFF_K, BKV2, w, 4, l);
+  bf16x8 vf[2][8];  // B operand of dP = dO V^T: V[key][16ks + 8hh .. +8], both key groups
+#pragma unroll
+  for (int kg = 0; kg < 2; ++kg)
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks)
+      vf[kg][ks] = as_bf16x8(ld16(vp + (long)(kw0 + 32 * kg + lr) * ld + 16 * ks + 8 * hh));
+
+  auto stage = [&](int it, int buf) {
+    const int hq = it / ntq, qt = it - hq * ntq;
+    const int h = hkv * G + hq;
+    const int q0 = qs + qt * QT;
+    stage_rows(qkv + (rowB + q0) * ld + (long)h * D, ld, smem + OFF_Q + buf * 8192, QT, w, 4, l);
+    stage_rows(dout + (rowB + q0) * lddo + (long)h * D, lddo, smem + OFF_DO + buf * 8192, QT, w, 4, l);
+    if (w == 0) {
+      const float* src = (l < 32 ? lse : delta) + ((long)b * Hq + h) * S + q0 + (l & 31);
+      glds4(src, smem + OFF_LD + buf * 256);
+    }
+  };
+
+  f32x16 dK[2][4], dV[2][4];
+#pragma unroll
+  for (int kg = 0; kg < 2; ++kg)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) { dK[kg][t] = f32x16{}; dV[kg][t] = f32x16{}; }
+  const int vrow = 4 * hh + ((l & 15) >> 2);
+  const int vcol = 16 * ((l >> 4) & 1) + 4 * (l & 3);
+
+  if (niter > 0) stage(0, 0);
+  wait_dma_barrier();
+  const bf16x8 ones = fold_ones(hh);
+  // Every LDS read in the loop is inline asm with counted lgkmcnt waits: hipcc orders a
+  // compiler-visible LDS read behind every LDS-DMA in flight (s_waitcnt vmcnt(0)), which would
+  // make each iteration wait for the NEXT tile's staging right after issuing it.
+  const u32 k_lds = lds_addr(smem + OFF_K);
+  for (int it = 0; it < niter; ++it) {
+    const int cur = it & 1;
+    const int qt = it % ntq;
+    const int q0 = qs + qt * QT;
+    if (it + 1 < niter) stage(it + 1, cur ^ 1);
+    const u32 q_lds = lds_addr(smem + OFF_Q + cur * 8192), do_lds = lds_addr(smem + OFF_DO + cur * 8192);
+    const u32 l_lds = lds_addr(smem + OFF_LD + cur * 256);
+    {
+      // No causal skip: a wave whose keys all lie above the tile's queries runs fully masked
+      // (diagonal tiles only, ~1.6 % of the work); a skip branch would make the loop-carried
+      // accumulators flow through a join, which hipcc resolves by copying all 256 of them
+      // AGPR -> VGPR -> AGPR every iteration.
+      float lse_s = ds_f32(l_lds + 4 * lr), dl = ds_f32(l_lds + 128 + 4 * lr);
+      // operand fragments one k-step ahead (4 reads per step)
+      bf16x8 fr[2][4];
+      auto rd = [&](int ks, int bf) {
+        fr[bf][0] = ds_b128(q_lds + swz(lr, 2 * ks + hh));
+        fr[bf][1] = ds_b128(do_lds + swz(lr, 2 * ks + hh));
+        fr[bf][2] = ds_b128(k_lds + swz(64 * w + lr, 2 * ks + hh));
+        fr[bf][3] = ds_b128(k_lds + swz(64 * w + 32 + lr, 2 * ks + hh));
+      };
+      rd(0, 0);
+      asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(lse_s), "+v"(dl) :: "memory");
+      // row constants -lse/scale and -delta of query row lr, folded once and shared by both groups
+      const f32x16 s_init = mfma32(fold_const(lse_s * inv_scale, hh), ones, f32x16{});
+      const f32x16 dp_init = mfma32(fold_const(dl, hh), ones, f32x16{});
+      f32x16 s[2] = {s_init, s_init}, dp[2] = {dp_init, dp_init};
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        const int bf = ks & 1;
+        if (ks < 7) {
+          rd(ks + 1, bf ^ 1);
+          lgkm_wait_tie<4>(fr[bf]);
+        } else {
+          lgkm_wait_tie<0>(fr[bf]);
+        }
+#pragma unroll
+        for (int kg = 0; kg < 2; ++kg) {
+          s[kg] = mfma32(fr[bf][0], fr[bf][2 + kg], s[kg]);
+          dp[kg] = mfma32(fr[bf][1], vf[kg][ks], dp[kg]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // causal mask without a branch (a masked/unmasked split doubles the live code and
+      // spills): element r of this lane is masked iff key - q0 - 4hh > (r & 3) + 8 (r >> 2)
+#pragma unroll
+      for (int kg = 0; kg < 2; ++kg) {
+        const int lim = kw0 + 32 * kg + lr - q0 - 4 * hh;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = __builtin_amdgcn_exp2f(s[kg][r] * c);
+          s[kg][r] = (CAUSAL && lim > (r & 3) + 8 * (r >> 2)) ? 0.f : p;
+        }
+      }
+      bf16x8 pf[2][2];
+#pragma unroll
+      for (int kg = 0; kg < 2; ++kg)
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          u32x4 u;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) u[i] = pack2(s[kg][8 * ss + 2 * i], s[kg][8 * ss + 2 * i + 1]);
+          pf[kg][ss] = as_bf16x8(u);
+        }
+      // dV^T += dO^T P and dK^T += Q^T dS: one transposed A fragment feeds both key groups,
+      // read one step ahead of its two MFMAs
+      auto tr = [&](u32 base, int st) {
+        const int row = 16 * (st & 1) + vrow, col = 32 * (st >> 1) + vcol;
+        return tr_pair_asm(base + swz8(row, col), base + swz8(row + 8, col));
+      };
+      bf16x8 ta[2];
+      ta[0] = tr(do_lds, 0);
+#pragma unroll
+      for (int st = 0; st < 8; ++st) {
+        const int t = st >> 1, ss = st & 1, bf = st & 1;
+        if (st < 7) {
+          ta[bf ^ 1] = tr(do_lds, st + 1);
+          lgkm_tie1<2>(ta[bf]);
+        } else {
+          lgkm_tie1<0>(ta[bf]);
+        }
+        mfma32_agpr(dV[0][t], ta[bf], pf[0][ss]);
+        mfma32_agpr(dV[1][t], ta[bf], pf[1][ss]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      bf16x8 sf[2][2];
+#pragma unroll
+      for (int kg = 0; kg < 2; ++kg)
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          u32x4 u;
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            u[i] = pack2(s[kg][8 * ss + 2 * i] * dp[kg][8 * ss + 2 * i],
+                         s[kg][8 * ss + 2 * i + 1] * dp[kg][8 * ss + 2 * i + 1]);
+          sf[kg][ss] = as_bf16x8(u);
+        }
+      ta[0] = tr(q_lds, 0);
+#pragma unroll
+      for (int st = 0; st < 8; ++st) {
+        const int t = st >> 1, ss = st & 1, bf = st & 1;
+        if (st < 7) {
+          ta[bf ^ 1] = tr(q_lds, st + 1);
+          lgkm_tie1<2>(ta[bf]);
+        } else {
+          lgkm_tie1<0>(ta[bf]);
+        }
+        mfma32_agpr(dK[0][t], ta[bf], sf[0][ss]);
+        mfma32_agpr(dK[1][t], ta[bf], sf[1][ss]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    wait_dma_barrier();
+  }
+  // ---- chunk partial sums: transpose [d][key] accumulators through LDS, row-contiguous adds
+  drain_mfma();
+  float* T = reinterpret_cast<float*>(smem);   // [256 keys][128 d] fp32 = 128 KB
+  auto flush = [&](const f32x16(&acc)[2][4], float mul, float* dst_base) {
+#pragma unroll
+    for (int kg = 0; kg < 2; ++kg)
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int d = 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          const int key = 64 * w + 32 * kg + lr;
+          T[key * 128 + (d ^ ((key & 31) << 2))] = acc[kg][t][r] * mul;
+        }
+    __syncthreads();
+    float* dst = dst_base + (rowB + kv0) * (long)(Hkv * D) + (long)hkv * D;
+    for (int e = tid; e < BKV2 * 128; e += 256) {
+      const int key = e >> 7, d = e & 127;
+      atomicAdd(dst + (long)key * Hkv * D + d, T[key * 128 + (d ^ ((key & 31) << 2))]);
+    }
+    __syncthreads();
   };
   flush(dK, scale, dk_acc);
   flush(dV, 1.f, dv_acc);
@@ -1004,6 +1495,13 @@ bool bwd_fork_enabled() {
   }();
   return on;
 }
+// dK/dV kernel choice, read per call: the 32-keys-per-wave kernel is the default (in-step
+// 1-GPU Llama-3-8B A/B with the dQ fork: 21.89k vs 21.76k tok/s, profiles/attention_microbench.txt);
+// KFAMD_FA_DKDV=64 selects the 64-key, one-wave-per-SIMD kernel.
+bool dkdv64_enabled() {
+  const char* e = getenv("KFAMD_FA_DKDV");
+  return e && std::atoi(e) == 64;
+}
 BwdFork* bwd_fork() {
   static BwdFork per_dev[64];
   int dev = 0;
@@ -1052,18 +1550,32 @@ int kf_flash_bwd(const void* qkv, long ld, const void* o, long ldo, const void* 
   if (skv != st &&
       (hipEventRecord(fk->pre, st) != hipSuccess || hipStreamWaitEvent(skv, fk->pre, 0) != hipSuccess))
     return fail(2);
+  const bool kv64 = dkdv64_enabled() && S % fb2::BKV2 == 0;
   int items = 0;
-  for (int kb = 0; kb < S / BKVW; ++kb) items += n_chunks(kb, S, causal);
+  if (kv64)
+    for (int kb = 0; kb < S / fb2::BKV2; ++kb) items += fb2::n_chunks(kb, S, causal);
+  else
+    for (int kb = 0; kb < S / BKVW; ++kb) items += n_chunks(kb, S, causal);
   const int g_kv = B * Hkv * items, g_q = B * Hq * ((S + BQ8 - 1) / BQ8);
   const float sl2 = scale * LOG2E;
+  if (kv64) {
+    if (causal)
+      flash_bwd_dkdv64_kernel<true><<<g_kv, 256, 0, skv>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo, lse,
+                                                           delta, dk_acc, dv_acc, B, S, Hq, Hkv, scale, items);
+    else
+      flash_bwd_dkdv64_kernel<false><<<g_kv, 256, 0, skv>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo, lse,
+                                                            delta, dk_acc, dv_acc, B, S, Hq, Hkv, scale, items);
+  }
   if (causal) {
-    flash_bwd_dkdv_kernel<true><<<g_kv, 64 * NWK, 0, skv>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo, lse,
-                                                         delta, dk_acc, dv_acc, B, S, Hq, Hkv, scale, items);
+    if (!kv64)
+      flash_bwd_dkdv_kernel<true><<<g_kv, 64 * NWK, 0, skv>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo,
+                                                         lse, delta, dk_acc, dv_acc, B, S, Hq, Hkv, scale, items);
     flash_bwd_dq_kernel<true><<<g_q, 512, 0, st>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo, lse,
                                                    delta, (bf16_t*)dqkv, lddqkv, B, S, Hq, Hkv, sl2, scale);
   } else {
-    flash_bwd_dkdv_kernel<false><<<g_kv, 64 * NWK, 0, skv>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo, lse,
-                                                          delta, dk_acc, dv_acc, B, S, Hq, Hkv, scale, items);
+    if (!kv64)
+      flash_bwd_dkdv_kernel<false><<<g_kv, 64 * NWK, 0, skv>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo,
+                                                        lse, delta, dk_acc, dv_acc, B, S, Hq, Hkv, scale, items);
     flash_bwd_dq_kernel<false><<<g_q, 512, 0, st>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo, lse,
                                                     delta, (bf16_t*)dqkv, lddqkv, B, S, Hq, Hkv, sl2, scale);
   }
