@@ -22,11 +22,21 @@ the next forward (runtime/trainer.py, parallel/ddp.py).  ``--no-zero1`` = all-re
 CRD-to-first-step (the metric's second half): before any GPU use, ``--crd-jobs`` PyTorchJob CRs
 of the same model (micro-batch 1, one step each) go through the in-repo control plane running
 as processes; the JSON line carries ``crd_to_first_step_p50_s`` / ``_p90_s`` and the breakdown
-(service_account_auth_improvements_amd/crdbench.py).
+(service_account_auth_improvements_amd/crdbench.py).  Each job asks for ``--gpus`` GPUs
+(``nprocPerNode`` = N), so at N > 1 the rendezvous and RCCL communicator set-up are inside the
+clock.  Under an external torchrun the other ranks wait (off the GPU) until rank 0 has measured.
+
+First contact with a multi-GPU node: the run refuses within seconds, with one JSON ``error``
+line and a non-zero status, when fewer GPUs are visible than ``--gpus``; a rank that makes no
+progress for ``--hang-timeout`` seconds (a hung or failed collective) prints a JSON line naming
+the step / bucket / collective it stopped at and exits non-zero (runtime/progress.py); the
+process-group timeout sits just above it and ``TORCH_NCCL_ASYNC_ERROR_HANDLING=1`` turns an
+RCCL error into an abort.  Every rank prints per-step progress to stderr.
 """
 from __future__ import annotations
 
 import argparse
+import datetime
 import json
 import os
 import socket
@@ -39,7 +49,8 @@ import torch.distributed as dist
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
-from service_account_auth_improvements_amd.parallel.state import init_distributed  # noqa: E402
+from service_account_auth_improvements_amd.parallel.state import init_distributed, visible_gpu_count  # noqa: E402
+from service_account_auth_improvements_amd.runtime import progress  # noqa: E402
 from service_account_auth_improvements_amd.runtime.trainer import (SyntheticData, TrainConfig,  # noqa: E402
                                                                    Trainer)
 
@@ -91,6 +102,60 @@ def _launch_ranks(n: int, crd: "dict | None") -> int:
 CRD_ENV = "KFAMD_BENCH_CRD_RESULT"
 
 
+def _error_exit(a, msg: str, code: int = 2, **extra) -> None:
+    """One JSON line naming what failed (the driver parses stdout), then exit ``code``."""
+    rec = {"metric": BASELINE_METRIC, "value": None, "unit": "tokens/s", "n_gpus": a.gpus,
+           "error": msg, **extra}
+    print(json.dumps(rec), flush=True)
+    print(f"bench: {msg}", file=sys.stderr, flush=True)
+    sys.exit(code)
+
+
+def _preflight(a) -> None:
+    """Refuse a run this node cannot do, before anything touches the GPU: fewer visible GPUs
+    than ``--gpus`` (no GPU at all = the CPU/gloo rehearsal, allowed)."""
+    n = visible_gpu_count()
+    if 0 < n < a.gpus:
+        _error_exit(a, f"--gpus {a.gpus} but only {n} GPU(s) visible: refusing (one rank per GPU)",
+                    visible_gpus=n)
+
+
+def _crd_gate_path() -> str:
+    tag = f"{os.environ.get('MASTER_PORT', '0')}_{os.environ.get('TORCHELASTIC_RUN_ID', 'none')}"
+    return os.path.join(os.environ.get("TMPDIR", "/tmp"), f"kfamd_bench_crd_{tag}.json")
+
+
+def _crd_gate(a, rank: int, crd) -> "dict | None":
+    """External launcher (the driver's torchrun): rank 0 measures CRD-to-first-step while the
+    other ranks wait here, off the GPU, for its marker file -- so the measured jobs have the
+    node to themselves and the process-group timeout need not cover the measurement."""
+    path = _crd_gate_path()
+    if rank == 0:
+        tmp = path + ".tmp"
+        with open(tmp, "w") as f:
+            json.dump(crd, f)
+        os.replace(tmp, path)
+        return crd
+    deadline = time.time() + a.crd_timeout * max(1, a.crd_jobs) + 120
+    while not os.path.exists(path):
+        if time.time() > deadline:
+            _error_exit(a, f"rank {rank}: rank 0's CRD-to-first-step phase did not finish", code=3)
+        time.sleep(0.2)
+    return None
+
+
+def _fault(rank: int, step: int) -> None:
+    """Fault injection for the hang tests: ``KFAMD_BENCH_FAULT=hang:RANK:STEP`` stops RANK at
+    global step STEP (warm-up steps count), as a rank that skipped its collectives would."""
+    spec = os.environ.get("KFAMD_BENCH_FAULT", "")
+    if spec.startswith("hang:"):
+        _, r, s_ = spec.split(":")
+        if int(r) == rank and int(s_) == step:
+            print(f"bench[r{rank}]: injected hang at step {step}", file=sys.stderr, flush=True)
+            while True:
+                time.sleep(3600)
+
+
 def _crd_to_first_step(a) -> "dict | None":
     """The metric's second half, measured before this process touches the GPU: the in-repo
     control plane as processes (apiserver / controller-manager / kubelet), ``--crd-jobs``
@@ -99,11 +164,13 @@ def _crd_to_first_step(a) -> "dict | None":
     if a.crd_jobs <= 0:
         return None
     from service_account_auth_improvements_amd.crdbench import measure
-    gpus = 1 if torch.cuda.device_count() > 0 else 0          # counts devices, no HIP context
+    on_gpu = visible_gpu_count() > 0            # amdsmi / sysfs: this process stays off the GPU
     t0 = time.time()
     try:
-        res = measure(jobs=a.crd_jobs, model=a.model, gpus=gpus, seq_len=a.seq_len, micro_batch=1,
-                      layers=a.layers, device="cuda" if gpus else "cpu", timeout=a.crd_timeout)
+        # each job is the bench's own world: --gpus ranks (nprocPerNode), so at N > 1 the
+        # N-rank rendezvous and RCCL communicator initialisation are inside the clock
+        res = measure(jobs=a.crd_jobs, model=a.model, gpus=a.gpus, seq_len=a.seq_len, micro_batch=1,
+                      layers=a.layers, device="cuda" if on_gpu else "cpu", timeout=a.crd_timeout)
     except Exception as e:   # the throughput half still runs; the record says what failed
         print(f"bench: CRD-to-first-step failed: {e}", file=sys.stderr, flush=True)
         return {"error": str(e)[-500:]}
@@ -155,20 +222,50 @@ def main():
                     help="PyTorchJobs submitted to the process-level control plane before the throughput run "
                          "to measure CRD-to-first-step (0 = skip)")
     ap.add_argument("--crd-timeout", type=float, default=300.0)
+    ap.add_argument("--hang-timeout", type=float, default=180.0,
+                    help="seconds without progress (step, bucket, collective) before a rank reports where it "
+                         "stopped and exits non-zero; the process-group timeout is this + 60 s")
     a = ap.parse_args()
 
     env_world = os.environ.get("WORLD_SIZE")
-    if env_world is None and a.gpus > 1:
-        sys.exit(_launch_ranks(a.gpus, _crd_to_first_step(a)))
+    if env_world is None:
+        _preflight(a)
+        if a.gpus > 1:
+            sys.exit(_launch_ranks(a.gpus, _crd_to_first_step(a)))
     if int(env_world or 1) != a.gpus:
-        print(f"bench: --gpus {a.gpus} but WORLD_SIZE={env_world}: refusing to report a "
-              "different GPU count", file=sys.stderr)
-        sys.exit(2)
+        _error_exit(a, f"--gpus {a.gpus} but WORLD_SIZE={env_world}: refusing to report a different GPU count")
+    rank = int(os.environ.get("RANK", "0"))
+    if env_world is not None and CRD_ENV not in os.environ:
+        _preflight(a)     # external torchrun: every rank checks before it touches a GPU
     crd = None
-    if int(os.environ.get("RANK", "0")) == 0:
-        # self-launched ranks inherit the parent's measurement; under an external launcher rank 0
-        # measures it while the other ranks wait in the process-group rendezvous
-        crd = json.loads(os.environ[CRD_ENV]) if CRD_ENV in os.environ else _crd_to_first_step(a)
+    if CRD_ENV in os.environ:          # self-launched ranks inherit the parent's measurement
+        crd = json.loads(os.environ[CRD_ENV]) if rank == 0 else None
+    else:
+        crd = _crd_to_first_step(a) if rank == 0 else None
+        if env_world is not None and int(env_world) > 1 and a.crd_jobs > 0:
+            crd = _crd_gate(a, rank, crd)
+    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+    # rank 0 reports first: the other ranks' watchdogs give it 15 s before they exit themselves
+    dog = progress.Watchdog(a.hang_timeout + (0 if rank == 0 else 15),
+                            lambda: {"metric": BASELINE_METRIC, "value": None, "n_gpus": a.gpus, "rank": rank},
+                            to_stdout=rank == 0).start()
+    try:
+        _run(a, rank, crd)
+    except SystemExit:
+        raise
+    except BaseException as e:   # a failed collective / kernel: one JSON line from rank 0, rc != 0
+        if rank == 0:
+            print(json.dumps({"metric": BASELINE_METRIC, "value": None, "n_gpus": a.gpus,
+                              "error": f"{type(e).__name__}: {str(e)[-400:]}", "stopped_at": progress.last()}),
+                  flush=True)
+        raise
+    finally:
+        dog.stop()
+
+
+def _run(a, rank: int, crd):
+    pg_timeout = int(a.hang_timeout + 60)
+    progress.mark("init_distributed")
     if a.force_collectives:
         if a.gpus != 1:
             sys.exit("bench: --force-collectives is a one-GPU rehearsal")
@@ -177,10 +274,12 @@ def main():
             os.environ.setdefault(k, v)
         if torch.cuda.is_available():
             torch.cuda.set_device(0)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", 0),
+                                    timeout=datetime.timedelta(seconds=pg_timeout))
         else:
-            dist.init_process_group("gloo")
-    st = init_distributed(tp=a.tp, pp=a.pp)
+            dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=pg_timeout))
+    st = init_distributed(tp=a.tp, pp=a.pp, timeout_s=pg_timeout)
+    progress.mark("model_init")
     world = st.world_size
     if a.zero1 is None:
         a.zero1 = st.dp > 1 or a.force_collectives
@@ -215,20 +314,33 @@ def main():
     init_s = time.time() - t0
 
     losses = []
-    for i in range(a.warmup):
+
+    def step(i: int, kind: str):
+        _fault(rank, i)
+        progress.mark(kind, f"step {i}")
+        t = time.perf_counter()
         losses.append(tr.train_step(batches[i % 2]))
+        if world > 1:     # per-rank progress (host time: steps run ahead of the device)
+            print(f"bench[r{rank}]: {kind} step {i} host {1e3 * (time.perf_counter() - t):.0f} ms",
+                  file=sys.stderr, flush=True)
+
+    for i in range(a.warmup):
+        step(i, "warmup")
+    progress.mark("pre-timing barrier")
     if dist.is_initialized():
         dist.barrier()
     if st.device.type == "cuda":
         torch.cuda.synchronize()
     t1 = time.perf_counter()
     for i in range(a.steps):
-        losses.append(tr.train_step(batches[i % 2]))
+        step(a.warmup + i, "timed")
+    progress.mark("post-timing synchronize")
     if st.device.type == "cuda":
         torch.cuda.synchronize()
     if dist.is_initialized():
         dist.barrier()
     el = time.perf_counter() - t1
+    progress.mark("report")
     el_t = torch.tensor([el], dtype=torch.float64, device=st.device)
     if dist.is_initialized():
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)

@@ -41,6 +41,15 @@ def _pod_ready(pod: dict) -> bool:
     return False
 
 
+
+_LAUNCHER_VARS = frozenset({"RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE",
+                            "ROLE_RANK", "ROLE_NAME", "ROLE_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"})
+
+
+def _launcher_var(name: str) -> bool:
+    """Process-launcher state of the kubelet's own parent (torchrun / the bench), not node state."""
+    return name in _LAUNCHER_VARS or name.startswith(("TORCHELASTIC_", "KFAMD_BENCH_"))
+
 class StatefulSetController(Controller):
     name = "statefulset-controller"
 
@@ -272,7 +281,11 @@ class Kubelet(Controller):
 
     def _start(self, pod: dict, gpu_ids: List[int]):
         ctr = pod["spec"]["containers"][0]
-        env = dict(os.environ)
+        # a container gets the node's base environment, never the rank identity of whatever
+        # launched this kubelet (a kubelet started by rank 0 of a torchrun job would otherwise
+        # hand its RANK / MASTER_PORT / TORCHELASTIC_USE_AGENT_STORE to every pod, whose
+        # rendezvous then waits on the outer job's store)
+        env = {k: v for k, v in os.environ.items() if not _launcher_var(k)}
         env.update(self.extra_env)
         # single-host cluster DNS: a value naming a Service of the pod's namespace
         # (e.g. MASTER_ADDR=<job>-master-0) resolves to this host

@@ -41,6 +41,7 @@ import torch
 import torch.distributed as dist
 
 from .. import ops
+from ..runtime import progress
 from ..runtime.flat import FlatGroup
 
 
@@ -175,6 +176,7 @@ class GradReducer:
         if not self.enabled:
             return
         self._drain_completed()
+        progress.mark("dp collective", f"{'all_to_all' if self.a2a else self.mode} {b.group.name}[{b.idx}]")
         if self.a2a:
             b.recv = torch.empty_like(x)
             b.work = dist.all_to_all_single(b.recv, x, group=self.dp_group, async_op=True)
@@ -226,6 +228,7 @@ class GradReducer:
         for bl in self.buckets.values():
             for b in bl:
                 self._launch(b)
+        progress.mark("dp collective wait", f"{len(self._pending)} buckets")
         for b in self._pending:
             self._complete(b)
         self._pending = []
@@ -241,6 +244,7 @@ class GradReducer:
         if not self.enabled or self.mode != "reduce_scatter":
             return
         r = dist.get_rank(self.dp_group) if self.dp_group is not None else dist.get_rank()
+        progress.mark("zero1 param all_gather")
         # RCCL gathers in place (input = output + rank * n, the NCCL in-place contract): no
         # staging copy of the shard and no transient 1/dp-of-the-model buffer; gloo needs one
         in_place = dist.get_backend(self.dp_group) == "nccl"

@@ -49,6 +49,43 @@ class ParallelState:
 _STATE: Optional[ParallelState] = None
 
 
+def visible_gpu_count() -> int:
+    """GPUs this process may use, counted WITHOUT initialising the HIP runtime, so a launcher
+    can call it before it starts its ranks.  ``KFAMD_VISIBLE_GPUS`` (set by a launcher that
+    already knows, or a test) wins; otherwise torch's amdsmi-based count (no HIP call) and, if
+    amdsmi cannot answer, the KFD topology in sysfs restricted by the ``*_VISIBLE_DEVICES``
+    lists.  Never ``hipGetDeviceCount`` (that creates the HIP runtime in the caller)."""
+    forced = os.environ.get("KFAMD_VISIBLE_GPUS")
+    if forced is not None:
+        return int(forced)
+    if not torch.version.hip:
+        return 0
+    try:
+        n = torch.cuda._device_count_amdsmi()
+    except Exception:       # noqa: BLE001 -- any amdsmi failure falls through to sysfs
+        n = -1
+    if n >= 0:
+        return n
+    root = os.environ.get("KFAMD_KFD_TOPOLOGY", "/sys/class/kfd/kfd/topology/nodes")
+    n = 0
+    try:
+        for node in os.listdir(root):
+            try:
+                with open(os.path.join(root, node, "properties")) as f:
+                    props = dict(line.split()[:2] for line in f if len(line.split()) >= 2)
+            except OSError:
+                continue
+            if int(props.get("simd_count", "0")) > 0:
+                n += 1
+    except OSError:
+        return 0
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip()]))
+    return n
+
+
 def init_distributed(tp: int = 1, pp: int = 1, backend: Optional[str] = None,
                      device: Optional[str] = None, timeout_s: int = 1800) -> ParallelState:
     """Initialise the default process group from torchrun env vars (RANK, WORLD_SIZE,
@@ -64,7 +101,13 @@ def init_distributed(tp: int = 1, pp: int = 1, backend: Optional[str] = None,
         # GPU (RCCL refuses duplicate devices); never for performance numbers
         backend = os.environ.get("KFAMD_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
     if use_gpu:
-        idx = local % max(1, torch.cuda.device_count())
+        ndev = torch.cuda.device_count()
+        if local >= ndev and backend != "gloo":
+            # one rank per GPU: a rank without a GPU of its own must not silently share one
+            # (KFAMD_DIST_BACKEND=gloo is the explicit several-ranks-per-GPU rehearsal)
+            raise RuntimeError(f"LOCAL_RANK {local} but only {ndev} visible GPU(s): one rank per GPU "
+                               f"needs {local + 1}")
+        idx = local % max(1, ndev)
         torch.cuda.set_device(idx)
         dev = torch.device("cuda", idx)
     else:

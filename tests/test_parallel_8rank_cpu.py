@@ -49,6 +49,71 @@ def test_bench_dp8_end_to_end():
     assert rec["value"] > 0 and rec["scaling"] == "weak"
 
 
+# ------------------------------------------------------------------ first contact with an 8-GPU node
+def _cpu_env(**kw):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1", **kw)
+    return env
+
+
+TINY = ["--model", "tiny", "--seq-len", "64", "--micro-batch", "1"]
+
+
+def test_bench_injected_hang_exits_nonzero_with_json_error():
+    """One rank stops making progress (as if it skipped its collectives): every other rank blocks
+    in its next collective; rank 0's watchdog names where it stopped in one JSON line and the
+    run ends non-zero well inside the driver's timeout (no 30-minute process-group wait)."""
+    import time
+    t0 = time.time()
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", *TINY, "--steps", "3",
+                        "--warmup", "1", "--crd-jobs", "0", "--hang-timeout", "15"],
+                       capture_output=True, text=True, timeout=300, env=_cpu_env(KFAMD_BENCH_FAULT="hang:5:2"),
+                       cwd="/tmp")
+    took = time.time() - t0
+    assert r.returncode != 0
+    recs = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(recs) == 1, r.stdout[-2000:]
+    rec = recs[0]
+    assert rec["value"] is None and "no progress" in rec["error"] and rec["rank"] == 0
+    assert rec["stopped_at"]["phase"] in ("dp collective", "dp collective wait", "timed", "zero1 param all_gather",
+                                          "post-timing synchronize"), rec
+    assert "injected hang at step 2" in r.stderr
+    assert took < 120, took
+
+
+def test_bench_refuses_more_gpus_than_visible():
+    """--gpus 2 on a node that shows one GPU: refused in seconds, before any rank starts."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--crd-jobs", "0"],
+                       capture_output=True, text=True, timeout=120, env=dict(_cpu_env(), KFAMD_VISIBLE_GPUS="1"),
+                       cwd="/tmp")
+    assert r.returncode == 2
+    rec = json.loads(r.stdout.strip().splitlines()[-1])
+    assert rec["value"] is None and rec["visible_gpus"] == 1 and "refusing" in rec["error"]
+    assert "torch.distributed.run" not in r.stderr          # no rank was launched
+
+
+@pytest.mark.parametrize("launcher", ["self", "torchrun"])
+def test_bench_crd_jobs_run_at_the_bench_world_size(launcher):
+    """The CRD-to-first-step half at N > 1 submits N-rank PyTorchJobs (nprocPerNode = N, so
+    the N-rank rendezvous is inside the clock).  Under an external torchrun rank 0 measures while
+    the other ranks wait, and the job's pods must not inherit rank 0's launcher identity
+    (RANK / MASTER_PORT / TORCHELASTIC_*), or their rendezvous waits on the outer job's store."""
+    n = 8 if launcher == "self" else 2
+    args = [os.path.join(ROOT, "bench.py"), "--gpus", str(n), *TINY, "--steps", "1", "--warmup", "1",
+            "--crd-jobs", "1", "--crd-timeout", "120"]
+    if launcher == "torchrun":
+        args = ["-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}", "--master-addr", "127.0.0.1",
+                "--master-port", "29937", *args]
+    r = subprocess.run([sys.executable, *args], capture_output=True, text=True, timeout=600, env=_cpu_env(),
+                       cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")][-1]
+    crd = rec["crd_to_first_step"]
+    assert "error" not in crd, crd
+    assert crd["gpus_per_node"] == n and crd["jobs"] == 1 and rec["crd_to_first_step_p50_s"] > 0
+    assert rec["n_gpus"] == n and rec["world_size_seen"] == n
+
+
 # ------------------------------------------------------------------ dp8 ZeRO-1 fp32 reduction
 def _dp_grad_body(rank, world):
     from service_account_auth_improvements_amd.parallel.state import init_distributed
