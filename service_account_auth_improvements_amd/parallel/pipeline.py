@@ -43,7 +43,13 @@ class P2P:
     one xGMI link.  Its tensor is kept alive until :meth:`flush` (end of the step).  Receives
     are waited for (a stream dependency under RCCL) before their data is used.  Every group
     pairs with one posted by the peer in the same order, and a receive is never posted ahead
-    of a send the peer needs first: RCCL runs P2P groups in order on one stream."""
+    of a send the peer needs first: RCCL runs P2P groups in order on one stream.
+
+    Live boundary tensors stay bounded by ``max_inflight`` (= max(2, pp), the 1F1B bound), not by
+    the step's micro-batch x chunk count: after every post, records of groups that have completed
+    are dropped (a completed group needs no wait), and the oldest still-running send-carrying
+    groups beyond the cap are waited for.  A group record keeps only its SEND tensors alive; its
+    receive buffers belong to whoever :meth:`take` s them."""
 
     def __init__(self, st: ParallelState, shape, dtype, device):
         self.st, self.shape, self.dtype, self.device = st, shape, dtype, device
@@ -52,8 +58,11 @@ class P2P:
         # orders its own stream against the compute stream.
         self._host = torch.device(device).type == "cuda" and dist.get_backend() == "gloo"
         self._inflight: list = []       # (works, tensors) of send-only groups not yet waited for
-        self._groups: list = []         # interleaved schedule: (group record, tensors) with sends
+        self._groups: list = []         # interleaved schedule: (group record, send tensors)
         self.sends_deferred = 0         # send-only groups left in flight (tests)
+        self.max_inflight = max(2, st.pp)
+        self.peak_live = 0              # most un-retired send-carrying groups held at once (tests)
+        self._seq = 0
 
     def _buf(self):
         return torch.empty(self.shape, dtype=self.dtype, device=self.device)
@@ -85,8 +94,37 @@ class P2P:
         # waits for ANOTHER message): by the first take() of one of its tensors, else by flush()
         grp = {"works": dist.batch_isend_irecv(ops_), "done": False}
         if sends:
-            self._groups.append((grp, [op.tensor for op in ops_]))
+            self._seq += 1
+            self._groups.append((grp, [op.tensor for op in ops_[:len(sends)]], self._seq))
+            self._retire()
         return [(kind, key, peer, (grp, b)) for kind, key, peer, b in bufs]
+
+    @staticmethod
+    def _completed(works) -> bool:
+        return all(w.is_completed() for w in works)
+
+    def _retire(self):
+        """Drop finished group records; wait for the oldest running ones beyond the cap."""
+        keep = []
+        for rec in self._groups:
+            grp = rec[0]
+            if not grp["done"] and self._completed(grp["works"]):
+                grp["done"] = True           # its receives are complete: take() returns at once
+            if not grp["done"]:
+                keep.append(rec)
+        self._groups = keep
+        self._inflight = [x for x in self._inflight if not self._completed(x[0])]
+        # the cap covers both kinds of record together, oldest post first
+        while len(self._groups) + len(self._inflight) > self.max_inflight:
+            if self._inflight and (not self._groups or self._inflight[0][2] < self._groups[0][2]):
+                for w in self._inflight.pop(0)[0]:
+                    w.wait()
+            else:
+                grp = self._groups.pop(0)[0]
+                for w in grp["works"]:
+                    w.wait()
+                grp["done"] = True
+        self.peak_live = max(self.peak_live, len(self._groups) + len(self._inflight))
 
     @staticmethod
     def take(handle):
@@ -99,11 +137,11 @@ class P2P:
 
     def flush(self):
         """Wait for every deferred send (before the optimizer step reuses any buffer)."""
-        for works, _ in self._inflight:
+        for works, _, _ in self._inflight:
             for w in works:
                 w.wait()
         self._inflight.clear()
-        for grp, _ in self._groups:
+        for grp, _, _ in self._groups:
             if not grp["done"]:
                 for w in grp["works"]:
                     w.wait()
@@ -116,8 +154,10 @@ class P2P:
         if all(op.op is dist.isend for op in ops):
             if self._host:
                 ops = [dist.P2POp(dist.isend, op.tensor.cpu(), op.peer) for op in ops]
-            self._inflight.append((dist.batch_isend_irecv(ops), [op.tensor for op in ops]))
+            self._seq += 1
+            self._inflight.append((dist.batch_isend_irecv(ops), [op.tensor for op in ops], self._seq))
             self.sends_deferred += 1
+            self._retire()
             return
         copies = []
         if self._host:

@@ -17,6 +17,9 @@
 // "namespace-selected"; the dashboard mirrors the iframe's own navigation into its URL.
 (function (root) {
   "use strict";
+  function ownOrigin() {
+    return root.location.origin || new URL(root.location.href).origin;
+  }
   var KF = root.KF, el = KF.el;
   var ALL_NAMESPACES = "All namespaces";
   // apps whose index pages can list every namespace at once (namespace.service.ts)
@@ -115,11 +118,12 @@
         if (frame && frame.contentWindow && ns.current) {
           var n = ns.current.namespace;
           frame.contentWindow.postMessage(n === ALL_NAMESPACES ? { type: "all-namespaces" }
-                                                              : { type: "namespace-selected", value: n }, "*");
+                                                              : { type: "namespace-selected", value: n }, ownOrigin());
         }
       }
       ns.listeners.push(post);
       root.addEventListener("message", function (ev) {
+        if (ev.origin && ev.origin !== ownOrigin()) return;
         if (ev.data && ev.data.type === "iframe-connected") post();
       });
 
@@ -188,18 +192,28 @@
       // iframe-wrapper: the app path without the "/_" prefix, with a trailing "/" (Istio-exported
       // services expect one), and the namespace as ?ns=; the iframe is only reloaded when the
       // browser URL and the iframe's own location differ
+      // (the upstream wrapper prefixes window.location.origin: leading slashes are collapsed and a
+      // src that still resolves to another origin is refused -- "#/_//evil.example/" loads nothing)
       function srcFor(route) {
-        var p = route.path.slice(2) || "/";
+        var p = "/" + (route.path.slice(2) || "/").replace(/^[\s\/\\]+/, "");
         var hashAt = p.indexOf("#"), frag = "";
         if (hashAt >= 0) { frag = p.slice(hashAt); p = p.slice(0, hashAt); }
         if (p[p.length - 1] !== "/" && p.split("/").pop().indexOf(".") < 0) p += "/";
         var q = {};
         Object.keys(route.query).forEach(function (k) { q[k] = route.query[k]; });
         var qs = new URLSearchParams(q).toString();
-        return p + (qs ? "?" + qs : "") + frag;
+        var u;
+        try { u = new URL(p + (qs ? "?" + qs : "") + frag, ownOrigin()); } catch (e) { return null; }
+        return u.origin === ownOrigin() ? u.pathname + u.search + u.hash : null;
       }
       function iframeWrapper(route) {
         var src = srcFor(route);
+        if (src === null) {
+          mode = "refused";
+          outlet.replaceChildren(el("div", { class: "error-page", "data-cy": "refused" }, "Refusing to load ",
+                                    el("b", {}, route.path.slice(2)), ": not a path of this site."));
+          return;
+        }
         if (mode !== "iframe" || !frame) {
           frame = el("iframe", { name: "content", "data-cy": "iframe" });
           frame.addEventListener("load", post);
@@ -213,17 +227,22 @@
       }
       // mirror the iframe's own navigation into the dashboard URL (the wrapper's 100 ms poll)
       function pollFrame() {
-        if (mode === "iframe" && frame && frame.contentWindow && frame.contentWindow.location) {
-          var l = frame.contentWindow.location, now = l.pathname + (l.search || "") + (l.hash || "");
-          if (l.pathname && now !== frameSeen) {
-            frameSeen = now;
-            var q = {};
-            new URLSearchParams(l.search || "").forEach(function (v, k) { q[k] = v; });
-            if (!q.ns && ns.current) q.ns = ns.current.namespace;
-            location.hash = buildHash("/_" + l.pathname + (l.hash || ""), q);
+        try {   // a cross-origin frame throws on .location: skip this tick, keep polling
+          if (mode === "iframe" && frame && frame.contentWindow && frame.contentWindow.location) {
+            var l = frame.contentWindow.location, now = l.pathname + (l.search || "") + (l.hash || "");
+            if (l.pathname && now !== frameSeen) {
+              frameSeen = now;
+              var q = {};
+              new URLSearchParams(l.search || "").forEach(function (v, k) { q[k] = v; });
+              if (!q.ns && ns.current) q.ns = ns.current.namespace;
+              location.hash = buildHash("/_" + l.pathname + (l.hash || ""), q);
+            }
           }
+        } catch (e) {
+          /* SecurityError on a cross-origin document */
+        } finally {
+          root.setTimeout(pollFrame, 100);
         }
-        root.setTimeout(pollFrame, 100);
       }
 
       function navigate() {

@@ -422,98 +422,11 @@
     }
   }
 
-  // ==================================================================== Central dashboard (T2/T3)
-  // Routes (centraldashboard-angular app-routing.module.ts): #/ home, #/_/<app path> the app in
-  // the iframe -- a path holding "{ns}" is resolved to the selected namespace, or, with no
-  // namespace to pick, redirected to #/namespace-needed (guards/iframe.guard.ts) --, #/manage
-  // contributors, anything else the 404 page.  Failed calls go through the error interceptor
-  // (KF.api: "[status] log" snack).
+  // ==================================================================== Central dashboard (T2)
+  // centraldashboard.js (the Polymer main-page / registration / dashboard-view / manage-users
+  // components); failed calls of its shell go through the error interceptor (KF.api snack)
   function dashboard() {
-    var j = function (p, quiet) { return api("GET", p, null, { quiet: quiet }); };
-    Promise.all([j("api/workgroup/env-info"), j("api/workgroup/exists"),
-                 j("api/dashboard-links", true).catch(function () { return { menuLinks: [] }; })]).then(function (r) {
-      var env = r[0], exists = r[1], links = r[2];
-      var nss = (env.namespaces || []).map(function (b) { return b.namespace; });
-      var nsSel = el("select", {}, (env.namespaces || []).map(function (b) {
-        return el("option", { value: b.namespace }, b.namespace + " (" + b.role + ")");
-      }));
-      var frame = el("iframe", { name: "content" });
-      var post = function () {
-        if (frame.contentWindow) frame.contentWindow.postMessage({ type: "namespace-selected", value: nsSel.value }, "*");
-      };
-      nsSel.addEventListener("change", function () { post(); go(); });
-      frame.addEventListener("load", post);
-      window.addEventListener("message", function (ev) {          // library.js protocol
-        if (ev.data && ev.data.type === "iframe-connected") post();
-      });
-      var main = el("div", { class: "dash-main" });
-      var nav = el("nav", {}, el("a", { href: "#/" }, "Home"),
-        (links.menuLinks || []).map(function (l) { return el("a", { href: "#/_" + l.link }, l.text); }),
-        el("a", { href: "#/manage" }, "Manage contributors"));
-      root.append(header("Kubeflow on MI355X", [nsSel, el("span", {}, env.user || "")]), el("div", { class: "dash" }, nav, main));
-      if (!exists.hasWorkgroup && exists.registrationFlowAllowed && exists.hasAuth) {
-        var inp = el("input", { value: exists.user });
-        main.replaceChildren(el("div", { class: "card" }, el("h2", {}, "Create your namespace"), inp,
-          el("button", { onclick: function () {
-            api("POST", "api/workgroup/create", { namespace: inp.value }).then(function () { location.reload(); });
-          } }, "Finish")));
-        return;
-      }
-      function go() {
-        var h = (location.hash || "#/").slice(1) || "/";
-        if (h === "/" || h === "") return home();
-        if (h === "/manage") return manage();
-        if (h.indexOf("/namespace-needed") === 0) return namespaceNeeded();
-        if (h.indexOf("/_/") === 0) {
-          var path = decodeURIComponent(h.slice(2));
-          if (path.indexOf("{ns}") >= 0) {
-            if (!nss.length) { location.hash = "#/namespace-needed?path=" + encodeURIComponent(path); return; }
-            path = path.split("{ns}").join(nsSel.value);
-          }
-          frame.src = path;
-          return main.replaceChildren(frame);
-        }
-        main.replaceChildren(el("div", { class: "error-page", "data-cy": "not-found" }, el("div", { class: "headline" }, "404"),
-          el("div", {}, "Sorry, ", el("b", {}, h), " is not a valid page."), el("a", { href: "#/" }, "back to home")));
-      }
-      function namespaceNeeded() {
-        main.replaceChildren(el("div", { class: "error-page", "data-cy": "namespace-needed" },
-          el("div", {}, "This page requires a namespace to be selected but no namespaces are currently available."),
-          el("a", { href: "#/" }, "back to home")));
-      }
-      function home() {
-        var ns = nsSel.value;
-        Promise.all([j("api/activities/" + ns, true).catch(function () { return []; }),
-                     j("api/metrics/node?interval=Last15m", true).catch(function () { return []; })]).then(function (r2) {
-          var acts = r2[0] || [], pts = Array.isArray(r2[1]) ? r2[1] : [];
-          main.replaceChildren(el("div", { style: "padding:16px" }, el("h2", {}, "Recent activity in " + ns),
-            KF.table([["Time", function (e) { return KF.dateTime(e.lastTimestamp || e.eventTime); }], ["Type", function (e) { return e.type; }],
-                      ["Object", function (e) { return (e.involvedObject || {}).kind + "/" + (e.involvedObject || {}).name; }],
-                      ["Message", function (e) { return e.message; }]], (Array.isArray(acts) ? acts : []).slice(0, 20),
-                     { empty: "No recent activity." }),
-            el("h2", {}, "Node CPU utilisation (15 min)"),
-            KF.table([["Time", function (p) { return new Date(p.timestamp * 1000).toLocaleTimeString(); }],
-                      ["Node", function (p) { return p.label; }], ["Value", function (p) { return (100 * p.value).toFixed(1) + " %"; }]],
-                     pts.slice(-20), { empty: "No metrics service configured." })));
-        });
-      }
-      function manage() {
-        var ns = nsSel.value;
-        j("api/workgroup/get-contributors/" + ns).catch(function () { return []; }).then(function (users) {
-          var who = el("input", { placeholder: "user@example.com" });
-          var call = function (m) {
-            return api(m, "api/workgroup/" + (m === "POST" ? "add" : "remove") + "-contributor/" + ns, { contributor: who.value })
-              .catch(function () {}).then(manage);
-          };
-          main.replaceChildren(el("div", { class: "card" }, el("h2", {}, "Contributors of " + ns),
-            el("ul", {}, users.map(function (u) { return el("li", {}, u); })), who,
-            el("button", { onclick: function () { call("POST"); } }, "Add"),
-            el("button", { onclick: function () { call("DELETE"); } }, "Remove")));
-        });
-      }
-      window.addEventListener("hashchange", go);
-      go();
-    });
+    self.CD.start(root).catch(function () {});
   }
 
   var apps = { jupyter: jupyter, volumes: volumes, tensorboards: tensorboards, dashboard: dashboard };

@@ -225,7 +225,8 @@
       window.addEventListener("message", function (ev) {        // central dashboard iframe protocol
         if (ev.data && ev.data.type === "namespace-selected") { sel.value = ev.data.value; onChange(sel.value); }
       });
-      if (window.parent !== window) window.parent.postMessage({ type: "iframe-connected" }, "*");
+      // the dashboard and the apps share one origin (behind the gateway): never post elsewhere
+      if (window.parent !== window) window.parent.postMessage({ type: "iframe-connected" }, location.origin || new URL(location.href).origin);
       return sel;
     });
   }

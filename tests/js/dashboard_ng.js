@@ -83,6 +83,19 @@ Promise.resolve()
         return env.go("#/no-such-page");
       }).then(function () {
         out.notFound = { page: !!env.q('[data-cy="not-found"]'), text: env.q('[data-cy="not-found"]').textContent };
+        // a protocol-relative app path stays on this origin; a cross-origin frame (its location
+        // throws SecurityError) does not stop the URL-mirroring poll
+        return env.go("#/_//evil.example/steal?ns=team-b");
+      }).then(function () {
+        var frame = env.q('[data-cy="iframe"]');
+        out.hostile = { src: frame && frame.src, refused: !!env.q('[data-cy="refused"]') };
+        frame.contentWindow = { postMessage: function () {} };
+        Object.defineProperty(frame.contentWindow, "location", { get: function () { throw new Error("SecurityError"); } });
+        var polls = function () { return env.timers.filter(function (t) { return t.ms === 100; }).length; };
+        var before = polls();
+        return env.tick().then(function () { return env.tick(); }).then(function () {
+          out.pollAlive = { before: before, after: polls() };
+        });
       });
     });
   })

@@ -197,6 +197,7 @@ function makeEnv(opts) {
   document.head = head;
   document.cookie = "XSRF-TOKEN=tok123";
   document.createElement = function (t) { return new Element_(t); };
+  document.createElementNS = function (ns, t) { var e = new Element_(t); e.namespaceURI = ns; return e; };
   document.createTextNode = function (t) { return new Text_(t); };
   document.getElementById = function (id) { return selectAll(document, "#" + id)[0] || null; };
   var baseHref = opts.base || "http://localhost/app/";
@@ -207,7 +208,8 @@ function makeEnv(opts) {
   var realQS = document.querySelector.bind(document);
   document.querySelector = function (s) { return s === "base" ? { href: baseHref } : realQS(s); };
   var loc = { _hash: opts.hash || "", search: opts.search || "", pathname: "/app/", href: baseHref,
-              reloaded: 0, reload: function () { this.reloaded++; } };
+              reloaded: 0, reload: function () { this.reloaded++; },
+              replaced: [], replace: function (u) { this.replaced.push(u); } };
   Object.defineProperty(loc, "hash", {
     get: function () { return this._hash; },
     set: function (v) {
@@ -227,10 +229,10 @@ function makeEnv(opts) {
   };
   window.parent = opts.inIframe ? { postMessage: function (d) { posted.push(d); } } : window;
   window.self = window;
-  function respond(method, url, body) {
+  function respond(method, url, body, headers) {
     var u = new URL(url);
     var path = u.pathname.replace(/^\/app\//, "").replace(/^\//, "") + u.search;
-    requests.push({ method: method, path: path, body: body === undefined ? undefined : JSON.parse(body) });
+    requests.push({ method: method, path: path, body: body === undefined ? undefined : JSON.parse(body), headers: headers || {} });
     var key = method + " " + path, h = routes[key] !== undefined ? routes[key] : routes[method + " " + path.split("?")[0]];
     if (typeof h === "function") h = h(body === undefined ? undefined : JSON.parse(body), path);
     if (h === undefined) h = { status: 404, body: { success: false, status: 404, log: "not found: " + key } };
@@ -253,7 +255,7 @@ function makeEnv(opts) {
                     setItem: function (k, v) { lstore[k] = String(v); },
                     removeItem: function (k) { delete lstore[k]; } },
     navigator: { clipboard: { writeText: function () { return Promise.resolve(); } } },
-    fetch: function (url, init) { init = init || {}; return respond(init.method || "GET", String(url), init.body); },
+    fetch: function (url, init) { init = init || {}; return respond(init.method || "GET", String(url), init.body, init.headers); },
     setTimeout: function (f, ms) { timers.push({ f: f, ms: ms }); return timers.length; },
     clearTimeout: function () {},
     confirm: function () { throw new Error("window.confirm used: pages must use KF.confirmDialog"); },

@@ -1,5 +1,6 @@
 // Renders the web apps' pages (static/kfamd-ui.js on lib/kf-common.js + lib/kf-logic.js) in
 // the DOM shim against fixture responses shaped like the reference frontends' Cypress fixtures
+// (the central dashboard has its own driver: centraldashboard.js)
 // (crud-web-apps/jupyter/frontend/cypress/fixtures), drives them like a user, and prints one
 // JSON object of observations for tests/test_ui.py.   usage: node ui_pages.js CONFIG_JSON
 "use strict";
@@ -202,35 +203,6 @@ Promise.resolve()
     env.qa("button").filter(function (b) { return b.textContent === "+ New TensorBoard"; })[0].click();
     return shim.flush().then(function () {
       out.twa = { posts: env.requests.filter(function (r) { return r.method === "POST"; }).map(function (r) { return r.body; }) };
-    });
-  })
-  // ---------------------------------------------------------------- dashboard: guard, 404, interceptor
-  .then(function () {
-    var dash = function (nss) {
-      return { "GET api/workgroup/env-info": { user: "alice@example.com", namespaces: nss, platform: {} },
-               "GET api/workgroup/exists": { hasWorkgroup: nss.length > 0, hasAuth: true, registrationFlowAllowed: false, user: "alice@example.com" },
-               "GET api/dashboard-links": { menuLinks: [{ text: "Notebooks", link: "/jupyter/" },
-                                                       { text: "Pipelines", link: "/pipeline/#/pipelines?ns={ns}" }] },
-               "GET api/activities/kubeflow-user": [], "GET api/metrics/node": [],
-               "GET api/workgroup/get-contributors/kubeflow-user": { status: 500, body: { error: "KFAM is down" } } };
-    };
-    return boot("dashboard", dash([{ namespace: "kubeflow-user", role: "owner" }])).then(function (env) {
-      var o = out.dash = { navLinks: env.qa("nav a").map(function (a) { return a.href; }) };
-      return env.go("#/_/pipeline/#/pipelines?ns={ns}").then(function () {
-        o.iframeSrc = (env.q("iframe") || {}).src;
-        return env.go("#/no/such/page");
-      }).then(function () {
-        o.notFound = env.text('[data-cy="not-found"]');
-        return env.go("#/manage");
-      }).then(function () {
-        o.snacks = env.snacks();
-        return boot("dashboard", dash([]), { hash: "#/_/pipeline/?ns={ns}" });
-      }).then(function (env2) {
-        return shim.flush().then(function () {
-          o.noNamespaceHash = env2.window.location.hash;
-          o.namespaceNeeded = env2.text('[data-cy="namespace-needed"]');
-        });
-      });
     });
   })
   .then(function () { process.stdout.write(JSON.stringify(out)); },

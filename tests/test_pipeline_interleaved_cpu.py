@@ -68,7 +68,8 @@ def _body(rank, world, pp, v, n_micro, dp_steps, tp=1):
     params = {s.name: tr.model.P(s.name).float().clone() for g in tr.model.groups for s in g.specs}
     names = sorted(g.name for g in tr.model.groups)
     return dict(losses=losses, params=params, coords=(st.dp_rank, st.pp_rank), dp=st.dp, groups=names,
-                deferred=tr.p2p.sends_deferred, tp_rank=st.tp_rank)
+                deferred=tr.p2p.sends_deferred, tp_rank=st.tp_rank, peak_live=tr.p2p.peak_live,
+                max_inflight=tr.p2p.max_inflight, left=len(tr.p2p._groups) + len(tr.p2p._inflight))
 
 
 def _reference(n_layers, n_batches_per_step):
@@ -82,8 +83,8 @@ def _reference(n_layers, n_batches_per_step):
 
 
 @pytest.mark.parametrize("world,pp,v,n_micro,tp", [(2, 2, 2, 2, 1), (2, 2, 2, 4, 1), (4, 4, 2, 4, 1), (4, 2, 2, 2, 1),
-                                                   (4, 2, 2, 2, 2)],
-                         ids=["pp2v2m2", "pp2v2m4", "pp4v2m4", "dp2xpp2v2-zero1", "tp2xpp2v2"])
+                                                   (4, 2, 2, 2, 2), (2, 2, 2, 8, 1)],
+                         ids=["pp2v2m2", "pp2v2m4", "pp4v2m4", "dp2xpp2v2-zero1", "tp2xpp2v2", "pp2v2m8"])
 def test_interleaved_training_matches_single_process(world, pp, v, n_micro, tp):
     from service_account_auth_improvements_amd.models.llama import Llama
     from service_account_auth_improvements_amd.parallel.state import ParallelState
@@ -94,6 +95,10 @@ def test_interleaved_training_matches_single_process(world, pp, v, n_micro, tp):
     for r in res:
         assert r["groups"] == sorted(f"{n}.v{c}" for n in ("matrices", "norms") for c in range(v))
         assert r["deferred"] > 0
+        # boundary tensors kept alive by posted sends stay at the 1F1B bound (max(2, pp)) mid-step,
+        # not 2 * M * v, and nothing is left over after the step's flush
+        assert r["peak_live"] <= r["max_inflight"] == max(2, pp), (r["peak_live"], r["max_inflight"])
+        assert r["left"] == 0
     for step in range(STEPS):
         per_replica = {r["coords"][0]: r["losses"][step] for r in res if r["coords"][1] == pp - 1}
         assert len(per_replica) == dp and all(x is not None for x in per_replica.values())

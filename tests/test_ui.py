@@ -224,14 +224,89 @@ def test_twa_form_posts_the_tensorboard(pages):
                                       "configurations": ["access-ml-pipeline"]}]
 
 
-def test_dashboard_routes_guard_and_404(pages):
-    d = pages["dash"]
-    assert d["navLinks"] == ["#/", "#/_/jupyter/", "#/_/pipeline/#/pipelines?ns={ns}", "#/manage"]
-    assert d["iframeSrc"] == "/pipeline/#/pipelines?ns=kubeflow-user"        # {ns} resolved (iframe guard)
-    assert d["notFound"].startswith("404Sorry, /no/such/page is not a valid page.")
-    assert d["noNamespaceHash"].startswith("#/namespace-needed?path=")        # no namespace: redirected
-    assert d["namespaceNeeded"].startswith("This page requires a namespace to be selected")
-    assert d["snacks"][0][0] == "ERROR" and d["snacks"][0][1].startswith("[500] KFAM is down")
+# ------------------------------------------------------------------ central dashboard (T2)
+# tests/js/centraldashboard.js drives static/centraldashboard.js like the reference's
+# centraldashboard/public/components/*_test.js drive the Polymer components.
+@pytest.fixture(scope="module")
+def cd():
+    r = subprocess.run(["node", os.path.join(ROOT, "tests", "js", "centraldashboard.js")], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    return json.loads(r.stdout)
+
+
+def test_cd_registration_validates_and_surfaces_backend_errors(cd):
+    """registration-page_test.js: the default name from the user id, validateNamespace's message
+    (no request sent), the backend's error in the form, then exists polled until the workgroup
+    appears and the app reloads."""
+    r = cd["registration"]
+    assert r["welcome"] and r["nsPageHidden"]
+    assert r["defaultName"] == "alice-smith-example-com"
+    assert r["invalidError"].startswith("Name can only start and end with alpha-num characters")
+    assert r["postsAfterInvalid"] == 0
+    assert r["backendError"] == "namespace alice already exists"
+    assert r["createBodies"] == [{"namespace": "alice"}, {"namespace": "alice"}]
+    assert r["existsPolls"] == 3 and r["reloaded"] == 1
+
+
+def test_cd_navigation_iframe_guard_and_logout(cd):
+    h = cd["home"]
+    nav = dict(h["nav"])
+    assert nav["Notebooks"] == "#/_/jupyter/?ns=kubeflow-user" and nav["Manage Contributors"] == "#/manage-users"
+    assert nav["Grafana"] == "https://grafana.example/"
+    assert h["quick"] == ["#/_/jupyter/new?ns=kubeflow-user"] and h["docs"] == ["https://www.kubeflow.org/docs/"]
+    assert h["iframeSrc"] == "/jupyter/?ns=kubeflow-user"
+    # namespace messages go to the dashboard's own origin only, and the choice is stored per user
+    assert h["messages"] == [[{"type": "namespace-selected", "value": "team-b"}, "http://localhost"]]
+    assert h["stored"] == "team-b"
+    # a protocol-relative or backslash path from the URL hash stays on this origin
+    assert h["hostile"]["iframe"] and h["hostileSrc"] == "/evil.example/steal"
+    assert h["hostile2"]["iframe"] and h["hostile2Src"] == "/evil.example/x"
+    assert h["notFound"].startswith("404Sorry, /no/such/page is not a valid page.")
+    assert h["activity"][:2] and "Created pod nb1-0" in h["activity"]
+    assert h["logout"] == {"method": "POST", "auth": "Bearer sess42", "replaced": ["/dex/auth?loggedout=1"]}
+
+
+def test_cd_resource_charts_from_metrics(cd):
+    """resource-chart_test.js: series per label, the 5 highest means when more (title "(Top 5)"),
+    a % axis for CPU, the interval menu re-queries."""
+    c = {x["metric"]: x for x in cd["home"]["charts"]}
+    assert c["node"]["title"] == "Cluster CPU Utilization (Top 5)" and c["node"]["lines"] == 5
+    assert c["node"]["legend"] == ["n7", "n6", "n5", "n4", "n3"]
+    assert c["podcpu"]["title"] == "Pod CPU Utilization" and c["podcpu"]["legend"] == ["kubeflow-user", "team-b"]
+    assert c["node"]["ymax"].endswith("%") and c["node"]["link"] == "https://grafana.example/d/cluster"
+    assert cd["home"]["metricRequests"] == ["api/metrics/node?interval=Last60m", "api/metrics/podcpu?interval=Last60m"]
+    assert cd["home"]["intervalRequest"] == "api/metrics/node?interval=Last5m"
+    assert cd["noNs"]["charts"] == 0           # /api/metrics 405: no charts
+
+
+def test_cd_notebooks_and_pipelines_cards(cd):
+    h = cd["home"]
+    assert [n[0] for n in h["notebooks"]] == ["d.ipynb", "b.ipynb", "f.ipynb", "c.ipynb", "a.ipynb"]   # newest 5
+    assert h["notebooks"][0][1] == "#/_/notebook/kubeflow-user/nb2/notebooks/d.ipynb"
+    assert h["pipelines"][0] == ["train-llama", "#/_/pipeline/?ns=kubeflow-user#/pipelines/details/p1"]
+    assert h["runs"] == [["run-ok", "success"], ["run-bad", "error"], ["run-now", "pending"]]
+    assert "resource_reference_key.id=kubeflow-user" in h["runsQuery"][0]
+    assert cd["noNs"]["notebooksMsg"] == "Choose a namespace to see Notebooks"
+    assert cd["pipelinesError"] == "Error retrieving Pipeline Runs"
+    assert cd["noNs"]["hash"] == "#/namespace-needed" and cd["noNs"]["page"].startswith("This page requires a namespace")
+
+
+def test_cd_manage_contributors_surfaces_every_failure(cd):
+    """manage-users-view(-contributor)_test.js: account info, the role table, the cluster-admin
+    overview, chips per contributor; add / remove update the chips, a failed add or remove shows
+    the backend error under the field, a failed fetch shows a toast."""
+    m = cd["manage"]
+    assert m["account"].endswith("alice@example.com (Cluster Admin)")
+    assert m["roles"][1:] == ["Ownerkubeflow-user", "Contributorteam-b", "Viewerteam-c"]
+    assert m["overview"][1] == "kubeflow-useralice@example.combob@example.com"
+    assert m["sections"] == ["kubeflow-user"] and m["chips0"] == ["bob@example.com"]
+    assert m["afterAdd"] == {"chips": ["bob@example.com", "carol@example.com"], "input": "", "error": ""}
+    assert m["badAdd"]["error"] == "Contributor doesn't look like a valid email address"
+    assert m["badAdd"]["chips"] == ["bob@example.com", "carol@example.com"] and m["badAdd"]["input"] == "not-an-email"
+    assert m["afterRemove"] == {"chips": ["carol@example.com"], "error": ""}
+    assert cd["removeError"] == {"error": "Unable to remove contributor", "chips": ["dave@example.com"]}
+    assert cd["fetchError"] == [["ERROR", "Failed to fetch contributor list for kubeflow-user, because: KFAM is down"]]
 
 
 # ------------------------------------------------------------------ second dashboard frontend (T3)
@@ -280,4 +355,8 @@ def test_ng_guard_404_and_error_interceptor(ng):
     assert ng["guard"]["page"] and ng["guard"]["hash"].startswith("#/namespace-needed?path=")
     assert ng["noNs"]["page"] and ng["noNs"]["after"].startswith("#/namespace-needed")
     assert ng["notFound"]["page"] and "/no-such-page" in ng["notFound"]["text"]
+    # "#/_//evil.example/..." loads a path of this origin, never the other host; a frame whose
+    # location throws (cross-origin) does not stop the URL-mirroring poll
+    assert ng["hostile"] == {"src": "/evil.example/steal/?ns=team-b", "refused": False}
+    assert ng["pollAlive"]["before"] >= 1 and ng["pollAlive"]["after"] >= 1
     assert ng["error"] == [["ERROR", "[500] kfam unreachable\nhttp://localhost/app/api/workgroup/env-info"]]
