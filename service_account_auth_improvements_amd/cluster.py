@@ -89,10 +89,11 @@ def add_platform_controllers(m: Manager, c, registry, labels_path: str = DEFAULT
 
 
 def register_admission(server: APIServer):
-    """The admission webhooks (PodDefault mutator, PVCViewer defaulter / validator), called
-    in-process by the API server."""
+    """The admission webhooks (PodDefault mutator, PVCViewer defaulter / validator, the
+    PyTorchJob / MPIJob validator), called in-process by the API server."""
     poddefault.register(server, InMemoryClient(server))
     pvcviewer.register(server)
+    training.register(server)
 
 
 class LocalCluster:

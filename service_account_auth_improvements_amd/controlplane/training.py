@@ -10,16 +10,31 @@ mpi-operator shapes, MI355X-native in what they put into pods:
   ``PET_*`` torchrun variables consumed by the launcher, plus ``HSA_ENABLE_IPC_MODE_LEGACY=0``
   for RCCL's dmabuf IPC.  ``HIP_VISIBLE_DEVICES`` is set by the node's device plugin from
   the ``amd.com/gpu`` allocation -- no ``CUDA_VISIBLE_DEVICES`` / NVIDIA assumptions;
-* status: ``Created`` / ``Running`` / ``Restarting`` / ``Succeeded`` / ``Failed``
-  conditions, ``replicaStatuses``, ``startTime`` / ``completionTime``; ``runPolicy``
-  ``backoffLimit`` (pod restarts for ``OnFailure`` / ``ExitCode``) and ``cleanPodPolicy``.
+* status: ``Created`` / ``Running`` / ``Restarting`` / ``Suspended`` / ``Succeeded`` /
+  ``Failed`` conditions, ``replicaStatuses``, ``startTime`` / ``completionTime``.
+* ``runPolicy`` (kubeflow.org/v1 RunPolicy): ``backoffLimit`` (pod restarts for ``OnFailure``
+  / ``ExitCode``), ``cleanPodPolicy``, ``activeDeadlineSeconds`` (counted from ``startTime``;
+  past it the job is Failed with reason ``DeadlineExceeded`` and its running pods are
+  deleted -- a deadline that left them running would not bound anything), ``ttlSecondsAfter
+  Finished`` (the finished job is deleted, its pods and services with it through owner
+  references) and ``suspend`` (pods and services deleted, job kept with ``Suspended``;
+  un-suspending recreates them with a fresh ``startTime``).  ``schedulingPolicy`` needs a gang
+  scheduler this platform does not run and is rejected at admission (:func:`validate_job`),
+  as is anything else the operator would otherwise silently ignore.
+* PyTorchJob ``elasticPolicy``: ``minReplicas`` / ``maxReplicas`` / ``maxRestarts`` /
+  ``rdzv*`` become the launcher's elastic rendezvous (``PET_NNODES=MIN:MAX``,
+  ``PET_RDZV_ENDPOINT``, ``PET_MAX_RESTARTS``): when a node is lost the survivors restart and
+  re-form the group at the smaller world size while at least ``minReplicas`` Workers remain;
+  the job fails only below that.  HPA ``metrics`` are rejected at admission.
 """
 from __future__ import annotations
 
 import copy
+import datetime as _dt
 import logging
 import os
 import sys
+import time
 from typing import Dict, List, Optional
 
 from .apiserver import ApiError, now_rfc3339, set_controller_reference
@@ -49,23 +64,112 @@ def _cond(ctype, reason, msg):
 
 
 def _set_condition(status: dict, ctype: str, reason: str, msg: str):
+    """Set condition ``ctype`` True (one entry per type, updated in place).  Running /
+    Restarting / Suspended exclude each other and end at a terminal condition."""
     conds = status.setdefault("conditions", [])
     for c in conds:
         if c["type"] == ctype and c.get("status") == "True":
             return
-    # Running / Restarting are mutually exclusive and end at a terminal condition
+    exclusive = {"Succeeded": ("Running", "Restarting"), "Failed": ("Running", "Restarting"),
+                 "Running": ("Restarting",), "Restarting": ("Running",), "Suspended": ("Running", "Restarting")}
+    t = now_rfc3339()
     for c in conds:
-        if ctype in ("Succeeded", "Failed") and c["type"] in ("Running", "Restarting"):
-            c["status"] = "False"
-        if ctype == "Running" and c["type"] == "Restarting":
-            c["status"] = "False"
-        if ctype == "Restarting" and c["type"] == "Running":
-            c["status"] = "False"
+        if c["type"] in exclusive.get(ctype, ()) and c.get("status") == "True":
+            c.update(status="False", lastUpdateTime=t, lastTransitionTime=t)
+    for c in conds:
+        if c["type"] == ctype:
+            c.update(_cond(ctype, reason, msg))
+            return
     conds.append(_cond(ctype, reason, msg))
 
 
 def _has(status: dict, ctype: str) -> bool:
     return any(c["type"] == ctype and c.get("status") == "True" for c in status.get("conditions") or [])
+
+
+def _parse_time(s: Optional[str]) -> Optional[float]:
+    if not s:
+        return None
+    try:
+        return _dt.datetime.fromisoformat(s.replace("Z", "+00:00")).timestamp()
+    except ValueError:
+        return None
+
+
+def _elastic(job: dict) -> Optional[dict]:
+    return job.get("spec", {}).get("elasticPolicy") if job.get("kind") == "PyTorchJob" else None
+
+
+def _elastic_bounds(job: dict) -> tuple:
+    """(minReplicas, maxReplicas) of an elastic PyTorchJob; both default to the Worker count."""
+    ep = _elastic(job) or {}
+    w = int(((job["spec"].get("pytorchReplicaSpecs") or {}).get("Worker") or {}).get("replicas", 1))
+    mx = int(ep.get("maxReplicas") or w)
+    return int(ep.get("minReplicas") or min(w, mx)), mx
+
+
+def validate_job(job: dict) -> Optional[str]:
+    """Admission check for PyTorchJob / MPIJob specs: what the operator cannot honour is refused
+    here instead of being accepted and ignored (the training-operator validation webhook plus
+    this platform's limits).  Returns the denial message, or None."""
+    kind = job.get("kind")
+    spec = job.get("spec") or {}
+    key = "pytorchReplicaSpecs" if kind == "PyTorchJob" else "mpiReplicaSpecs"
+    specs = spec.get(key) or {}
+    if not specs:
+        return f"{kind} needs spec.{key}"
+    allowed = ("Master", "Worker") if kind == "PyTorchJob" else ("Launcher", "Worker")
+    for rtype, rs in specs.items():
+        if rtype not in allowed:
+            return f"{kind} replica type {rtype!r} is not one of {', '.join(allowed)}"
+        if not ((rs.get("template") or {}).get("spec") or {}).get("containers"):
+            return f"{kind} {rtype} template needs at least one container"
+    if kind == "PyTorchJob" and int((specs.get("Master") or {}).get("replicas", 1)) > 1:
+        return "PyTorchJob Master replicas must be 1"
+    if kind == "MPIJob" and int((specs.get("Launcher") or {}).get("replicas", 1)) != 1:
+        return "MPIJob Launcher replicas must be 1"
+    rp = spec.get("runPolicy") or {}
+    if rp.get("schedulingPolicy"):
+        return ("runPolicy.schedulingPolicy needs a gang scheduler (volcano / scheduler-plugins), which this "
+                "platform does not run; remove it (pods are scheduled individually)")
+    ep = spec.get("elasticPolicy")
+    if ep is not None:
+        if kind != "PyTorchJob":
+            return "elasticPolicy is a PyTorchJob field"
+        if ep.get("metrics"):
+            return "elasticPolicy.metrics (HPA autoscaling of Workers) is not supported"
+        if (ep.get("rdzvBackend") or "c10d") != "c10d":
+            return f"elasticPolicy.rdzvBackend {ep.get('rdzvBackend')!r} is not supported (c10d only)"
+        if "Master" in specs:
+            return "an elastic PyTorchJob runs Worker replicas only (no Master)"
+        if "Worker" not in specs:
+            return "an elastic PyTorchJob needs Worker replicas"
+        mn, mx = _elastic_bounds(job)
+        w = int(specs["Worker"].get("replicas", 1))
+        if mn > mx:
+            return f"elasticPolicy.minReplicas {mn} > maxReplicas {mx}"
+        if not mn <= w <= mx:
+            return f"Worker replicas {w} outside elasticPolicy [{mn}, {mx}]"
+    return None
+
+
+def admission_review(request: dict) -> dict:
+    """Validating webhook body (``/validate-kubeflow-org-v1-pytorchjob`` / ``-v2beta1-mpijob``)."""
+    if request.get("operation") == "DELETE":
+        return {"uid": request.get("uid"), "allowed": True}
+    err = validate_job(request.get("object") or {})
+    if err:
+        return {"uid": request.get("uid"), "allowed": False,
+                "status": {"code": 422, "reason": "Invalid", "message": err}}
+    return {"uid": request.get("uid"), "allowed": True}
+
+
+def register(server):
+    from .apiserver import Webhook
+    server.add_validating_webhook(Webhook("validator.pytorchjob.training-operator.kubeflow.org", "kubeflow.org",
+                                          "PyTorchJob", ("CREATE", "UPDATE"), admission_review))
+    server.add_validating_webhook(Webhook("validator.mpijob.training-operator.kubeflow.org", "kubeflow.org",
+                                          "MPIJob", ("CREATE", "UPDATE"), admission_review))
 
 
 def _gpus(tpl: dict) -> int:
@@ -135,6 +239,17 @@ class _JobBase(Controller):
         return int((job.get("metadata", {}).get("annotations") or {}).get("kfamd.io/master-port", DEFAULT_PORT))
 
     # --- reconcile
+    def _delete_pods_and_services(self, pods: dict, ns: str, phases=None):
+        c = self.client
+        for p in pods.values():
+            if phases is not None and p.get("status", {}).get("phase") not in phases:
+                continue
+            for kind in ("Pod", "Service"):
+                try:
+                    c.delete("v1", kind, p["metadata"]["name"], ns)
+                except ApiError:
+                    pass
+
     def reconcile(self, req: Request) -> Result:
         c = self.client
         job = c.get_or_none(self.api, self.kind, req.name, req.namespace)
@@ -142,12 +257,42 @@ class _JobBase(Controller):
             return Result()
         status = copy.deepcopy(job.get("status") or {})
         run_policy = job["spec"].get("runPolicy") or {}
+        now = time.time()
+        requeue = 0.0
         if not _has(status, "Created"):
             _set_condition(status, "Created", f"{self.kind}Created",
                            f'{self.kind} {req.name} is created.')
         terminal = _has(status, "Succeeded") or _has(status, "Failed")
+        # runPolicy.ttlSecondsAfterFinished: the finished job goes (pods / services follow it
+        # through their owner references)
+        if terminal and run_policy.get("ttlSecondsAfterFinished") is not None:
+            done_at = _parse_time(status.get("completionTime"))
+            if done_at is not None:
+                left = done_at + int(run_policy["ttlSecondsAfterFinished"]) - now
+                if left <= 0:
+                    try:
+                        c.delete(self.api, self.kind, req.name, req.namespace)
+                    except ApiError:
+                        pass
+                    return Result()
+                requeue = left
         pods = {p["metadata"]["name"]: p for p in c.list("v1", "Pod", req.namespace,
                                                          label_selector=f"{LBL_JOB}={req.name}")}
+        # runPolicy.suspend: no pods while suspended; resuming starts the clock again
+        if run_policy.get("suspend") and not terminal:
+            self._delete_pods_and_services(pods, req.namespace)
+            if not _has(status, "Suspended"):
+                _set_condition(status, "Suspended", f"{self.kind}Suspended", f"{self.kind} {req.name} is suspended.")
+            status.pop("startTime", None)
+            status["replicaStatuses"] = {rt: {"active": 0, "succeeded": 0, "failed": 0}
+                                         for rt in (job["spec"].get(self.specs_key) or {})}
+            self._write_status(job, status)
+            return Result()
+        if _has(status, "Suspended"):
+            for cd in status["conditions"]:
+                if cd["type"] == "Suspended" and cd.get("status") == "True":
+                    cd.update(status="False", reason=f"{self.kind}Resumed", message=f"{self.kind} {req.name} is resumed.",
+                              lastUpdateTime=now_rfc3339(), lastTransitionTime=now_rfc3339())
         desired = self._desired_pods(job)
         if not terminal:
             for pod in desired:
@@ -156,9 +301,11 @@ class _JobBase(Controller):
                     pods[pn] = c.create(pod)
                 if c.get_or_none("v1", "Service", pn, req.namespace) is None and self._wants_service(pod):
                     c.create(self._service(job, pod))
+            status.setdefault("startTime", now_rfc3339())
         # replica statuses
         rstat: Dict[str, dict] = {}
         restarts = int(status.get("restartCount", 0))
+        per_type = dict(status.get("replicaRestarts") or {})
         backoff = run_policy.get("backoffLimit")
         failed_msg = None
         specs = job["spec"].get(self.specs_key) or {}
@@ -174,33 +321,54 @@ class _JobBase(Controller):
                 code = self._exit_code(live)
                 retryable = policy == "OnFailure" or (policy == "ExitCode" and code is not None and code >= 128)
                 limit = self._backoff_limit(rtype, backoff)
-                if retryable and not terminal and (limit is None or restarts < int(limit)):
+                used = self._restarts_used(rtype, restarts, per_type)
+                if retryable and not terminal and (limit is None or used < int(limit)):
                     restarts += 1
+                    per_type[rtype] = per_type.get(rtype, 0) + 1
                     c.delete("v1", "Pod", live["metadata"]["name"], req.namespace)
                     _set_condition(status, "Restarting", f"{self.kind}Restarting",
                                    f'{self.kind} {req.name} is restarting because {rtype} replica(s) failed.')
                     rs["active"] += 1
                 else:
                     rs["failed"] += 1
-                    msg = self._failure_message(req.name, rtype, live)
+                    msg = self._failure_message(job, rtype, live)
                     if msg:
                         failed_msg = msg
             elif phase in ("Running", "Pending", None) and live is not None:
                 rs["active"] += 1
         status["replicaStatuses"] = rstat
         status["restartCount"] = restarts
+        if per_type:
+            status["replicaRestarts"] = per_type
         if not terminal:
-            if failed_msg:
+            failed_msg = failed_msg or self._job_failure(job, rstat)
+            # runPolicy.activeDeadlineSeconds, counted from startTime
+            ads = run_policy.get("activeDeadlineSeconds")
+            started = _parse_time(status.get("startTime"))
+            deadline_hit = False
+            if ads is not None and started is not None and not failed_msg:
+                left = started + int(ads) - now
+                if left <= 0:
+                    deadline_hit = True
+                else:
+                    requeue = min(requeue, left) if requeue else left
+            if deadline_hit:
+                _set_condition(status, "Failed", "DeadlineExceeded",
+                               f"{self.kind} {req.name} is active more than {int(ads)} seconds.")
+                status["completionTime"] = now_rfc3339()
+                self._delete_pods_and_services(pods, req.namespace, phases=("Running", "Pending", None))
+            elif failed_msg:
                 _set_condition(status, "Failed", f"{self.kind}Failed", failed_msg)
                 status["completionTime"] = now_rfc3339()
-            elif self._succeeded(rstat, specs):
+            elif self._succeeded(job, rstat, specs):
                 _set_condition(status, "Succeeded", f"{self.kind}Succeeded",
                                f'{self.kind} {req.name} is successfully completed.')
                 status["completionTime"] = now_rfc3339()
             elif self._running(pods, rstat):
                 if not _has(status, "Running"):
                     _set_condition(status, "Running", f"{self.kind}Running", f'{self.kind} {req.name} is running.')
-                status.setdefault("startTime", now_rfc3339())
+            if (_has(status, "Succeeded") or _has(status, "Failed")) and run_policy.get("ttlSecondsAfterFinished") is not None:
+                requeue = max(0.05, float(run_policy["ttlSecondsAfterFinished"]))
         if _has(status, "Succeeded") or _has(status, "Failed"):
             clean = run_policy.get("cleanPodPolicy", "None")
             for p in pods.values():
@@ -210,10 +378,22 @@ class _JobBase(Controller):
                         c.delete("v1", "Pod", p["metadata"]["name"], req.namespace)
                     except ApiError:
                         pass
+        self._write_status(job, status)
+        return Result(requeue_after=requeue) if requeue > 0 else Result()
+
+    def _write_status(self, job: dict, status: dict):
         if status != (job.get("status") or {}):
             job["status"] = status
-            c.update_status(job)
-        return Result()
+            self.client.update_status(job)
+
+    def _restarts_used(self, rtype: str, total: int, per_type: dict) -> int:
+        """Restarts counted against ``rtype``'s backoff limit (job-wide, as the training
+        operator counts them)."""
+        return total
+
+    def _job_failure(self, job: dict, rstat: dict) -> Optional[str]:
+        """A job-level failure decided from the replica counts (elastic PyTorchJobs), or None."""
+        return None
 
     def _restart_policy(self, job, rtype, specs) -> str:
         return specs[rtype].get("restartPolicy", "OnFailure")
@@ -223,10 +403,10 @@ class _JobBase(Controller):
         unlimited)."""
         return backoff
 
-    def _failure_message(self, name: str, rtype: str, pod: dict) -> Optional[str]:
+    def _failure_message(self, job: dict, rtype: str, pod: dict) -> Optional[str]:
         """The Failed condition's message when a non-retried ``rtype`` pod failing ends the job,
         or None when that failure does not decide the job."""
-        return f'{self.kind} {name} has failed because {rtype} replica(s) failed.'
+        return f'{self.kind} {job["metadata"]["name"]} has failed because {rtype} replica(s) failed.'
 
     def _running(self, pods: dict, rstat: dict) -> bool:
         return any(p.get("status", {}).get("phase") == "Running" for p in pods.values())
@@ -242,7 +422,7 @@ class _JobBase(Controller):
     def _wants_service(self, pod) -> bool:
         return True
 
-    def _succeeded(self, rstat, specs) -> bool:
+    def _succeeded(self, job, rstat, specs) -> bool:
         raise NotImplementedError
 
 
@@ -255,6 +435,9 @@ class PyTorchJobReconciler(_JobBase):
 
     def _nproc(self, job, tpl) -> int:
         v = job["spec"].get("nprocPerNode")
+        ep = _elastic(job) or {}
+        if v is None and ep.get("nProcPerNode"):
+            v = ep["nProcPerNode"]
         if v in (None, "auto", "gpu"):
             return max(1, _gpus(tpl))
         return int(v)
@@ -266,15 +449,47 @@ class PyTorchJobReconciler(_JobBase):
         rank = index if rtype == "Master" else index + (1 if "Master" in specs else 0)
         port = self._port(job)
         nproc = self._nproc(job, tpl)
-        return [{"name": "MASTER_ADDR", "value": master}, {"name": "MASTER_PORT", "value": str(port)},
-                {"name": "WORLD_SIZE", "value": str(nnodes)}, {"name": "RANK", "value": str(rank)},
-                {"name": "PET_MASTER_ADDR", "value": master}, {"name": "PET_MASTER_PORT", "value": str(port)},
-                {"name": "PET_NNODES", "value": str(nnodes)}, {"name": "PET_NODE_RANK", "value": str(rank)},
-                {"name": "PET_NPROC_PER_NODE", "value": str(nproc)},
-                {"name": "HSA_ENABLE_IPC_MODE_LEGACY", "value": "0"},
-                {"name": "PYTHONUNBUFFERED", "value": "1"}]
+        env = [{"name": "MASTER_ADDR", "value": master}, {"name": "MASTER_PORT", "value": str(port)},
+               {"name": "WORLD_SIZE", "value": str(nnodes)}, {"name": "RANK", "value": str(rank)},
+               {"name": "PET_MASTER_ADDR", "value": master}, {"name": "PET_MASTER_PORT", "value": str(port)},
+               {"name": "PET_NNODES", "value": str(nnodes)}, {"name": "PET_NODE_RANK", "value": str(rank)},
+               {"name": "PET_NPROC_PER_NODE", "value": str(nproc)},
+               {"name": "HSA_ENABLE_IPC_MODE_LEGACY", "value": "0"},
+               {"name": "PYTHONUNBUFFERED", "value": "1"}]
+        ep = _elastic(job)
+        if ep is not None:
+            # elastic rendezvous (kfamd-launch --nnodes MIN:MAX, hosted by worker 0's agent)
+            mn, mx = _elastic_bounds(job)
+            host = ep.get("rdzvHost") or master
+            rport = int(ep.get("rdzvPort") or port + 1)
+            over = {"PET_NNODES": f"{mn}:{mx}", "PET_RDZV_BACKEND": ep.get("rdzvBackend") or "c10d",
+                    "PET_RDZV_ENDPOINT": f"{host}:{rport}", "PET_RDZV_ID": ep.get("rdzvId") or name,
+                    "PET_MAX_RESTARTS": str(int(ep.get("maxRestarts") or 0))}
+            for kv in ep.get("rdzvConf") or []:
+                if kv.get("key") == "last_call_timeout":
+                    over["KFAMD_RDZV_LAST_CALL"] = str(kv.get("value"))
+            env = [e for e in env if e["name"] not in over] + [{"name": k, "value": v} for k, v in over.items()]
+        return env
 
-    def _succeeded(self, rstat, specs):
+    def _failure_message(self, job, rtype, pod):
+        if _elastic(job) is not None and rtype == "Worker":
+            return None          # decided by _job_failure: only below minReplicas
+        return super()._failure_message(job, rtype, pod)
+
+    def _job_failure(self, job, rstat):
+        if _elastic(job) is None:
+            return None
+        w = rstat.get("Worker", {})
+        mn, _ = _elastic_bounds(job)
+        if w.get("failed", 0) and w.get("active", 0) + w.get("succeeded", 0) < mn:
+            return (f'PyTorchJob {job["metadata"]["name"]} has failed because fewer than minReplicas={mn} '
+                    f'Worker replicas remain ({w.get("failed", 0)} failed).')
+        return None
+
+    def _succeeded(self, job, rstat, specs):
+        if _elastic(job) is not None:      # elastic: the surviving group finished
+            w = rstat.get("Worker", {})
+            return w.get("succeeded", 0) >= 1 and w.get("active", 0) == 0
         if "Master" in specs:
             return rstat.get("Master", {}).get("succeeded", 0) >= int(specs["Master"].get("replicas", 1))
         w = specs.get("Worker", {})
@@ -426,7 +641,7 @@ class MPIJobReconciler(_JobBase):
     def _wants_service(self, pod):
         return pod["metadata"]["labels"][LBL_RTYPE] == "worker"
 
-    def _succeeded(self, rstat, specs):
+    def _succeeded(self, job, rstat, specs):
         return rstat.get("Launcher", {}).get("succeeded", 0) >= 1
 
     # --- mpi-operator v2beta1 outcome semantics (pkg/controller/mpi_job_controller.go
@@ -441,7 +656,13 @@ class MPIJobReconciler(_JobBase):
             return self.BATCH_BACKOFF_DEFAULT if backoff is None else backoff
         return backoff
 
-    def _failure_message(self, name, rtype, pod):
+    def _restarts_used(self, rtype, total, per_type):
+        # the Launcher's batch Job counts its own failures only: Worker restarts (OnFailure
+        # Workers without an mpirun Launcher) do not use up the Launcher's retries
+        return per_type.get(rtype, 0) if rtype == "Launcher" else total
+
+    def _failure_message(self, job, rtype, pod):
+        name = job["metadata"]["name"]
         if rtype == "Launcher":
             return f"MPIJob {name} has failed because the launcher failed."
         if (pod.get("status") or {}).get("reason") == "Evicted":

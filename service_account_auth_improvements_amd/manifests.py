@@ -155,16 +155,35 @@ def crds() -> Dict[str, dict]:
                                       "rewrite": STR, "timeout": STR}, ["targetPort", "basePrefix"]),
                    "rwoScheduling": BOOL}, ["pvc"])
     pv_status = obj({"conditions": CONDITIONS, "ready": BOOL, "url": STR})
+    # kubeflow.org/v1 RunPolicy: every field is declared (so none is pruned silently); the ones
+    # this platform cannot honour (schedulingPolicy: no gang scheduler) are rejected at admission
+    # by controlplane/training.py validate_job
     run_policy = obj({"cleanPodPolicy": {"type": "string", "enum": ["All", "Running", "None"]},
                       "backoffLimit": {"type": "integer", "minimum": 0},
-                      "activeDeadlineSeconds": INT, "ttlSecondsAfterFinished": INT})
+                      "activeDeadlineSeconds": {"type": "integer", "minimum": 0},
+                      "ttlSecondsAfterFinished": {"type": "integer", "minimum": 0},
+                      "suspend": BOOL,
+                      "schedulingPolicy": obj({"minAvailable": INT, "queue": STR, "minResources": QUANTITY_MAP,
+                                               "priorityClass": STR, "scheduleTimeoutSeconds": INT})})
     job_status = obj({"conditions": CONDITIONS,
                       "replicaStatuses": {"type": "object", "additionalProperties": REPLICA_STATUS},
-                      "restartCount": INT, "startTime": STR, "completionTime": STR, "lastReconcileTime": STR})
+                      "restartCount": INT, "startTime": STR, "completionTime": STR, "lastReconcileTime": STR,
+                      # restarts per replica type (an MPIJob Launcher's backoffLimit counts its own only)
+                      "replicaRestarts": {"type": "object", "additionalProperties": INT}})
     pt_spec = obj({"pytorchReplicaSpecs": obj({"Master": REPLICA_SPEC, "Worker": REPLICA_SPEC}),
                    "nprocPerNode": {"x-kubernetes-int-or-string": True}, "runPolicy": run_policy,
-                   "elasticPolicy": obj({"minReplicas": INT, "maxReplicas": INT, "rdzvBackend": STR,
-                                         "maxRestarts": INT, "nProcPerNode": INT})}, ["pytorchReplicaSpecs"])
+                   "elasticPolicy": obj({"minReplicas": {"type": "integer", "minimum": 1},
+                                         "maxReplicas": {"type": "integer", "minimum": 1},
+                                         "rdzvBackend": STR, "rdzvHost": STR, "rdzvPort": INT, "rdzvId": STR,
+                                         "rdzvConf": arr(obj({"key": STR, "value": STR})),
+                                         "maxRestarts": {"type": "integer", "minimum": 0}, "nProcPerNode": INT,
+                                         "standalone": BOOL,
+                                         # autoscaling/v2 MetricSpec (declared; refused at admission)
+                                         "metrics": arr(obj({"type": STR, "resource": obj({
+                                             "name": STR, "target": obj({"type": STR, "averageUtilization": INT,
+                                                                         "averageValue": INT_OR_STR,
+                                                                         "value": INT_OR_STR})})}))})},
+                  ["pytorchReplicaSpecs"])
     mpi_spec = obj({"mpiReplicaSpecs": obj({"Launcher": REPLICA_SPEC, "Worker": REPLICA_SPEC}),
                     "slotsPerWorker": {"type": "integer", "minimum": 1}, "runPolicy": run_policy,
                     "mpiImplementation": {"type": "string", "enum": ["OpenMPI", "Intel", "MPICH"]},

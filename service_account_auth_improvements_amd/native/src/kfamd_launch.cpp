@@ -2,14 +2,19 @@
 // on MI355X nodes (SURVEY.md §1.2 layer D3, §3.7).
 //
 // What the PyTorchJob / MPIJob operators put in a pod is:
-//   kfamd-launch --nnodes N --node-rank R --nproc-per-node P \
+//   kfamd-launch --nnodes N|MIN:MAX --node-rank R --nproc-per-node P \
 //                --master-addr A --master-port M [--rdzv-port Q] [--max-restarts K] \
-//                [--heartbeat-timeout S] [--isolate-devices] -- <worker command...>
+//                [--rdzv-last-call S] [--heartbeat-timeout S] [--isolate-devices] -- <worker command...>
 //
 // 1. Rendezvous (TCP, node 0 hosts it on --rdzv-port, default M+1): every node agent
 //    registers (node_rank, nproc, hostname); once all N have joined, the server sends each
 //    agent its global rank offset, the world size and a round id.  A restart starts a new
 //    round, so all nodes restart their workers together.
+//    Elastic (--nnodes MIN:MAX, PyTorchJob elasticPolicy): a round closes when MAX agents
+//    have joined, or when at least MIN have and no new one has joined for --rdzv-last-call
+//    seconds.  Rank offsets follow node-rank order among the members, so after a node is
+//    lost the survivors' restart re-forms the group at the smaller world size; a
+//    replacement agent joins at the next round.
 // 2. Spawn: P workers per node, each with RANK, LOCAL_RANK, WORLD_SIZE,
 //    LOCAL_WORLD_SIZE, GROUP_RANK, NODE_RANK, MASTER_ADDR, MASTER_PORT (and the OpenMPI
 //    OMPI_COMM_WORLD_{RANK,SIZE,LOCAL_RANK,LOCAL_SIZE} names), the ROCm IPC
@@ -29,6 +34,7 @@
 #include <netdb.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#include <poll.h>
 #include <signal.h>
 #include <sys/socket.h>
 #include <sys/stat.h>
@@ -52,6 +58,8 @@ namespace {
 
 struct Args {
   int nnodes = 1, node_rank = 0, nproc = 1, max_restarts = 0;
+  int min_nodes = 1;                       // elastic lower bound (== nnodes unless MIN:MAX)
+  double last_call = 5.0;                  // elastic: quiet period before a round closes at >= MIN
   std::string master_addr = "127.0.0.1";
   int master_port = 29500, rdzv_port = -1;
   double heartbeat_timeout = 0.0, rdzv_timeout = 600.0, grace = 10.0;
@@ -80,25 +88,45 @@ void logf(const char* fmt, ...) {
   std::fprintf(stderr,
                "usage: kfamd-launch [--nnodes N] [--node-rank R] [--nproc-per-node P]\n"
                "  [--master-addr A] [--master-port M] [--rdzv-port Q] [--max-restarts K]\n"
-               "  [--heartbeat-timeout S] [--rdzv-timeout S] [--isolate-devices] -- cmd...\n");
+               "  [--rdzv-last-call S] [--heartbeat-timeout S] [--rdzv-timeout S] [--isolate-devices] -- cmd...\n"
+               "  --nnodes MIN:MAX = elastic membership (PET_NNODES / PET_RDZV_ENDPOINT / PET_MAX_RESTARTS too)\n");
   std::exit(2);
+}
+
+// "N" or "MIN:MAX"
+void parse_nnodes(const std::string& v, Args& a) {
+  const size_t c = v.find(':');
+  if (c == std::string::npos) {
+    a.nnodes = a.min_nodes = std::stoi(v);
+  } else {
+    a.min_nodes = std::stoi(v.substr(0, c));
+    a.nnodes = std::stoi(v.substr(c + 1));
+  }
 }
 
 Args parse(int argc, char** argv) {
   Args a;
   auto env_int = [](const char* k, int d) { const char* v = getenv(k); return v ? atoi(v) : d; };
   // operator-injected defaults (training-operator PET_* convention)
-  a.nnodes = env_int("PET_NNODES", 1);
+  parse_nnodes(getenv("PET_NNODES") ? getenv("PET_NNODES") : "1", a);
   a.node_rank = env_int("PET_NODE_RANK", 0);
   a.nproc = env_int("PET_NPROC_PER_NODE", 1);
+  a.max_restarts = env_int("PET_MAX_RESTARTS", 0);
   if (const char* v = getenv("PET_MASTER_ADDR")) a.master_addr = v;
   a.master_port = env_int("PET_MASTER_PORT", 29500);
+  if (const char* v = getenv("PET_RDZV_ENDPOINT")) {          // host:port of the c10d-style rendezvous
+    const std::string e = v;
+    const size_t c = e.rfind(':');
+    if (c != std::string::npos) a.rdzv_port = std::stoi(e.substr(c + 1));
+  }
+  if (const char* v = getenv("KFAMD_RDZV_LAST_CALL")) a.last_call = std::stod(v);
   int i = 1;
   for (; i < argc; ++i) {
     std::string s = argv[i];
     auto next = [&]() -> std::string { if (i + 1 >= argc) usage(); return argv[++i]; };
     if (s == "--") { ++i; break; }
-    else if (s == "--nnodes") a.nnodes = std::stoi(next());
+    else if (s == "--nnodes") parse_nnodes(next(), a);
+    else if (s == "--rdzv-last-call") a.last_call = std::stod(next());
     else if (s == "--node-rank") a.node_rank = std::stoi(next());
     else if (s == "--nproc-per-node") a.nproc = std::stoi(next());
     else if (s == "--master-addr") a.master_addr = next();
@@ -113,7 +141,9 @@ Args parse(int argc, char** argv) {
     else { a.cmd.push_back(s); }
   }
   for (; i < argc; ++i) a.cmd.push_back(argv[i]);
-  if (a.cmd.empty() || a.nnodes < 1 || a.nproc < 1 || a.node_rank < 0 || a.node_rank >= a.nnodes) usage();
+  if (a.cmd.empty() || a.nnodes < 1 || a.min_nodes < 1 || a.min_nodes > a.nnodes || a.nproc < 1 ||
+      a.node_rank < 0 || a.node_rank >= a.nnodes)
+    usage();
   if (a.rdzv_port < 0) a.rdzv_port = a.master_port + 1;
   return a;
 }
@@ -197,20 +227,32 @@ struct Assignment {
 // Node 0: serve one rendezvous round (all nnodes join) and answer every member.
 // Runs in a background thread for the launcher's lifetime so restarts can re-join.
 struct RdzvServer {
-  int fd = -1, nnodes = 1;
+  int fd = -1, nnodes = 1, min_nodes = 1;
+  double last_call = 5.0;
   std::thread th;
-  void start(int port, int nn) {
+  void start(int port, int nn, int mn, double lc) {
     nnodes = nn;
+    min_nodes = mn;
+    last_call = lc;
     fd = listen_on(port);
     if (fd < 0) return;
     th = std::thread([this] { loop(); });
     th.detach();
   }
+  // a round is complete with all nnodes members, or (elastic) with >= min_nodes and no join
+  // for last_call seconds
+  bool complete(size_t n, double last_join) const {
+    if ((int)n >= nnodes) return true;
+    return (int)n >= min_nodes && min_nodes < nnodes && now_s() - last_join >= last_call;
+  }
   void loop() {
     int round = 0;
     while (!g_stop) {
       std::map<int, std::pair<int, int>> members;  // node_rank -> (nproc, fd)
-      while ((int)members.size() < nnodes && !g_stop) {
+      double last_join = now_s();
+      while (!complete(members.size(), last_join) && !g_stop) {
+        pollfd pfd{fd, POLLIN, 0};
+        if (::poll(&pfd, 1, 100) <= 0) continue;
         int c = ::accept(fd, nullptr, nullptr);
         if (c < 0) continue;
         std::string line;
@@ -222,7 +264,9 @@ struct RdzvServer {
         if (tag != "JOIN" || nr < 0 || nr >= nnodes || np < 1) { send_line(c, "ERR bad join"); ::close(c); continue; }
         if (members.count(nr)) ::close(members[nr].second);   // a restarted agent re-joins
         members[nr] = {np, c};
+        last_join = now_s();
       }
+      if (g_stop) break;
       ++round;
       int offset = 0, world = 0;
       for (auto& m : members) world += m.second.first;
@@ -243,7 +287,7 @@ bool rendezvous(const Args& a, Assignment& out) {
   std::string line;
   bool ok = recv_line(fd, line, a.rdzv_timeout);
   ::close(fd);
-  if (!ok) { logf("rendezvous: timed out waiting for %d nodes", a.nnodes); return false; }
+  if (!ok) { logf("rendezvous: timed out waiting for %d nodes", a.min_nodes); return false; }
   std::istringstream is(line);
   std::string tag;
   is >> tag >> out.rank_offset >> out.world >> out.round;
@@ -404,7 +448,7 @@ int main(int argc, char** argv) {
   signal(SIGINT, on_signal);
   signal(SIGPIPE, SIG_IGN);
   RdzvServer server;
-  if (a.node_rank == 0) server.start(a.rdzv_port, a.nnodes);
+  if (a.node_rank == 0) server.start(a.rdzv_port, a.nnodes, a.min_nodes, a.last_call);
   int rc = 1;
   for (int attempt = 0; attempt <= a.max_restarts; ++attempt) {
     Assignment as;

@@ -13,6 +13,7 @@
 #   kbench:BIN[:A,B,..]     tools/kbench/bin/BIN A B ..                         -> OUTDIR/kbench.txt
 #   pmc:BIN[:A,B,..]        two PMC passes over a kbench binary (tools/kbench/pmc.sh)
 #   tool:SCRIPT[:A,B,..]    python -u tools/SCRIPT A B ..                       -> OUTDIR/SCRIPT.log
+#   env:VAR=VALUE           export VAR=VALUE for the steps after it (env:VAR= unsets it)
 # Counter runs never combine --pmc with trace domains; nothing here sets GPU_MAX_HW_QUEUES.
 set -o pipefail
 export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
@@ -64,6 +65,10 @@ for step in "$@"; do
       log=$O/${a1%.py}_$n.log
       timeout -k 10 600 python -u "tools/$a1" "${args[@]}" > "$log" 2>&1 || fail "$step" $? "$log"
       grep -v amdgpu.ids "$log" | tail -8 | cut -c1-300 ;;
+    env)
+      v=${step#env:}
+      if [ -z "${v#*=}" ]; then unset "${v%%=*}"; else export "$v"; fi
+      echo "env $v" ;;
     *)
       echo "unknown step '$step'"; exit 2 ;;
   esac

@@ -1,7 +1,7 @@
 // Standalone microbench for the dW GEMM (ops/csrc/gemm.hip) at the Llama-3-8B training shapes
 // (K = 32768 tokens = micro-batch 4 x 8192 by default): C[M,N] = A^T B with A [K, M], B [K, N].  Prints per-shape time, TFLOP/s
 // and a checksum so build variants (-D flags) can be compared.  Run: gemm_bench [iters].
-#include "../../service_account_auth_improvements_amd/ops/csrc/gemm.hip"
+#include "gemm_lab.hip"   // production kernel + lab variants (KF_GEMM_IMPL=4: 4-wave tn4)
 
 #include <cstdio>
 #include <cstring>
@@ -36,6 +36,8 @@ __global__ void checksum(const bf16_t* c, long n, double* out) {
 int main(int argc, char** argv) {
   const int iters = argc > 1 ? atoi(argv[1]) : 20;
   const int K = argc > 2 ? atoi(argv[2]) : 32768;
+  const int impl = getenv("KF_GEMM_IMPL") ? atoi(getenv("KF_GEMM_IMPL")) : 8;
+  printf("impl %d\n", impl);
   struct Shape { const char* name; int M, N; };
   const Shape shapes[] = {{"wqkv", 6144, 4096}, {"wo", 4096, 4096}, {"wgu", 28672, 4096},
                           {"wd", 4096, 14336}, {"lm_head", 128256, 4096}};
@@ -50,7 +52,11 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e1));
   double tot_ms = 0, tot_fl = 0;
   for (const Shape& s : shapes) {
-    auto run = [&] { if (kf_gemm_tn(A, s.M, B, s.N, C, s.N, s.M, s.N, K, 0, 0)) { fprintf(stderr, "bad shape\n"); exit(1); } };
+    auto run = [&] {
+      const int rc = impl == 4 ? kf_gemm_tn4(A, s.M, B, s.N, C, s.N, s.M, s.N, K, 0, 0)
+                               : kf_gemm_tn(A, s.M, B, s.N, C, s.N, s.M, s.N, K, 0, 0);
+      if (rc) { fprintf(stderr, "bad shape\n"); exit(1); }
+    };
     for (int i = 0; i < 3; ++i) run();
     CK(hipDeviceSynchronize());
     CK(hipEventRecord(e0));
