@@ -36,7 +36,7 @@ from .. import ops
 from ..ops.attention import attention_bwd, attention_fwd
 from ..parallel import context as cpx
 from ..parallel.state import (ParallelState, _chunk_rows, get_state, tp_all_gather_rows, tp_all_reduce,
-                              tp_reduce_scatter_rows)
+                              tp_all_reduce_work, tp_reduce_scatter_into, tp_reduce_scatter_rows)
 
 # KFAMD_DX_T=0 runs the activation-gradient GEMMs on the untransposed weights (A/B switch)
 _DX_T = os.environ.get("KFAMD_DX_T", "1") != "0"
@@ -307,7 +307,7 @@ class Llama:
             return x, []
         if self._sp:
             return tp_reduce_scatter_rows(x, self.st, self.tp_comm_chunks, async_op=True)
-        return x, [dist.all_reduce(x, group=self.st.tp_group, async_op=True)]
+        return x, [tp_all_reduce_work(x, self.st)]
 
     @staticmethod
     def _finish(pending):
@@ -324,20 +324,19 @@ class Llama:
         c = _chunk_rows(T, self.tp_comm_chunks, self.tp)
         if self.tp == 1 or c == 1:
             return self._reduce_out(torch.mm(x, W.t()))
-        n, tp, g = T // c, self.tp, self.st.tp_group
+        n, tp = T // c, self.tp
         works, keep = [], []
         if self._sp:
             out = torch.empty((T // tp, W.shape[0]), dtype=x.dtype, device=x.device)
             for k in range(c):
                 yk = torch.mm(x[k * n:(k + 1) * n], W.t())
                 keep.append(yk)               # alive until its reduce-scatter has run
-                works.append(dist.reduce_scatter_tensor(out[k * n // tp:(k + 1) * n // tp], yk, group=g,
-                                                        async_op=True))
+                works.append(tp_reduce_scatter_into(out[k * n // tp:(k + 1) * n // tp], yk, self.st))
         else:
             out = torch.empty((T, W.shape[0]), dtype=x.dtype, device=x.device)
             for k in range(c):
                 torch.mm(x[k * n:(k + 1) * n], W.t(), out=out[k * n:(k + 1) * n])
-                works.append(dist.all_reduce(out[k * n:(k + 1) * n], group=g, async_op=True))
+                works.append(tp_all_reduce_work(out[k * n:(k + 1) * n], self.st))
         for w in works:
             w.wait()
         return out

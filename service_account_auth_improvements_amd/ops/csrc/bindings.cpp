@@ -37,6 +37,9 @@ int kf_flash_fwd(const void*, long, void*, long, float*, int, int, int, int, int
 int kf_flash_bwd(const void*, long, const void*, long, const void*, long, const float*, float*,
                  float*, float*, void*, long, int, int, int, int, int, float, int, hipStream_t);
 int kf_decode_splits(int, int, int);
+int kf_decode_splits1(int, int, int);
+int kf_decode_attn_fused(const void*, long, const void*, const void*, const int*, const int*, void*, long, float*,
+                         float*, int*, int, int, int, int, int, int, float, hipStream_t);
 int kf_decode_attn(const void*, long, const void*, const void*, const int*, const int*, void*, long,
                    float*, float*, int, int, int, int, int, int, float, hipStream_t);
 int kf_rope_append(void*, long, int, int, int, int, const float*, const float*, const int*, const int*, void*,
@@ -67,6 +70,10 @@ int kf_car_close(void*);
 int kf_car_free(void*);
 int kf_car_allreduce(void* const*, int, int, const void*, void*, long, long, int, hipStream_t);
 int kf_car_error(void*, hipStream_t);
+long kf_ts_header_bytes();
+int kf_ts_alloc(long, int, void**, void*);
+int kf_ts_run(int, void* const*, int, int, const void*, void*, long, long, int, hipStream_t);
+int kf_ts_error(void*, hipStream_t);
 }
 
 namespace {
@@ -301,6 +308,28 @@ void check_rows_i32(const at::Tensor& t, int64_t B, const char* name) {
               " must be int32 [B] on the GPU");
 }
 
+// Per-device arrival tickets of the fused decode attention (4096 int32, zeroed once).  Returns
+// nullptr while the current stream is capturing a graph and the buffer does not exist yet (the
+// caller then takes the two-kernel path); the serving engine's warm-up runs before capture.
+int* decode_tickets(int dev) {
+  static std::mutex mu;
+  static int* buf[64] = {nullptr};
+  if (dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> lk(mu);
+  if (buf[dev] == nullptr) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(cur_stream(), &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+    int* p = nullptr;
+    if (hipMalloc(&p, 4096 * sizeof(int)) != hipSuccess) return nullptr;
+    if (hipMemset(p, 0, 4096 * sizeof(int)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+      (void)hipFree(p);
+      return nullptr;
+    }
+    buf[dev] = p;
+  }
+  return buf[dev];
+}
+
 // q2d: [B, >=Hq*D] rows (e.g. the q columns of fused qkv rows). Returns o [B, Hq*D].
 at::Tensor decode_attn(const at::Tensor& q2d, const at::Tensor& kc, const at::Tensor& vc,
                        const at::Tensor& slots, const at::Tensor& lengths, int64_t Hq, double scale) {
@@ -316,8 +345,29 @@ at::Tensor decode_attn(const at::Tensor& q2d, const at::Tensor& kc, const at::Te
     const char* v = std::getenv("KFAMD_DECODE_SPLITS");   // tuning override (tools/bench_decode_splits.py)
     return v ? std::atoi(v) : 0;
   }();
-  const int splits = splits_env > 0 ? splits_env : kf_decode_splits((int)B, (int)Hkv, (int)Lmax);
   auto f32 = q2d.options().dtype(at::kFloat);
+  // small batches: split-K + merge in one launch (kf_decode_attn_fused), whose arrival tickets
+  // live in a per-device zeroed buffer that every launch leaves zero (allocated on first use,
+  // outside any graph capture; KFAMD_DECODE_FUSED=0 keeps the two-kernel form)
+  const char* fv = std::getenv("KFAMD_DECODE_FUSED");      // read per call (tests compare both forms)
+  const bool fused_on = !(fv && fv[0] == '0');
+  if (fused_on && B <= 4 && B * Hkv <= 4096 && Hq / Hkv <= 8) {
+    int* tickets = decode_tickets(q2d.device().index());
+    if (tickets != nullptr) {
+      const int splits1 = kf_decode_splits1((int)B, (int)Hkv, (int)Lmax);
+      const int64_t slots_per = B * Hkv * 64;                        // MAX_SPLITS1 = 64
+      auto po = at::empty({slots_per * (Hq / Hkv) * D}, f32);
+      auto pml = at::empty({slots_per * (Hq / Hkv) * 2}, f32);
+      auto out = at::empty({B, Hq * D}, q2d.options());
+      check_rc(kf_decode_attn_fused(q2d.data_ptr(), q2d.stride(0), kc.data_ptr(), vc.data_ptr(),
+                                    slots.data_ptr<int>(), lengths.data_ptr<int>(), out.data_ptr(), out.stride(0),
+                                    po.data_ptr<float>(), pml.data_ptr<float>(), tickets, (int)B, (int)Hq, (int)Hkv,
+                                    (int)D, (int)Lmax, splits1, (float)scale, cur_stream()),
+               "decode_attn_fused");
+      return out;
+    }
+  }
+  const int splits = splits_env > 0 ? splits_env : kf_decode_splits((int)B, (int)Hkv, (int)Lmax);
   auto po = at::empty({B * Hq * splits * D}, f32);
   auto pml = at::empty({B * Hq * splits * 2}, f32);
   auto out = at::empty({B, Hq * D}, q2d.options());
@@ -557,6 +607,38 @@ void car_allreduce_(const std::vector<int64_t>& ptrs, int64_t rank, at::Tensor& 
 
 int64_t car_error(int64_t own) { return kf_car_error(reinterpret_cast<void*>(own), cur_stream()); }
 
+// ---- two-shot reduce-scatter / all-gather / all-reduce (ops/csrc/custom_ar.hip, namespace ts);
+// open / close / free are the one-shot ones (plain IPC handles).
+std::tuple<int64_t, at::Tensor> ts_alloc(int64_t slot_bytes, int64_t world) {
+  void* p = nullptr;
+  auto h = at::empty({64}, at::TensorOptions().dtype(at::kByte));
+  TORCH_CHECK(kf_ts_alloc(slot_bytes, (int)world, &p, h.data_ptr()) == 0, "ts_alloc: uncached IPC allocation failed");
+  return {reinterpret_cast<int64_t>(p), h};
+}
+
+// mode 0: all-reduce x in place (out is x); 1: reduce-scatter x[n] -> out[n / world];
+// 2: all-gather x[n / world] -> out[n].  Runs on the current stream.
+void ts_run(int64_t mode, const std::vector<int64_t>& ptrs, int64_t rank, const at::Tensor& x, at::Tensor& out,
+            int64_t slot_bytes, int64_t blocks) {
+  check_bf16_cuda(x, "x");
+  check_bf16_cuda(out, "out");
+  const long w = (long)ptrs.size();
+  TORCH_CHECK(x.is_contiguous() && out.is_contiguous(), "ts_run: contiguous tensors");
+  const long n = mode == 2 ? x.numel() * w : x.numel();
+  const long n_out = mode == 1 ? n / w : n;
+  TORCH_CHECK(out.numel() == n_out, "ts_run: out has ", out.numel(), " elements, expected ", n_out);
+  TORCH_CHECK(n % (8 * w) == 0 && 2 * n <= slot_bytes, "ts_run: numel % (8 world) == 0 that fits the slot");
+  TORCH_CHECK(mode != 0 || x.data_ptr() == out.data_ptr(), "ts_run: all-reduce is in place");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  std::vector<void*> pv;
+  for (auto v : ptrs) pv.push_back(reinterpret_cast<void*>(v));
+  check_rc(kf_ts_run((int)mode, pv.data(), (int)w, (int)rank, x.data_ptr(), out.data_ptr(), n, slot_bytes,
+                     (int)blocks, cur_stream()),
+           "ts_run");
+}
+
+int64_t ts_error(int64_t own) { return kf_ts_error(reinterpret_cast<void*>(own), cur_stream()); }
+
 // Weight-gradient GEMM: C[M, N] (+)= a^T . b with a = [K, M], b = [K, N] (row stride may
 // exceed the width: views into fused activations); C may be a view into the flat grad buffer.
 bool gemm_tn_ok(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c) {
@@ -673,6 +755,9 @@ TORCH_LIBRARY(kfamd, m) {
   m.def("car_free", &car_free);
   m.def("car_allreduce_(int[] ptrs, int rank, Tensor(a!) x, int slot_bytes, int blocks) -> ()", &car_allreduce_);
   m.def("car_error", &car_error);
+  m.def("ts_alloc", &ts_alloc);
+  m.def("ts_run(int mode, int[] ptrs, int rank, Tensor x, Tensor(a!) out, int slot_bytes, int blocks) -> ()", &ts_run);
+  m.def("ts_error", &ts_error);
   m.def("gemm_tn_ok", &gemm_tn_ok);
   m.def("gemm_tn_(Tensor a, Tensor b, Tensor(a!) c, bool accumulate) -> ()", &gemm_tn_);
   m.def("gemm_tn2_(Tensor a0, Tensor b0, Tensor(a!) c0, Tensor a1, Tensor b1, Tensor(b!) c1, bool accumulate) -> ()",

@@ -94,6 +94,134 @@ __global__ __launch_bounds__(NT) void one_shot_ar_kernel(Peers peers, int rank, 
 }
 }  // namespace car
 
+// ==== two-shot reduce-scatter / all-gather for training-size TP messages (16-268 MB) ===========
+// RCCL's ring moves an all-reduce over one link per hop; on a full xGMI mesh every rank can pull
+// from all N-1 peers at once.  Two-shot: rank r owns chunk r (1/N of the tensor); phase 1 it
+// reads chunk r from every peer's input and sums it (fp32, rank order -> every rank's result is
+// bit-identical, and for N = 2 equal to one bf16 rounding of the exact sum, as RCCL's), phase 2
+// every rank reads every peer's reduced chunk.  Each link carries 2 S / N per direction -- the
+// all-reduce minimum -- and all N-1 links of a GPU carry it concurrently.
+//   mode AR: input x[n] -> out[n] (sum)      mode RS: x[n] -> out[n/N] (own chunk of the sum)
+//   mode AG: x[n/N] (own chunk) -> out[n] (concatenation in rank order)
+// Buffer (uncached, IPC-exported, zeroed): [phase-1 flags | phase-2 flags: 2 slots x MAXB x MAXW
+// int32 each][epochs MAXB][err][pad to 16 KB][in: 2 slots x slot_bytes][red: 2 slots x slot_bytes/N]
+// Same per-block epoch / two-slot argument as the one-shot kernel: to enter call e a block has
+// seen every peer's call-(e-1) phase-2 flag, so no peer still reads call e-2's slot.
+// Every block's epoch advances once per call, so the communicator keeps ONE grid size for its
+// life (parallel/custom_ar.py TwoShot) and issues its calls on ONE stream: then every in-flight
+// block of every rank is in call k or k+1, and parity slots never collide.
+namespace ts {
+constexpr int MAXW = 8, MAXB = 64, NT = 512;
+constexpr long FLAGS1 = 0, FLAGS2 = 2L * MAXB * MAXW * 4, EPOCH_OFF = 2 * FLAGS2, ERR_OFF = EPOCH_OFF + MAXB * 4;
+constexpr long DATA_OFF = 16384;
+constexpr unsigned SPIN_LIMIT = 1u << 24;
+enum Mode { AR = 0, RS = 1, AG = 2 };
+
+__device__ __forceinline__ int* flag(char* base, long off, int slot, int b, int r) {
+  return reinterpret_cast<int*>(base + off) + ((slot * MAXB + b) * MAXW + r);
+}
+// lanes 0..W-1: post e to every peer's flag (release first), then wait for every peer's flag
+template <int W>
+__device__ __forceinline__ void exchange(const car::Peers& P, int rank, long off, int slot, int b, int e, char* mine) {
+  const int tid = threadIdx.x;
+  __syncthreads();
+  if (tid < W) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    __hip_atomic_store(flag(P.p[tid], off, slot, b, rank), e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    int* f = flag(mine, off, slot, b, tid);
+    unsigned spins = 0;
+    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != e) {
+      if (++spins > SPIN_LIMIT) {
+        __hip_atomic_store(reinterpret_cast<int*>(mine + ERR_OFF), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  }
+  __syncthreads();
+}
+
+template <int W, int MODE>
+__global__ __launch_bounds__(NT) void two_shot_kernel(car::Peers P, int rank, const bf16_t* x, bf16_t* out,
+                                                      long n, long slot_bytes) {
+  __shared__ int e_sh;
+  const int b = blockIdx.x, tid = threadIdx.x;
+  char* mine = P.p[rank];
+  int* epoch = reinterpret_cast<int*>(mine + EPOCH_OFF) + b;
+  if (tid == 0) e_sh = __hip_atomic_load(epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  __syncthreads();
+  const int e = e_sh, slot = e & 1;
+  const long red_bytes = slot_bytes / W;
+  auto in_of = [&](int p) { return reinterpret_cast<u32x4*>(P.p[p] + DATA_OFF + slot * slot_bytes); };
+  auto red_of = [&](int p) {
+    return reinterpret_cast<u32x4*>(P.p[p] + DATA_OFF + 2 * slot_bytes + slot * red_bytes);
+  };
+  // this block's share of one chunk, in 16-byte vectors (chunk = n / W elements)
+  const long cv = n / W / 8, per = (cv + gridDim.x - 1) / gridDim.x;
+  const long v0 = b * per, v1 = min(cv, v0 + per);
+  const u32x4* xin = reinterpret_cast<const u32x4*>(x);
+  if (MODE != AG) {
+    u32x4* mine_in = in_of(rank);
+    for (int c = 0; c < W; ++c)
+      for (long v = v0 + tid; v < v1; v += NT) mine_in[c * cv + v] = xin[c * cv + v];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    exchange<W>(P, rank, FLAGS1, slot, b, e, mine);
+    // phase 1: reduce my chunk over every peer's input (rank order)
+    u32x4* red = red_of(rank);
+    for (long v = v0 + tid; v < v1; v += NT) {
+      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      u32x4 src[W];
+#pragma unroll
+      for (int p = 0; p < W; ++p) src[p] = in_of(p)[rank * cv + v];
+#pragma unroll
+      for (int p = 0; p < W; ++p) {
+        float f[8];
+        unpack8(src[p], f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += f[j];
+      }
+      const u32x4 r = pack8(acc);
+      if (MODE == AR) red[v] = r;
+      reinterpret_cast<u32x4*>(out)[(MODE == AR ? rank * cv : 0) + v] = r;
+    }
+    if (MODE == AR) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    u32x4* red = red_of(rank);
+    for (long v = v0 + tid; v < v1; v += NT) {
+      red[v] = xin[v];
+      reinterpret_cast<u32x4*>(out)[rank * cv + v] = xin[v];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  if (MODE != RS) {
+    exchange<W>(P, rank, FLAGS2, slot, b, e, mine);
+    // phase 2: every peer's reduced chunk
+    for (long v = v0 + tid; v < v1; v += NT) {
+      u32x4 src[W];
+#pragma unroll
+      for (int p = 0; p < W; ++p) src[p] = red_of(p)[v];
+#pragma unroll
+      for (int p = 0; p < W; ++p)
+        if (p != rank) reinterpret_cast<u32x4*>(out)[p * cv + v] = src[p];
+    }
+  } else {
+    // RS posts phase 2 too (without reading anything): the slot-reuse argument needs every
+    // call's phase-2 flags
+    exchange<W>(P, rank, FLAGS2, slot, b, e, mine);
+  }
+  if (tid == 0) __hip_atomic_store(epoch, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int W>
+void launch_two_shot(int mode, int blocks, hipStream_t st, const car::Peers& P, int rank, const bf16_t* x, bf16_t* o,
+                     long n, long slot_bytes) {
+  if (mode == AR) hipLaunchKernelGGL((two_shot_kernel<W, AR>), dim3(blocks), dim3(NT), 0, st, P, rank, x, o, n, slot_bytes);
+  else if (mode == RS) hipLaunchKernelGGL((two_shot_kernel<W, RS>), dim3(blocks), dim3(NT), 0, st, P, rank, x, o, n, slot_bytes);
+  else hipLaunchKernelGGL((two_shot_kernel<W, AG>), dim3(blocks), dim3(NT), 0, st, P, rank, x, o, n, slot_bytes);
+}
+}  // namespace ts
+
 using namespace car;
 
 extern "C" {
@@ -141,6 +269,57 @@ int kf_car_allreduce(void* const* ptrs, int world, int rank, const void* x, void
   }
   KF_CHECK_LAUNCH();
   return 0;
+}
+
+long kf_ts_header_bytes() { return ts::DATA_OFF; }
+
+// this rank's two-shot buffer: header + 2 input slots + 2 reduced-chunk slots
+int kf_ts_alloc(long slot_bytes, int world, void** ptr, void* handle) {
+  if (world < 1 || world > ts::MAXW) return 5;
+  const long bytes = ts::DATA_OFF + 2 * slot_bytes + 2 * (slot_bytes / world);
+  if (hipExtMallocWithFlags(ptr, bytes, hipDeviceMallocUncached) != hipSuccess) return 1;
+  if (hipMemset(*ptr, 0, bytes) != hipSuccess) return 2;
+  if (hipDeviceSynchronize() != hipSuccess) return 3;
+  hipIpcMemHandle_t h;
+  if (hipIpcGetMemHandle(&h, *ptr) != hipSuccess) return 4;
+  std::memcpy(handle, &h, sizeof(h));
+  return 0;
+}
+
+// mode 0 all-reduce (x[n] -> out[n]), 1 reduce-scatter (x[n] -> out[n/world]), 2 all-gather
+// (x[n/world] -> out[n]); n is the FULL element count; n % (8 world) == 0, 2n <= slot_bytes.
+int kf_ts_run(int mode, void* const* ptrs, int world, int rank, const void* x, void* out, long n, long slot_bytes,
+              int blocks, hipStream_t st) {
+  if (world < 1 || world > ts::MAXW || rank < 0 || rank >= world || mode < 0 || mode > 2) return 1;
+  if (n % (8L * world) || 2 * n > slot_bytes || slot_bytes % (16L * world)) return 1;
+  if (((uintptr_t)x | (uintptr_t)out) & 15) return 2;
+  if (mode == ts::AR && x != out) return 3;              // in place, like dist.all_reduce
+  blocks = std::max(1, std::min(blocks, ts::MAXB));
+  Peers P{};
+  for (int i = 0; i < world; ++i) P.p[i] = static_cast<char*>(ptrs[i]);
+  auto X = static_cast<const bf16_t*>(x);
+  auto O = static_cast<bf16_t*>(out);
+  switch (world) {
+    case 1: ts::launch_two_shot<1>(mode, blocks, st, P, rank, X, O, n, slot_bytes); break;
+    case 2: ts::launch_two_shot<2>(mode, blocks, st, P, rank, X, O, n, slot_bytes); break;
+    case 4: ts::launch_two_shot<4>(mode, blocks, st, P, rank, X, O, n, slot_bytes); break;
+    case 8: ts::launch_two_shot<8>(mode, blocks, st, P, rank, X, O, n, slot_bytes); break;
+    default: return 4;
+  }
+  KF_CHECK_LAUNCH();
+  return 0;
+}
+
+int kf_ts_error(void* own, hipStream_t st) {
+  int v = 0;
+  char* p = static_cast<char*>(own) + ts::ERR_OFF;
+  if (hipMemcpyAsync(&v, p, 4, hipMemcpyDeviceToHost, st) != hipSuccess) return -1;
+  if (hipStreamSynchronize(st) != hipSuccess) return -1;
+  if (v) {
+    const int z = 0;
+    hipMemcpy(p, &z, 4, hipMemcpyHostToDevice);
+  }
+  return v;
 }
 
 // error word (1 = a peer never arrived within the spin budget); cleared by the read

@@ -54,6 +54,9 @@ __global__ __launch_bounds__(NT) void decode_split_kernel(
       part_ml[(obase + (long)tid * splits) * 2 + 0] = -INFINITY;
       part_ml[(obase + (long)tid * splits) * 2 + 1] = 0.f;
     }
+    // zero partial o too: the combine weighs it by 0, and 0 x (NaN left in an uninitialised
+    // workspace) is NaN
+    for (int e = tid; e < G * D; e += NT) part_o[(obase + (long)(e / D) * splits) * D + e % D] = 0.f;
     return;
   }
   const int n = end - start;
@@ -209,6 +212,193 @@ __global__ __launch_bounds__(CB_NT) void decode_combine_kernel(const float* __re
   }
 }
 
+// ---- small-batch decode (B <= SMALL_B): split-K and the combine in ONE launch ------------------
+// At B = 1 the two-kernel form is latency-bound (ctx 1024: 4 MB of K/V per layer in 8 + 4.7 us,
+// ~0.3 TB/s): each split kernel block runs three dependent phases, then a second launch merges.
+// Here every block streams its chunk in rounds of 32 keys with all four of a thread's 16-byte
+// loads (2 K rows, 2 V rows) in flight together, keeps an online softmax per thread (its own
+// keys), merges the 16 key streams of the block at the end, publishes its partial with
+// write-through (sc1) stores, and takes a ticket on a per-(row, kv head) counter: the block
+// whose ticket comes last merges all splits (sc1 loads) and writes the output, then re-arms the
+// counter for the next launch (the hand-off form of MI355X_MICROARCH.md "Valid forms", row 1).
+constexpr int SMALL_B = 4, MAX_SPLITS1 = 64, KR = 32;   // keys per round: 2 per 16-lane group
+__device__ __forceinline__ void st_sc1(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int G>
+__global__ __launch_bounds__(NT) void decode_fused_kernel(
+    const bf16_t* __restrict__ q, long q_ld, int hq_total,
+    const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
+    const int* __restrict__ slots, const int* __restrict__ lengths,
+    long slot_stride, long head_stride, int splits, float scale_log2,
+    float* __restrict__ part_o, float* __restrict__ part_ml, int* __restrict__ tickets,
+    bf16_t* __restrict__ out, long out_ld) {
+  __shared__ float sm[4][G], sl[4][G];
+  __shared__ float so[4][G][D];
+  __shared__ int is_last;
+  const int s = blockIdx.x, hk = blockIdx.y, b = blockIdx.z, Hkv = gridDim.y;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int sub = lane & 15, grp = tid >> 4;
+  const int len = min(lengths[b], (int)(head_stride / D));
+  const int chunk = ((len + splits - 1) / splits + 15) & ~15;     // 16-key granules
+  const int start = s * chunk, end = min(len, start + chunk);
+
+  float qf[G][8];
+#pragma unroll
+  for (int h = 0; h < G; ++h) {
+    const u32x4 v = ld16(q + (long)b * q_ld + (long)(hk * G + h) * D + sub * 8);
+    unpack8(v, qf[h]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) qf[h][i] *= scale_log2;
+  }
+  const long kvbase = (long)slots[b] * slot_stride + (long)hk * head_stride;
+  const bf16_t* kp = kc + kvbase;
+  const bf16_t* vp = vc + kvbase;
+
+  float m[G], l[G], acc[G][8];
+#pragma unroll
+  for (int h = 0; h < G; ++h) {
+    m[h] = -INFINITY;
+    l[h] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[h][i] = 0.f;
+  }
+  for (int r0 = start; r0 < end; r0 += KR) {
+    const int j0 = r0 + grp, j1 = r0 + 16 + grp;
+    const bool ok0 = j0 < end, ok1 = j1 < end;
+    const u32x4 zero = u32x4{0u, 0u, 0u, 0u};
+    const u32x4 k0 = ok0 ? ld16(kp + (long)j0 * D + sub * 8) : zero;
+    const u32x4 k1 = ok1 ? ld16(kp + (long)j1 * D + sub * 8) : zero;
+    const u32x4 v0 = ok0 ? ld16(vp + (long)j0 * D + sub * 8) : zero;
+    const u32x4 v1 = ok1 ? ld16(vp + (long)j1 * D + sub * 8) : zero;
+    float kf0[8], kf1[8], vf0[8], vf1[8];
+    unpack8(k0, kf0);
+    unpack8(k1, kf1);
+    unpack8(v0, vf0);
+    unpack8(v1, vf1);
+#pragma unroll
+    for (int h = 0; h < G; ++h) {
+      float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        a0 = fmaf(qf[h][i], kf0[i], a0);
+        a1 = fmaf(qf[h][i], kf1[i], a1);
+      }
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        a0 += __shfl_xor(a0, o, 64);
+        a1 += __shfl_xor(a1, o, 64);
+      }
+      a0 = ok0 ? a0 : -INFINITY;
+      a1 = ok1 ? a1 : -INFINITY;
+      const float mn = fmaxf(m[h], fmaxf(a0, a1));
+      if (mn == -INFINITY) continue;              // no valid key yet for this stream
+      const float al = exp2f(m[h] - mn), p0 = exp2f(a0 - mn), p1 = exp2f(a1 - mn);
+      m[h] = mn;
+      l[h] = fmaf(l[h], al, p0 + p1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[h][i] = fmaf(acc[h][i], al, fmaf(p0, vf0[i], p1 * vf1[i]));
+    }
+  }
+  // merge the 4 key streams of each wave (lanes l, l^16, l^32, l^48 hold the same columns)
+#pragma unroll
+  for (int h = 0; h < G; ++h) {
+#pragma unroll
+    for (int o = 16; o < 64; o <<= 1) {
+      const float mo = __shfl_xor(m[h], o, 64), lo_ = __shfl_xor(l[h], o, 64);
+      const float mn = fmaxf(m[h], mo);
+      const float a = mn == -INFINITY ? 0.f : exp2f(m[h] - mn), c = mn == -INFINITY ? 0.f : exp2f(mo - mn);
+      l[h] = l[h] * a + lo_ * c;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[h][i] = acc[h][i] * a + __shfl_xor(acc[h][i], o, 64) * c;
+      m[h] = mn;
+    }
+  }
+  if (lane < 16) {
+#pragma unroll
+    for (int h = 0; h < G; ++h) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) so[wave][h][sub * 8 + i] = acc[h][i];
+      if (sub == 0) { sm[wave][h] = m[h]; sl[wave][h] = l[h]; }
+    }
+  }
+  __syncthreads();
+  // the block's partial: merge the 4 waves, publish write-through
+  const long pbase = ((long)b * Hkv + hk) * MAX_SPLITS1 + s;          // (row, kv head, split)
+  for (int e = tid; e < G * D; e += NT) {
+    const int h = e / D, d = e % D;
+    float M = sm[0][h];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) M = fmaxf(M, sm[w][h]);
+    float o = 0.f;
+    if (M != -INFINITY) {
+#pragma unroll
+      for (int w = 0; w < 4; ++w) o = fmaf(exp2f(sm[w][h] - M), so[w][h][d], o);
+    }
+    st_sc1(part_o + (pbase * G + h) * D + d, o);
+  }
+  if (tid < G) {
+    float M = sm[0][tid];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) M = fmaxf(M, sm[w][tid]);
+    float L = 0.f;
+    if (M != -INFINITY) {
+#pragma unroll
+      for (int w = 0; w < 4; ++w) L = fmaf(exp2f(sm[w][tid] - M), sl[w][tid], L);
+    }
+    st_sc1(part_ml + (pbase * G + tid) * 2 + 0, M);
+    st_sc1(part_ml + (pbase * G + tid) * 2 + 1, L);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");       // every storing wave drains its stores
+  __syncthreads();
+  if (tid == 0) {
+    const int t = __hip_atomic_fetch_add(tickets + (long)b * Hkv + hk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    is_last = t == splits - 1;
+  }
+  __syncthreads();
+  if (!is_last) return;
+  // last block: merge every split of this (row, kv head) and write the G heads' outputs.
+  // (1) all (m, l) pairs at once; (2) per head one wave: global max, split weights, denominator;
+  // (3) every output element sums its splits' weighted partials, 8 independent loads in flight.
+  const long obase = ((long)b * Hkv + hk) * MAX_SPLITS1;
+  __shared__ float wt[MAX_SPLITS1][G], lt[MAX_SPLITS1][G], den[G];
+  for (int e = tid; e < splits * G; e += NT) {
+    const int t = e / G, h = e % G;
+    wt[t][h] = ld_sc1(part_ml + ((obase + t) * G + h) * 2);
+    lt[t][h] = ld_sc1(part_ml + ((obase + t) * G + h) * 2 + 1);
+  }
+  __syncthreads();
+  for (int h = wave; h < G; h += NT / 64) {
+    const float ms = lane < splits ? wt[lane][h] : -INFINITY;
+    const float M = wave_max(ms);
+    const float w = (M == -INFINITY || ms == -INFINITY) ? 0.f : exp2f(ms - M);
+    const float L = wave_sum(lane < splits ? w * lt[lane][h] : 0.f);
+    if (lane < splits) wt[lane][h] = w;
+    if (lane == 0) den[h] = L;
+  }
+  __syncthreads();
+  for (int e = tid; e < G * D; e += NT) {
+    const int h = e / D, d = e % D;
+    float o = 0.f;
+#pragma unroll 8
+    for (int t = 0; t < splits; ++t) o = fmaf(wt[t][h], ld_sc1(part_o + ((obase + t) * G + h) * D + d), o);
+    out[(long)b * out_ld + (long)(hk * G + h) * D + d] = f2bf(den[h] > 0.f ? o / den[h] : 0.f);
+  }
+  if (tid == 0) __hip_atomic_store(tickets + (long)b * Hkv + hk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int G>
+void launch_fused(dim3 grid, hipStream_t st, const bf16_t* q, long q_ld, int hq, const bf16_t* kc,
+                  const bf16_t* vc, const int* slots, const int* lengths, long slot_stride, long head_stride,
+                  int splits, float sl2, float* po, float* pml, int* tickets, bf16_t* out, long out_ld) {
+  hipLaunchKernelGGL(decode_fused_kernel<G>, grid, dim3(NT), 0, st, q, q_ld, hq, kc, vc, slots, lengths,
+                     slot_stride, head_stride, splits, sl2, po, pml, tickets, out, out_ld);
+}
+
 template <int G>
 void launch_split(dim3 grid, hipStream_t st, const bf16_t* q, long q_ld, int hq, const bf16_t* kc,
                   const bf16_t* vc, const int* slots, const int* lengths, long slot_stride,
@@ -226,6 +416,43 @@ extern "C" int kf_decode_splits(int B, int Hkv, int Lmax) {
   int max_by_len = std::max(1, Lmax / 64);
   int min_by_lds = (Lmax + MAXCHUNK - 17) / (MAXCHUNK - 16);
   return std::max(min_by_lds, std::min(want, max_by_len));
+}
+
+// Small-batch single-launch decode attention (B <= SMALL_B).  splits1: key splits per (row, kv
+// head), <= MAX_SPLITS1; workspace part_o fp32 [B*Hkv*MAX_SPLITS1*G*D], part_ml fp32
+// [B*Hkv*MAX_SPLITS1*G*2]; tickets int32 [B*Hkv], zero before the first launch (each launch
+// leaves them zero).
+extern "C" int kf_decode_splits1(int B, int Hkv, int Lmax) {
+  // ~one workgroup per CU (B = 1, 8 kv heads: 32 splits), <= MAX_SPLITS1 splits: more splits
+  // lengthen the last block's merge (its loads are a serial tail) more than they shorten the rest
+  const int want = std::max(1, 256 / std::max(1, B * Hkv));
+  return std::max(1, std::min({want, MAX_SPLITS1, (Lmax + 15) / 16}));
+}
+
+extern "C" int kf_decode_attn_fused(const void* q, long q_ld, const void* kc, const void* vc, const int* slots,
+                                    const int* lengths, void* out, long out_ld, float* part_o, float* part_ml,
+                                    int* tickets, int B, int Hq, int Hkv, int Dh, int Lmax, int splits,
+                                    float scale, hipStream_t st) {
+  if (Dh != D || Hkv <= 0 || Hq % Hkv != 0) return 1;
+  const int G = Hq / Hkv;
+  if (G > MAXG || splits <= 0 || splits > MAX_SPLITS1 || B > SMALL_B) return 2;
+  if (B == 0) return 0;
+  const long head_stride = (long)Lmax * D, slot_stride = (long)Hkv * head_stride;
+  const float sl2 = scale * LOG2E;
+  dim3 grid(splits, Hkv, B);
+  auto q16 = (const bf16_t*)q;
+  auto k16 = (const bf16_t*)kc;
+  auto v16 = (const bf16_t*)vc;
+  auto o16 = (bf16_t*)out;
+  switch (G) {
+    case 1: launch_fused<1>(grid, st, q16, q_ld, Hq, k16, v16, slots, lengths, slot_stride, head_stride, splits, sl2, part_o, part_ml, tickets, o16, out_ld); break;
+    case 2: launch_fused<2>(grid, st, q16, q_ld, Hq, k16, v16, slots, lengths, slot_stride, head_stride, splits, sl2, part_o, part_ml, tickets, o16, out_ld); break;
+    case 4: launch_fused<4>(grid, st, q16, q_ld, Hq, k16, v16, slots, lengths, slot_stride, head_stride, splits, sl2, part_o, part_ml, tickets, o16, out_ld); break;
+    case 8: launch_fused<8>(grid, st, q16, q_ld, Hq, k16, v16, slots, lengths, slot_stride, head_stride, splits, sl2, part_o, part_ml, tickets, o16, out_ld); break;
+    default: return 4;
+  }
+  KF_CHECK_LAUNCH();
+  return 0;
 }
 
 // q: rows of [Hq*D] bf16 with row stride q_ld (the q columns of a fused qkv row work).

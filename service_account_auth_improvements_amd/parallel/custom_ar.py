@@ -1,4 +1,7 @@
-"""One-shot all-reduce over peer-mapped HIP IPC buffers for latency-bound TP collectives.
+"""Peer-mapped HIP IPC collectives for tensor parallelism inside one MI355X node.
+
+``OneShotAllReduce``: latency-bound decode messages (below).  ``TwoShot``: bandwidth-bound
+training messages (reduce-scatter / all-gather / all-reduce of 16-268 MB activations).
 
 SURVEY.md §2.8 C7 / §5 "distributed communication backend": the decode step of an
 InferenceService with TP > 1 all-reduces a [B, hidden] bf16 activation twice per layer.
@@ -87,3 +90,136 @@ class OneShotAllReduce:
             torch.cuda.synchronize()
             k.car_free(self._own)
             self._own = 0
+
+
+class _Done:
+    """Work handle of a two-shot collective: ``wait()`` orders the CURRENT stream after it
+    (the ``torch.distributed`` async-work contract the model code uses)."""
+
+    def __init__(self, event):
+        self.event = event
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self.event)
+        return True
+
+
+class TwoShot:
+    """Two-shot reduce-scatter / all-gather / all-reduce over xGMI (ops/csrc/custom_ar.hip, ts).
+
+    RCCL runs a TP=8 reduction as a ring: 2(N-1) steps, each over ONE xGMI link at a time, so
+    a 128 MB all-reduce moves 2*(7/8)*128 MB through a single ~50 GB/s link direction per GPU.
+    On the full-mesh xGMI of an MI355X node every GPU has a direct link to every peer, so here
+    rank r pulls chunk r of every peer's input over all N-1 links AT ONCE, sums it in fp32 in
+    rank order, and (all-gather half) every rank pulls every peer's reduced chunk: each link
+    carries 2 S / N bytes per direction and the N-1 links work concurrently (per-link bytes
+    for the 70B TP=8 shard: profiles/llama3_70b_tp8_shard.md).  Results are bit-identical on
+    every rank (the chunk owner sums once) and, for N = 2, bit-identical to RCCL (one bf16
+    rounding of the exact fp32 sum).  For N > 2 RCCL's ring order differs: within rounding.
+
+    Layouts match ``dist.reduce_scatter_tensor`` / ``dist.all_gather_into_tensor`` (rank r's
+    block is the r-th contiguous 1/N of the full tensor), so :mod:`parallel.state` swaps it in
+    for those calls.  Every call runs on the communicator's own stream (the kernel's slot
+    protocol needs ONE stream and ONE grid size per communicator) ordered after the caller's
+    stream; ``async_op=True`` returns a handle whose ``wait()`` orders the caller's stream after
+    it, else the caller's stream is ordered immediately.  CPU tensors, other dtypes and sizes
+    outside the buffer fall back to ``torch.distributed`` (gloo / RCCL).
+
+        st.tp_comm = TwoShot(st.tp_group)      # collective over the TP group
+        tp_reduce_scatter_rows(x, st)          # now runs the two-shot kernel
+    """
+
+    def __init__(self, group=None, max_bytes: int = 288 << 20, blocks: int = 64):
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        assert self.world in (1, 2, 4, 8), "two-shot collectives support 1, 2, 4 or 8 ranks"
+        self.max_bytes = int(max_bytes) // (16 * self.world) * (16 * self.world)
+        self.blocks = max(1, min(int(blocks), 64))
+        k = _ext.ops()
+        self._own, handle = k.ts_alloc(self.max_bytes, self.world)
+        handles: List[Optional[torch.Tensor]] = [None] * self.world
+        dist.all_gather_object(handles, handle, group=group)
+        self.ptrs, self._opened = [], []
+        for r, h in enumerate(handles):
+            if r == self.rank:
+                self.ptrs.append(self._own)
+            else:
+                p = k.car_open(h)
+                self._opened.append(p)
+                self.ptrs.append(p)
+        self.stream = torch.cuda.Stream()
+        dist.barrier(group=group)
+        self.failed = False
+        self.calls = 0
+
+    def supports(self, full_numel: int, x: torch.Tensor) -> bool:
+        return (x.is_cuda and x.dtype == torch.bfloat16 and full_numel % (8 * self.world) == 0
+                and 2 * full_numel <= self.max_bytes)
+
+    def _run(self, mode: int, x: torch.Tensor, out: torch.Tensor, async_op: bool):
+        cur = torch.cuda.current_stream()
+        x = x.contiguous()
+        self.stream.wait_stream(cur)
+        with torch.cuda.stream(self.stream):
+            _ext.ops().ts_run(mode, self.ptrs, self.rank, x, out, self.max_bytes, self.blocks)
+        # both stay allocated until the comm stream has used them
+        x.record_stream(self.stream)
+        out.record_stream(self.stream)
+        self.calls += 1
+        ev = torch.cuda.Event()
+        ev.record(self.stream)
+        done = _Done(ev)
+        if not async_op:
+            done.wait()
+        return done
+
+    def all_reduce(self, x: torch.Tensor, async_op: bool = False):
+        """In place, as ``dist.all_reduce``; returns a work handle (``async_op``) or None."""
+        if not (x.is_contiguous() and self.supports(x.numel(), x)):
+            return dist.all_reduce(x, group=self.group, async_op=async_op)
+        w = self._run(0, x, x, async_op)
+        return w if async_op else None
+
+    def reduce_scatter(self, out: torch.Tensor, x: torch.Tensor, async_op: bool = False):
+        """``dist.reduce_scatter_tensor(out, x)``: out = rank r's 1/N block of the sum."""
+        if not (out.is_contiguous() and self.supports(x.numel(), x)):
+            return dist.reduce_scatter_tensor(out, x, group=self.group, async_op=async_op)
+        w = self._run(1, x, out, async_op)
+        return w if async_op else None
+
+    def all_gather(self, out: torch.Tensor, x: torch.Tensor, async_op: bool = False):
+        """``dist.all_gather_into_tensor(out, x)``: out = every rank's x in rank order."""
+        if not (out.is_contiguous() and self.supports(out.numel(), x)):
+            return dist.all_gather_into_tensor(out, x, group=self.group, async_op=async_op)
+        w = self._run(2, x, out, async_op)
+        return w if async_op else None
+
+    def check(self):
+        """Raise if a call since the last check timed out waiting for a peer (the
+        communicator is then out of step for good, as the one-shot one)."""
+        if self.failed or int(_ext.ops().ts_error(self._own)):
+            self.failed = True
+            raise RuntimeError("two-shot TP collective: a peer did not arrive within the spin budget; "
+                               "results since the last check are invalid (restart the job)")
+
+    def close(self):
+        k = _ext.ops()
+        torch.cuda.synchronize()
+        for p in self._opened:
+            k.car_close(p)
+        self._opened = []
+        if self._own:
+            k.car_free(self._own)
+            self._own = 0
+
+
+def make_tp_comm(kind: str, st):
+    """The TP communicator a trainer installs as ``st.tp_comm``: ``"twoshot"`` -> :class:`TwoShot`
+    over ``st.tp_group`` when the ranks drive GPUs (fails loudly if the HIP extension is missing);
+    ``"rccl"``, tp == 1 or a CPU (gloo) job -> None, i.e. plain ``torch.distributed``."""
+    if kind not in ("rccl", "twoshot"):
+        raise ValueError(f"tp_comm must be 'rccl' or 'twoshot', not {kind!r}")
+    if kind == "rccl" or st.tp == 1 or st.device.type != "cuda":
+        return None
+    return TwoShot(st.tp_group)

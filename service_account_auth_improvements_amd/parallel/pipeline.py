@@ -488,6 +488,8 @@ class PipelineTrainer:
         self.model.sequence_parallel = getattr(tcfg, "sequence_parallel", False)
         if self.st.tp > 1:
             self.model.tp_comm_chunks = getattr(tcfg, "tp_comm_chunks", self.model.tp_comm_chunks)
+            from .custom_ar import make_tp_comm
+            self.st.tp_comm = make_tp_comm(getattr(tcfg, "tp_comm", "rccl"), self.st)
         assert not getattr(tcfg, "context_parallel", False), "context parallelism is not combined with PP"
         zero1 = getattr(tcfg, "zero1", False)
         force = getattr(tcfg, "force_collectives", False)

@@ -36,6 +36,9 @@ class ParallelState:
     pp_next: Optional[int] = None
     device: torch.device = torch.device("cpu")
     backend: str = "none"
+    # TP collective backend: None = torch.distributed (RCCL / gloo); a parallel.custom_ar.TwoShot
+    # takes the TP reduce-scatter / all-gather / all-reduce it supports (runtime.trainer tp_comm)
+    tp_comm: Optional[object] = None
 
     @property
     def is_first_stage(self):
@@ -86,6 +89,14 @@ def visible_gpu_count() -> int:
     return n
 
 
+def local_device_index(local_rank: Optional[int] = None) -> int:
+    """The GPU index a rank with ``LOCAL_RANK`` uses (one rank per GPU; the gloo several-ranks-
+    per-GPU rehearsal wraps around) -- shared by :func:`init_distributed` and the trainer's
+    device warm-up thread, so both touch the same device."""
+    local = int(os.environ.get("LOCAL_RANK", "0")) if local_rank is None else local_rank
+    return local % max(1, torch.cuda.device_count())
+
+
 def init_distributed(tp: int = 1, pp: int = 1, backend: Optional[str] = None,
                      device: Optional[str] = None, timeout_s: int = 1800) -> ParallelState:
     """Initialise the default process group from torchrun env vars (RANK, WORLD_SIZE,
@@ -107,7 +118,7 @@ def init_distributed(tp: int = 1, pp: int = 1, backend: Optional[str] = None,
             # (KFAMD_DIST_BACKEND=gloo is the explicit several-ranks-per-GPU rehearsal)
             raise RuntimeError(f"LOCAL_RANK {local} but only {ndev} visible GPU(s): one rank per GPU "
                                f"needs {local + 1}")
-        idx = local % max(1, ndev)
+        idx = local_device_index(local)
         torch.cuda.set_device(idx)
         dev = torch.device("cuda", idx)
     else:
@@ -166,8 +177,29 @@ def set_state(st: ParallelState):
 def tp_all_reduce(x: torch.Tensor, st: Optional[ParallelState] = None) -> torch.Tensor:
     st = st or get_state()
     if st.tp > 1:
-        dist.all_reduce(x, group=st.tp_group)
+        tp_all_reduce_work(x, st, async_op=False)
     return x
+
+
+def tp_all_reduce_work(x: torch.Tensor, st: ParallelState, async_op: bool = True):
+    """In-place TP all-reduce on ``st.tp_comm`` (two-shot) or ``torch.distributed``."""
+    if st.tp_comm is not None:
+        return st.tp_comm.all_reduce(x, async_op=async_op)
+    return dist.all_reduce(x, group=st.tp_group, async_op=async_op)
+
+
+def tp_reduce_scatter_into(out: torch.Tensor, x: torch.Tensor, st: ParallelState, async_op: bool = True):
+    """``dist.reduce_scatter_tensor`` over the TP group, on ``st.tp_comm`` when it is set."""
+    if st.tp_comm is not None:
+        return st.tp_comm.reduce_scatter(out, x, async_op=async_op)
+    return dist.reduce_scatter_tensor(out, x, group=st.tp_group, async_op=async_op)
+
+
+def tp_all_gather_into(out: torch.Tensor, x: torch.Tensor, st: ParallelState, async_op: bool = True):
+    """``dist.all_gather_into_tensor`` over the TP group, on ``st.tp_comm`` when it is set."""
+    if st.tp_comm is not None:
+        return st.tp_comm.all_gather(out, x, async_op=async_op)
+    return dist.all_gather_into_tensor(out, x, group=st.tp_group, async_op=async_op)
 
 
 def _chunk_rows(n: int, chunks: int, tp: int) -> int:
@@ -193,8 +225,8 @@ def tp_all_gather_rows(x: torch.Tensor, st: Optional[ParallelState] = None, chun
     out = torch.empty((x.shape[0] * st.tp,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
     x = x.contiguous()
     n = x.shape[0] // c
-    works = [dist.all_gather_into_tensor(out[k * n * st.tp:(k + 1) * n * st.tp], x[k * n:(k + 1) * n],
-                                         group=st.tp_group, async_op=async_op) for k in range(c)]
+    works = [tp_all_gather_into(out[k * n * st.tp:(k + 1) * n * st.tp], x[k * n:(k + 1) * n], st, async_op)
+             for k in range(c)]
     return (out, works) if async_op else out
 
 
@@ -211,8 +243,8 @@ def tp_reduce_scatter_rows(x: torch.Tensor, st: Optional[ParallelState] = None, 
     out = torch.empty((x.shape[0] // st.tp,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
     x = x.contiguous()
     n = x.shape[0] // c
-    works = [dist.reduce_scatter_tensor(out[k * n // st.tp:(k + 1) * n // st.tp], x[k * n:(k + 1) * n],
-                                        group=st.tp_group, async_op=async_op) for k in range(c)]
+    works = [tp_reduce_scatter_into(out[k * n // st.tp:(k + 1) * n // st.tp], x[k * n:(k + 1) * n], st, async_op)
+             for k in range(c)]
     return (out, works) if async_op else out
 
 

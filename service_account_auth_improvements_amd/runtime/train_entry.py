@@ -80,7 +80,7 @@ def main(argv=None):
     t_start = time.time()
     _event("process_start")
     import torch
-    from ..parallel.state import init_distributed
+    from ..parallel.state import init_distributed, local_device_index
     from .trainer import SyntheticData, TrainConfig, Trainer
     _event("imported", seconds=time.time() - t_start)
 
@@ -92,8 +92,9 @@ def main(argv=None):
     warm = None
     if dev == "cuda" and os.environ.get("KFAMD_WARM", "1") != "0":
         import threading
-        warm = threading.Thread(target=_warm_device, args=(int(os.environ.get("LOCAL_RANK", "0")),),
-                                name="kfamd-warm", daemon=True)
+        # the device init_distributed will select (not the raw LOCAL_RANK, which differs in the
+        # several-ranks-per-GPU gloo rehearsal)
+        warm = threading.Thread(target=_warm_device, args=(local_device_index(),), name="kfamd-warm", daemon=True)
         warm.start()
     st = init_distributed(tp=a.tp, pp=a.pp, device=dev)
     _event("dist_ready", seconds=time.time() - t_start)

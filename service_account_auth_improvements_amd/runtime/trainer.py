@@ -15,6 +15,7 @@ import torch
 import torch.distributed as dist
 
 from ..models.llama import Llama, LlamaConfig
+from ..parallel.custom_ar import make_tp_comm
 from ..parallel.ddp import GradReducer
 from ..parallel.state import ParallelState, get_state
 from .optim import AdamWConfig, FlatAdamW
@@ -52,6 +53,10 @@ class TrainConfig:
     # TP forward communication overlap: token chunks per row-/column-parallel projection
     # (models/llama.py _row_parallel / _col_parallel); 1 = one GEMM + one blocking collective
     tp_comm_chunks: int = 4
+    # TP collective backend: "rccl" (torch.distributed) or "twoshot" (parallel/custom_ar.py TwoShot:
+    # peer-mapped reduce-scatter / all-gather over all xGMI links at once; GPU jobs only, a CPU
+    # job keeps torch.distributed)
+    tp_comm: str = "rccl"
     # TP forward: split each micro-batch into two half-batches whose layers are interleaved at
     # every TP collective, then one full-batch backward (models/llama.py stage_forward_dual);
     # needs an even micro-batch, one pipeline stage, no recomputation and no SP.
@@ -80,6 +85,7 @@ class Trainer:
         self.model.sequence_parallel = tcfg.sequence_parallel
         if self.st.tp > 1:
             self.model.tp_comm_chunks = getattr(tcfg, "tp_comm_chunks", self.model.tp_comm_chunks)
+            self.st.tp_comm = make_tp_comm(getattr(tcfg, "tp_comm", "rccl"), self.st)
         self.cp = self.st.dp if tcfg.context_parallel else 1
         if self.cp > 1:
             self.model.set_context_parallel(self.st.dp_group, self.st.dp, self.st.dp_rank)

@@ -93,7 +93,9 @@ def test_bench_refuses_world_size_mismatch():
                LOCAL_RANK="0")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", *ARGS],
                        capture_output=True, text=True, timeout=300, env=env, cwd="/tmp")
-    assert r.returncode != 0 and not _json_lines(r.stdout)
+    assert r.returncode != 0
+    recs = _json_lines(r.stdout)      # one diagnostic line, never a throughput number
+    assert len(recs) == 1 and recs[0]["value"] is None and "WORLD_SIZE=1" in recs[0]["error"]
 
 
 def test_bench_rehearsal_flag_marks_the_record():

@@ -229,3 +229,68 @@ def test_tp_dual_batch_forward_matches_plain_forward():
             assert abs(x - y) <= 1e-5 * abs(y), (a["losses"], b["losses"])
         for name in a["params"]:
             assert torch.allclose(a["params"][name], b["params"][name], rtol=0, atol=1e-6), name
+
+
+class _RecordingComm:
+    """Stands in for parallel.custom_ar.TwoShot on CPU: counts what the model routes to it and
+    delegates to torch.distributed (gloo)."""
+
+    def __init__(self, group):
+        self.group, self.calls = group, {"ar": 0, "rs": 0, "ag": 0}
+
+    def all_reduce(self, x, async_op=False):
+        import torch.distributed as dist
+        self.calls["ar"] += 1
+        return dist.all_reduce(x, group=self.group, async_op=async_op)
+
+    def reduce_scatter(self, out, x, async_op=False):
+        import torch.distributed as dist
+        self.calls["rs"] += 1
+        return dist.reduce_scatter_tensor(out, x, group=self.group, async_op=async_op)
+
+    def all_gather(self, out, x, async_op=False):
+        import torch.distributed as dist
+        self.calls["ag"] += 1
+        return dist.all_gather_into_tensor(out, x, group=self.group, async_op=async_op)
+
+
+def _comm_body(rank, world, sp, install):
+    from service_account_auth_improvements_amd.parallel.custom_ar import make_tp_comm
+    from service_account_auth_improvements_amd.parallel.state import init_distributed
+    from service_account_auth_improvements_amd.runtime.trainer import TrainConfig, Trainer
+    st = init_distributed(tp=world, pp=1, device="cpu")
+    # a CPU (gloo) job asking for the two-shot communicator keeps torch.distributed
+    tr = Trainer(TrainConfig(model="tiny", seq_len=32, micro_batch=2, n_layers=2, lr=LR, sequence_parallel=sp,
+                             tp_comm_chunks=4, tp_comm="twoshot"), st, full_init=True)
+    assert st.tp_comm is None and make_tp_comm("rccl", st) is None
+    rec = _RecordingComm(st.tp_group) if install else None
+    st.tp_comm = rec
+    losses = [float(tr.train_step(_batches(tr.mcfg.vocab_size, 1, seed=900 + s))) for s in range(STEPS)]
+    return dict(losses=losses, calls=rec.calls if rec else None,
+                params={s.name: tr.model.P(s.name).float() for g in tr.model.groups for s in g.specs})
+
+
+@pytest.mark.parametrize("sp", [False, True], ids=["tp2", "tp2+sp"])
+def test_tp_collectives_route_through_the_tp_communicator(sp):
+    """Every activation collective of the TP forward and backward (chunked row-parallel
+    reductions, SP all-gathers, async input-gradient reductions) goes to ``st.tp_comm`` when one
+    is installed (the two-shot kernel on GPU), with results identical to plain torch.distributed."""
+    plain = run_ranks(_comm_body, world=2, args=(sp, False))
+    routed = run_ranks(_comm_body, world=2, args=(sp, True))
+    for a, b in zip(plain, routed):
+        assert a["losses"] == b["losses"]
+        for name in a["params"]:
+            assert torch.equal(a["params"][name], b["params"][name]), name
+        c = b["calls"]
+        if sp:
+            assert c["rs"] > 0 and c["ag"] > 0
+        else:
+            assert c["ar"] > 0 and c["rs"] == 0 and c["ag"] == 0
+
+
+def test_make_tp_comm_rejects_unknown_backends():
+    from service_account_auth_improvements_amd.parallel.custom_ar import make_tp_comm
+    from service_account_auth_improvements_amd.parallel.state import ParallelState
+    with pytest.raises(ValueError):
+        make_tp_comm("nvls", ParallelState(tp=2))
+    assert make_tp_comm("twoshot", ParallelState(tp=1)) is None

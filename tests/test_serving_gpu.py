@@ -47,6 +47,58 @@ def test_decode_attn(B, Hq, Hkv, Lmax, lens):
     assert err < 2e-2, err
 
 
+@pytest.mark.parametrize("B,Lmax,lens", [(1, 1024, [1024]), (1, 8192, [8192]), (1, 8192, [1]),
+                                        (4, 1024, [1024, 1, 517, 33]), (4, 8192, [8192, 4096, 100, 7777]),
+                                        (2, 4096, [16, 17])])
+def test_decode_attn_fused_matches_two_kernel_and_fp32(B, Lmax, lens, monkeypatch):
+    """The small-batch single-launch kernel (split-K + last-arriver merge) against the
+    two-kernel form and the fp32 reference at B = 1 / 4, contexts up to 8k (Llama-3-8B heads)."""
+    assert _ext.load()
+    Hq, Hkv = 32, 8
+    g = torch.Generator(device="cpu").manual_seed(B * 131 + Lmax)
+    kc = torch.randn(B + 1, Hkv, Lmax, 128, generator=g).to(DEV, torch.bfloat16)
+    vc = torch.randn(B + 1, Hkv, Lmax, 128, generator=g).to(DEV, torch.bfloat16)
+    qkv = torch.randn(B, (Hq + 2 * Hkv) * 128, generator=g).to(DEV, torch.bfloat16)
+    slots = torch.arange(1, B + 1, dtype=torch.int32, device=DEV)
+    lengths = torch.tensor(lens, dtype=torch.int32, device=DEV)
+    monkeypatch.setenv("KFAMD_DECODE_FUSED", "1")
+    fused = decode_attention(qkv, kc, vc, slots, lengths, Hq)
+    monkeypatch.setenv("KFAMD_DECODE_FUSED", "0")
+    two = decode_attention(qkv, kc, vc, slots, lengths, Hq)
+    ref = _ref_decode(qkv, kc, vc, slots, lengths, Hq)
+    assert (fused.float().cpu() - ref).abs().max().item() < 2e-2
+    assert (fused.float() - two.float()).abs().max().item() < 2e-2
+
+
+def test_decode_attn_fused_in_a_graph_rearms_its_tickets():
+    """Captured once, replayed many times with changing lengths: each replay's last-arriving
+    block re-arms the tickets, so every replay matches an eager call."""
+    Hq, Hkv, Lmax = 32, 8, 2048
+    g = torch.Generator(device="cpu").manual_seed(9)
+    kc = torch.randn(2, Hkv, Lmax, 128, generator=g).to(DEV, torch.bfloat16)
+    vc = torch.randn(2, Hkv, Lmax, 128, generator=g).to(DEV, torch.bfloat16)
+    qkv = torch.randn(1, (Hq + 2 * Hkv) * 128, generator=g).to(DEV, torch.bfloat16)
+    slots = torch.tensor([1], dtype=torch.int32, device=DEV)
+    lengths = torch.tensor([5], dtype=torch.int32, device=DEV)
+    decode_attention(qkv, kc, vc, slots, lengths, Hq)            # allocates the tickets (outside capture)
+    s = torch.cuda.Stream(device=DEV)
+    s.wait_stream(torch.cuda.current_stream())
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        decode_attention(qkv, kc, vc, slots, lengths, Hq)
+        with torch.cuda.graph(graph):
+            out = decode_attention(qkv, kc, vc, slots, lengths, Hq)
+    torch.cuda.synchronize()
+    for L in (1, 33, 1024, 2048, 700, 1):
+        lengths.fill_(L)
+        graph.replay()
+        torch.cuda.synchronize()
+        eager = decode_attention(qkv, kc, vc, slots, lengths, Hq)
+        assert torch.equal(out, eager), L
+        ref = _ref_decode(qkv, kc, vc, slots, lengths, Hq)
+        assert (out.float().cpu() - ref).abs().max().item() < 2e-2, L
+
+
 def test_kv_append_and_fill():
     Hq, Hkv, Lmax = 8, 2, 64
     kc = torch.zeros(4, Hkv, Lmax, 128, device=DEV, dtype=torch.bfloat16)
