@@ -57,6 +57,9 @@ BGEMM_MIN_ROWS, BGEMM_MAX_ROWS = 33, 128   # at 32 rows its reduce launch costs 
 # prompts admitted in one scheduler iteration are prefilled together up to this many tokens
 PREFILL_MAX_TOKENS = int(os.environ.get("KFAMD_PREFILL_MAX_TOKENS", "16384"))
 PREFILL_PAD_RATIO = 1.25      # ... in length groups padded to at most 1.25x
+# batch 1: the whole decode step as ONE persistent kernel (ops/csrc/decode_step.hip) where the
+# model is its shape; KFAMD_DECODE_PERSISTENT=0 keeps the kernel-per-op graph (A/B, fallback)
+PERSISTENT_DECODE = os.environ.get("KFAMD_DECODE_PERSISTENT", "1") != "0"
 # hipBLASLt/rocBLAS solutions for the decode GEMM shapes above SKINNY_MAX_ROWS where the library
 # heuristic picks a poor kernel (tools/tune_decode_gemm.py; only the shapes that measured >= 5 %
 # faster HBM-cold are kept, profiles/serve_large_batch.md).  Loaded into PyTorch TunableOp with
@@ -77,6 +80,54 @@ def _load_tuned_decode_gemms(dev, cfg, tp: int) -> bool:
     tn.tuning_enable(False)           # never tune inside a serving process
     tn.read_file(path)
     return True
+
+
+class PersistentDecode:
+    """Batch-1 decode step as one persistent launch (ops/csrc/decode_step.hip): 256 workgroups,
+    one per CU, stream every weight byte of the step once by LDS-DMA while grid barriers order
+    the layer's phases.  Built for Llama-3-8B at TP 1 on a 256-CU MI355X; ``build`` returns
+    None for anything else.  The kernel's grid barriers are bounded: a timed-out step sets the
+    error word (``failed()``), the engine disables this path and recomputes the step."""
+
+    def __init__(self, engine: "Engine"):
+        from ..ops import _ext
+        m, cfg = engine.m, engine.cfg
+        self.k = _ext.ops()
+        dev = engine.dev
+        rows = []
+        for li, i in enumerate(m.layers):
+            rows.append([m.P(f"l{i}.wqkv").data_ptr(), m.P(f"l{i}.wo").data_ptr(), m.P(f"l{i}.wgu").data_ptr(),
+                         m.P(f"l{i}.wd").data_ptr(), m.P(f"l{i}.norm1").data_ptr(), m.P(f"l{i}.norm2").data_ptr(),
+                         engine.kc[li].data_ptr(), engine.vc[li].data_ptr()])
+        self.tab = torch.tensor(rows, dtype=torch.int64, device=dev)
+        self.ws = torch.zeros(int(self.k.decode_step_ws_bytes()), dtype=torch.uint8, device=dev)
+        off = int(self.k.decode_step_err_offset())
+        self.err = self.ws[off:off + 4].view(torch.int32)
+        self.logits = torch.empty(m.P("lm_head").shape[0], dtype=torch.bfloat16, device=dev)
+        self.cfg, self.m, self.lmax = cfg, m, engine.max_len
+
+    @staticmethod
+    def supported(engine: "Engine") -> bool:
+        m, cfg = engine.m, engine.cfg
+        return (PERSISTENT_DECODE and engine.dev.type == "cuda" and m.tp == 1 and m.first and m.last
+                and (cfg.hidden, cfg.ffn, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim) == (4096, 14336, 32, 8, 128)
+                and len(m.layers) <= 32 and m.P("lm_head").shape[0] % 256 == 0)
+
+    @classmethod
+    def build(cls, engine: "Engine"):
+        return cls(engine) if cls.supported(engine) else None
+
+    def __call__(self, tokens, slots, pos):
+        """Launch one step for row 0 (token, slot, pos: device [1] tensors); returns logits
+        [1, V] or None when the kernel refused the shape / device (nothing launched)."""
+        m, cfg = self.m, self.cfg
+        rc = self.k.decode_step(self.tab, cfg.hidden, cfg.ffn, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim,
+                                m.P("embed"), m.P("final_norm"), m.P("lm_head"), m.cos, m.sin, tokens, slots, pos,
+                                self.lmax, float(cfg.norm_eps), 1.0 / math.sqrt(cfg.head_dim), self.ws, self.logits)
+        return self.logits.view(1, -1) if rc == 0 else None
+
+    def failed(self) -> bool:
+        return int(self.err.item()) != 0
 
 
 class Engine:
@@ -101,6 +152,7 @@ class Engine:
         if model.tp > 1 and self.dev.type == "cuda":
             from ..parallel.custom_ar import OneShotAllReduce
             self.car = OneShotAllReduce(model.st.tp_group)
+        self.persist = PersistentDecode.build(self)
         self._graphs: Dict[int, tuple] = {}
         self._staging: Dict[int, tuple] = {}   # bucket -> (pinned host [3, Bb], device [3, Bb], copy-done event)
 
@@ -224,6 +276,11 @@ class Engine:
 
     def _decode_body(self, tokens, slots, pos, lengths):
         m, cfg = self.m, self.cfg
+        if self.persist is not None and tokens.shape[0] == 1:
+            out = self.persist(tokens, slots, pos)
+            if out is not None:
+                return out
+            self.persist = None             # refused (device / shape): kernel-per-op from now on
         r = self._embed(tokens)
         d = None
         for li, i in enumerate(m.layers):
@@ -278,6 +335,9 @@ class Engine:
             p = torch.tensor(pos, dtype=torch.int32, device=dev)
             out = self._decode_body(t, sl, p, p + 1)
             self._check_comm()
+            if B == 1 and self.persist is not None and self.persist.failed():
+                self.persist = None
+                return self.decode(tokens, slots, pos)
             return out
         Bb = next((b for b in BUCKETS if b >= B), None)
         if Bb is None:
@@ -306,6 +366,12 @@ class Engine:
         gl.copy_(dev_rows[2] + 1)
         graph.replay()
         self._check_comm()
+        if Bb == 1 and self.persist is not None and self.persist.failed():
+            # a grid barrier timed out (a CU never arrived): drop the persistent path, rebuild the
+            # bucket's graph kernel-per-op and recompute this step (it rewrites the step's K/V)
+            self.persist = None
+            self._graphs.pop(1, None)
+            return self.decode(tokens, slots, pos)
         return out[:B]
 
     def _check_comm(self):

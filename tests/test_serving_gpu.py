@@ -314,3 +314,50 @@ def test_bgemm_decode_shapes_and_strided_rows():
         ref = torch.mm(x.float(), w.float().t())
         err = ((y.float() - ref).abs().max() / ref.abs().max()).item()
         assert err < 1e-2, (N, K, err)
+
+
+def _llama8b_engine(n_layers, use_graphs, max_len=4096):
+    from service_account_auth_improvements_amd.serving.engine import build_engine
+    return build_engine("llama3-8b", device=DEV, n_slots=2, max_len=max_len, n_layers=n_layers, use_graphs=use_graphs)
+
+
+@pytest.mark.parametrize("ctx", [64, 3000])
+def test_persistent_decode_step_matches_kernel_per_op(ctx):
+    """The batch-1 persistent decode kernel (ops/csrc/decode_step.hip) against the kernel-per-op
+    decode path on the same KV cache, Llama-3-8B shapes (2 layers), short and long context."""
+    e = _llama8b_engine(2, use_graphs=False)
+    assert e.persist is not None, "persistent decode path not selected for Llama-3-8B at TP 1"
+    persist = e.persist
+    g = torch.Generator().manual_seed(ctx)
+    prompt = torch.randint(0, e.cfg.vocab_size, (ctx,), generator=g).tolist()
+    tok = int(e.prefill(0, prompt).float().argmax())
+    for step in range(4):
+        pos = ctx + step
+        e.persist = None
+        ref = e.decode([tok], [0], [pos]).float()
+        e.persist = persist
+        got = e.decode([tok], [0], [pos]).float()
+        assert e.persist is persist and not persist.failed()
+        cos = torch.nn.functional.cosine_similarity(got.flatten(), ref.flatten(), dim=0)
+        assert cos > 0.999, (step, float(cos))
+        assert (got - ref).abs().max() <= 0.05 * ref.abs().max(), (step, float((got - ref).abs().max()))
+        tok = int(ref.argmax())
+
+
+def test_persistent_decode_step_in_a_graph_replays_identically():
+    """Captured in the bucket-1 HIP graph (memset + kernel nodes), replays give the eager
+    persistent kernel's logits bit for bit, step after step."""
+    eg = _llama8b_engine(2, use_graphs=True, max_len=1024)
+    ee = _llama8b_engine(2, use_graphs=False, max_len=1024)
+    assert eg.persist is not None and ee.persist is not None
+    prompt = list(range(10, 74))
+    tg = int(eg.prefill(0, prompt).float().argmax())
+    te = int(ee.prefill(0, prompt).float().argmax())
+    assert tg == te
+    for step in range(6):
+        pos = len(prompt) + step
+        lg = eg.decode([tg], [0], [pos]).clone()
+        le = ee.decode([te], [0], [pos]).clone()
+        assert torch.equal(lg, le), step
+        tg = te = int(le.float().argmax())
+    assert not eg.persist.failed()

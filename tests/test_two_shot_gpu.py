@@ -83,7 +83,7 @@ def _train_body(rank, world, kind, sp):
     v = tr.mcfg.vocab_size
     losses = []
     for _ in range(2):
-        b = [(torch.randint(0, v, (2, 64), generator=g), torch.randint(0, v, (2, 64), generator=g))]
+        b = [(torch.randint(0, v, (2, 64), generator=g).cuda(), torch.randint(0, v, (2, 64), generator=g).cuda())]
         losses.append(float(tr.train_step(b)))
     torch.cuda.synchronize()
     st.tp_comm.check()
@@ -104,7 +104,7 @@ def test_two_shot_tp2_training_matches_one_rank(sp):
     v = tr.mcfg.vocab_size
     ref = []
     for _ in range(2):
-        b = [(torch.randint(0, v, (2, 64), generator=g), torch.randint(0, v, (2, 64), generator=g))]
+        b = [(torch.randint(0, v, (2, 64), generator=g).cuda(), torch.randint(0, v, (2, 64), generator=g).cuda())]
         ref.append(float(tr.train_step(b)))
     (l0, c0), (l1, c1) = res
     assert l0 == l1                       # both ranks computed the same bits

@@ -69,8 +69,10 @@ def main():
             e.decode(toks, slots, [a.ctx + k] * B)
         torch.cuda.synchronize()
         dt = (time.time() - t0) / a.steps
+        path = "persistent" if (B == 1 and getattr(e, "persist", None) is not None) else "kernel-per-op graph"
         print(json.dumps({"bench": "decode", "model": a.model, "batch": B, "context": a.ctx,
-                          "ms_per_step": round(1e3 * dt, 3), "tokens_per_s": round(B / dt, 1)}), flush=True)
+                          "ms_per_step": round(1e3 * dt, 3), "tokens_per_s": round(B / dt, 1),
+                          "decode_path": path}), flush=True)
     # decode-attention kernel alone: HBM bytes of K+V read per call
     from service_account_auth_improvements_amd.ops.attention import decode_attention
     m = e.m
