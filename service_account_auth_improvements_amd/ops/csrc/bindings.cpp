@@ -73,8 +73,9 @@ int kf_car_error(void*, hipStream_t);
 long kf_ts_header_bytes();
 long kf_decode_step_ws_bytes();
 long kf_decode_step_err_offset();
-int kf_decode_step(const void*, int, int, int, int, int, int, int, const void*, const void*, const void*, const float*,
-                   const float*, const long*, const int*, const int*, int, float, float, void*, void*, hipStream_t);
+int kf_decode_step(const void*, int, int, int, int, int, int, int, int, const void*, const void*, const void*,
+                   const float*, const float*, const long*, const int*, const int*, int, float, float, void*, void*,
+                   hipStream_t);
 int kf_ts_alloc(long, int, void**, void*);
 int kf_ts_run(int, void* const*, int, int, const void*, void*, long, long, int, hipStream_t);
 int kf_ts_error(void*, hipStream_t);
@@ -383,10 +384,11 @@ at::Tensor decode_attn(const at::Tensor& q2d, const at::Tensor& kc, const at::Te
   return out;
 }
 
-// Batch-1 decode step as one persistent launch (ops/csrc/decode_step.hip).  tab: int64 [L, 8]
-// device pointers per layer (wqkv, wo, wgu, wd, norm1, norm2, k cache, v cache); ws: uint8
-// workspace of decode_step_ws_bytes(); logits: bf16 [V].  Returns the kernel's rc (0 = launched,
-// else the model / device is not the shape it is built for and nothing ran).
+// Decode step for 1-4 rows as one persistent launch (ops/csrc/decode_step.hip).  tab: int64 [L, 8]
+// device pointers per layer (wqkv, wo, wgu, wd, norm1, norm2, k cache, v cache); token int64 [M],
+// slot / pos int32 [M]; ws: uint8 workspace of decode_step_ws_bytes(); logits: bf16 [M, V].
+// Returns the kernel's rc (0 = launched, else the model / device is not the shape it is built
+// for and nothing ran).
 int64_t decode_step_ws_bytes() { return kf_decode_step_ws_bytes(); }
 int64_t decode_step_err_offset() { return kf_decode_step_err_offset(); }
 
@@ -402,17 +404,19 @@ int64_t decode_step(const at::Tensor& tab, int64_t hidden, int64_t ffn, int64_t 
   check_bf16_cuda(logits, "logits");
   TORCH_CHECK(embed.is_contiguous() && lm.is_contiguous() && fnorm.is_contiguous() && logits.is_contiguous(),
               "decode_step: contiguous weights");
-  TORCH_CHECK(lm.dim() == 2 && lm.size(1) == hidden && logits.numel() == lm.size(0), "decode_step: lm_head / logits");
+  const int64_t M = token.numel();
+  TORCH_CHECK(lm.dim() == 2 && lm.size(1) == hidden && logits.numel() == M * lm.size(0), "decode_step: lm_head / logits");
   TORCH_CHECK(cos.is_cuda() && cos.scalar_type() == at::kFloat && sin.is_cuda() && sin.scalar_type() == at::kFloat &&
                   cos.is_contiguous() && sin.is_contiguous() && cos.size(-1) == 64 && cos.numel() >= lmax * 64,
               "decode_step: fp32 RoPE tables [max_seq, 64] covering lmax");
-  TORCH_CHECK(token.is_cuda() && token.scalar_type() == at::kLong && token.numel() == 1, "decode_step: token int64 [1]");
-  check_rows_i32(slot, 1, "slot");
-  check_rows_i32(pos, 1, "pos");
+  TORCH_CHECK(token.is_cuda() && token.scalar_type() == at::kLong && token.is_contiguous() && M >= 1 && M <= 4,
+              "decode_step: token int64 [1..4]");
+  check_rows_i32(slot, M, "slot");
+  check_rows_i32(pos, M, "pos");
   TORCH_CHECK(ws.is_cuda() && ws.scalar_type() == at::kByte && ws.numel() >= kf_decode_step_ws_bytes(),
               "decode_step: workspace too small");
   c10::hip::HIPGuardMasqueradingAsCUDA g(logits.device());
-  return kf_decode_step(tab.data_ptr(), (int)tab.size(0), (int)hidden, (int)ffn, (int)hq, (int)hkv, (int)hd,
+  return kf_decode_step(tab.data_ptr(), (int)tab.size(0), (int)M, (int)hidden, (int)ffn, (int)hq, (int)hkv, (int)hd,
                         (int)lm.size(0), embed.data_ptr(), fnorm.data_ptr(), lm.data_ptr(), cos.data_ptr<float>(),
                         sin.data_ptr<float>(), (const long*)token.data_ptr<int64_t>(), slot.data_ptr<int>(),
                         pos.data_ptr<int>(), (int)lmax, (float)eps, (float)scale, ws.data_ptr(), logits.data_ptr(),

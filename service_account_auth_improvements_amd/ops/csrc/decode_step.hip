@@ -1,36 +1,38 @@
-// Batch-1 decode step as ONE persistent launch (VERDICT r3 "Next round" #5).
+// Small-batch decode step (1-4 sequences) as ONE persistent launch (VERDICT r3
+// "Next round" #5).
 //
-// At batch 1 a Llama-3-8B token is a 16 GB weight stream with a dependency chain on top:
+// At batch 1-4 a Llama-3-8B token step is a 16 GB weight stream with a dependency chain on top:
 // norm -> QKV -> RoPE / KV append -> attention -> O -> norm -> gate/up + SwiGLU -> down, 32 times,
 // then the LM head.  As graph-captured kernels (gemv.hip, decode_attn.hip, ...) every one of the
 // ~160 launches pays a grid fill / drain and a ~1.2 us boundary, and the short ones (wo: 33 MB)
 // never reach the HBM rate.  Here one workgroup per CU (256 x 512 threads) walks the whole step:
 //
 //  * Weight stream: each WG owns a fixed slice of every projection (QKV 12 RoPE pairs = 24 rows,
-//    O 16 rows, gate/up 56 + 56 rows, down 16 rows, LM head V/256 rows), so its weight bytes for
-//    the WHOLE step are a sequence of 8 KB stages known before any activation exists.  Each of
-//    the 8 waves streams its own 1 KB piece of every stage by LDS-DMA (global_load_lds_dwordx4
-//    nt) into a private ring slot, RS stages ahead, and consumes exactly the piece it loaded: no
-//    workgroup barrier or handshake in the stream, one counted vmcnt per stage.  The ring runs
-//    across phase and layer seams, so while a WG waits at a grid barrier or computes attention
-//    its next RS stages keep arriving (the "prefetch credit" of a run-ahead loader).
-//  * Activations never leave the chip's caches: the residual stream is tracked by EVERY WG
-//    redundantly in LDS (bf16, as the kernel-per-op path rounds it), the normalised GEMV operand
-//    is staged in LDS once per phase, and the five per-layer hand-offs (q/k/v, attention output,
-//    O output, SwiGLU output, down output) go through small global buffers.
+//    O 16 rows, gate/up 56 + 56 rows, down 64 rows x a quarter of K, LM head V/256 rows), and each
+//    of its 8 waves owns every 8th of those rows, so a wave's weight bytes for the WHOLE step are
+//    a sequence of 1 KB pieces known before any activation exists.  The wave streams them by
+//    LDS-DMA (global_load_lds_dwordx4 nt) into a private ring of RS slots and consumes exactly the
+//    pieces it loaded: no workgroup barrier or handshake in the stream, one counted vmcnt per
+//    piece, one wave reduction per row.  The ring runs across phase and layer seams, so while a WG
+//    waits at a grid barrier or computes attention its next RS pieces per wave keep arriving.
+//  * Activations stay in the caches: every WG tracks the residual stream of the M rows itself in
+//    LDS (bf16, as the kernel-per-op path rounds it), stages the normalised GEMV operand in LDS
+//    once per phase, and the per-layer hand-offs (q/k/v, attention output, O output, SwiGLU
+//    output, down partials) go through small global buffers.  The down projection is split over
+//    K in quarters (its operand slice fits LDS at 4 rows); the next phase sums the 4 partials.
 //  * Hand-offs (MI355X_MICROARCH.md "Valid forms" row 1): producers store `sc1` (agent atomic
 //    stores), every storing wave drains (vmcnt 0), a workgroup barrier, then ONE lane adds to its
 //    shard of an 8-way sharded barrier counter; consumers poll every shard with `sc1` loads, join
 //    a workgroup barrier and read the bytes with `sc1` loads only.  The attention split merge is
-//    done by the last arriver of each kv head (its ticket add's return value), as in
+//    done by the last arriver of each (row, kv head) (its ticket add's return value), as in
 //    decode_attn.hip's fused kernel.  Every spin is bounded: a timeout sets the error word and
-//    every WG leaves after draining its DMA (the engine raises and falls back).
+//    every WG leaves after draining its DMA (the engine then falls back and recomputes the step).
 //  * Numerics follow the kernel-per-op path: bf16 residual, bf16 normalised operands, fp32 dot
 //    products (v_dot2c_f32_bf16), bf16 q/k/v with RoPE on the rounded values, fp32 online
 //    softmax, bf16 attention / SwiGLU / projection outputs; only the summation order differs.
 //
-// Shape: Llama-3-8B (hidden 4096, ffn 14336, 32 q / 8 kv heads of 128, vocab % 256 == 0), batch 1,
-// TP 1, 256 CUs.  Anything else keeps the kernel-per-op path (kf_decode_step returns non-zero).
+// Shape: Llama-3-8B (hidden 4096, ffn 14336, 32 q / 8 kv heads of 128, vocab % 256 == 0), TP 1,
+// 256 CUs.  Anything else keeps the kernel-per-op path (kf_decode_step returns non-zero).
 #include "common.h"
 
 using namespace kf;
@@ -40,22 +42,31 @@ namespace ds {
 constexpr int H = 4096, F = 14336, HQ = 32, HKV = 8, HD = 128, G = HQ / HKV;
 constexpr int NQKV = (HQ + 2 * HKV) * HD;          // 6144 qkv rows
 constexpr int NWG = 256, NT = 512, NW = NT / 64;   // one 8-wave workgroup per CU
-constexpr int PIECE = 1024, STAGE = NW * PIECE;    // a stage = 4096 bf16 = one K-4096 row
-constexpr int RS = 14;                             // ring stages (112 KB of LDS)
+constexpr int PIECE = 1024;                        // 512 bf16: one wave-instruction of LDS-DMA
+constexpr int PPR = H * 2 / PIECE;                 // 8 pieces per K-4096 row
 constexpr int PAIRS = NQKV / 2 / NWG;              // 12 RoPE pairs per WG
-constexpr int S_QKV = 2 * PAIRS;                   // 24
-constexpr int ROWS_O = H / NWG;                    // 16 (also the down rows)
-constexpr int ROWS_G = F / NWG;                    // 56 gate (+ 56 up) rows
-constexpr int S_O = ROWS_O, S_GU = 2 * ROWS_G, S_D = ROWS_O * F / 4096;
-constexpr int S_LAYER = S_QKV + S_O + S_GU + S_D;  // 208 stages = 1.66 MB per WG per layer
-constexpr int NS = NWG / HKV;                      // 32 key splits per kv head
-constexpr int MAXL = 32;
-constexpr int XS_BYTES = 2 * F;                    // staged operand (down: 14336 bf16)
+constexpr int R_QKV = 2 * PAIRS, R_O = H / NWG, R_G = F / NWG;   // 24, 16, 56 (+56 up) rows per WG
+constexpr int DKS = 4, KQ = F / DKS;               // down: K quarters of 3584 columns
+constexpr int PPD = KQ * 2 / PIECE;                // 7 pieces per down row segment
+constexpr int R_D = H / (NWG / DKS);               // 64 down row segments per WG
+constexpr int P_QKV = R_QKV / NW * PPR, P_O = R_O / NW * PPR, P_GU = 2 * R_G / NW * PPR, P_D = R_D / NW * PPD;
+constexpr int P_LAYER = P_QKV + P_O + P_GU + P_D;  // 208 pieces per wave per layer (1.66 MB per WG)
+constexpr int MAXL = 32, MAXM = 4;
+constexpr int MAXROWS_LM = 512;                    // V / 256 rows per WG
+constexpr int ATT_BYTES = (G * HD + 2 * HD + NW * G * HD + 2 * NW * G + 2 * 32 * G) * 4;
 constexpr int SHARD = 32;                          // ints between counters (128-B lines)
-constexpr int SYNC_INTS = 8 * SHARD + HKV * SHARD + SHARD;
+constexpr int N_TICKETS = MAXM * HKV;
+constexpr int SYNC_INTS = 8 * SHARD + N_TICKETS * SHARD + SHARD;
+constexpr int ERR_INT = (8 + N_TICKETS) * SHARD;
 constexpr unsigned SPIN_LIMIT = 1u << 23;
-static_assert(H == 4096 && F % 512 == 0 && (NQKV / 2) % NWG == 0 && PAIRS % 4 == 0, "stage geometry");
-static_assert((ROWS_O * F) % 4096 == 0 && ROWS_G % 2 == 0 && ROWS_O % 2 == 0, "row slices");
+static_assert(H == 4096 && F % (DKS * 512) == 0 && (NQKV / 2) % NWG == 0 && PAIRS % 4 == 0, "geometry");
+static_assert(R_QKV % NW == 0 && R_O % NW == 0 && (2 * R_G) % NW == 0 && R_D % NW == 0, "rows per wave");
+
+template <int M> struct Cfg;   // ring slots per wave (KB) and the staged-operand region per M
+template <> struct Cfg<1> { static constexpr int RS = 16; };
+template <> struct Cfg<2> { static constexpr int RS = 14; };
+template <> struct Cfg<3> { static constexpr int RS = 12; };
+template <> struct Cfg<4> { static constexpr int RS = 10; };
 
 struct Tab {                 // per layer, device memory (built once by the engine)
   const bf16_t *wqkv, *wo, *wgu, *wd, *n1, *n2;
@@ -64,24 +75,24 @@ struct Tab {                 // per layer, device memory (built once by the engi
 
 struct Args {
   const Tab* tab;
-  int L, V, lmax;
+  int L, V, lmax, ns;        // ns: key splits per (row, kv head)
   const bf16_t* embed;
   const bf16_t* fnorm;
   const bf16_t* lm;
   const float* cos_t;        // [max_seq, 64]
   const float* sin_t;
-  const long* token;         // device scalars (graph-static)
+  const long* token;         // [M] device (graph-static)
   const int* slot;
   const int* pos;
   float eps, scale_log2;
-  float* qkvf;               // [NQKV] bf16-exact q / k / v after RoPE
-  bf16_t* ob;                // [H] attention output
-  bf16_t* dab;               // [H] O projection
-  bf16_t* sb;                // [F] SwiGLU output
-  bf16_t* db;                // [H] down projection
-  float* part;               // [HKV][NS][G][HD + 2]
+  float* qkvf;               // [M][NQKV] bf16-exact q / k / v after RoPE
+  bf16_t* ob;                // [M][H] attention output
+  bf16_t* dab;               // [M][H] O projection
+  bf16_t* sb;                // [M][F] SwiGLU output
+  float* dpart;              // [DKS][M][H] down partial sums
+  float* part;               // [M][HKV][32][G][HD + 2] attention split partials
   int* sync;                 // SYNC_INTS, zero at launch
-  bf16_t* logits;            // [V]
+  bf16_t* logits;            // [M][V]
 };
 
 typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
@@ -129,13 +140,17 @@ __device__ __forceinline__ u32 ld_u(const bf16_t* p) {
   return __hip_atomic_load(reinterpret_cast<const u32*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+template <int M>
 __global__ __launch_bounds__(NT) void decode_step_kernel(Args a) {
-  __shared__ __attribute__((aligned(16))) char ring[RS * STAGE];
-  __shared__ __attribute__((aligned(16))) char xsb[XS_BYTES];
-  __shared__ __attribute__((aligned(16))) bf16_t rres[H];     // residual stream (bf16)
-  __shared__ float red[S_GU][NW];                              // per-row wave partials
+  constexpr int RS = Cfg<M>::RS;
+  constexpr int XS_BYTES = (M * H * 2 > ATT_BYTES ? M * H * 2 : ATT_BYTES);
+  __shared__ __attribute__((aligned(16))) char ring[NW * RS * PIECE];
+  __shared__ __attribute__((aligned(16))) char xsb[XS_BYTES];   // operand rows / attention scratch
+  __shared__ __attribute__((aligned(16))) bf16_t rres[M][H];    // residual stream (bf16)
+  __shared__ float outr[MAXROWS_LM][M];                          // row results of the current phase
   __shared__ const char* wtab[MAXL][4];
-  __shared__ float bsum[NW];
+  __shared__ float bsum[NW][M];
+  __shared__ int tok_sh[M], slot_sh[M], pos_sh[M];
   __shared__ int flag_sh;
   __shared__ int dead_sh;
   // the arguments live in LDS and are re-read where used (volatile): kept in SGPRs for the whole
@@ -144,11 +159,12 @@ __global__ __launch_bounds__(NT) void decode_step_kernel(Args a) {
   volatile Args& A = sa;
 
   int tid = threadIdx.x;    // re-made opaque every layer (below): no hoisted lane masks
-  const int lane = tid & 63;
+  int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   int g = blockIdx.x;
   const int L = a.L, rows_lm = a.V / NWG;
-  const int T = L * S_LAYER + rows_lm;                         // stages in this WG's stream
+  const int nlm = (rows_lm - wave + NW - 1) / NW;               // this wave's LM head rows
+  const int T = L * P_LAYER + nlm * PPR;                        // pieces in this wave's stream
   bf16_t* xs = reinterpret_cast<bf16_t*>(xsb);
 
   if (tid < 4 * L) {
@@ -156,52 +172,65 @@ __global__ __launch_bounds__(NT) void decode_step_kernel(Args a) {
     const int k = tid & 3;
     wtab[tid >> 2][k] = (const char*)(k == 0 ? tb.wqkv : k == 1 ? tb.wo : k == 2 ? tb.wgu : tb.wd);
   }
+  if (tid < M) {
+    tok_sh[tid] = (int)a.token[tid];
+    slot_sh[tid] = a.slot[tid];
+    pos_sh[tid] = a.pos[tid];
+  }
   if (tid == 0) {
     dead_sh = 0;
     sa = a;
   }
-  int token = (int)a.token[0], slot = a.slot[0], pos = a.pos[0];
   __syncthreads();
-  if (token < 0 || token >= a.V || slot < 0 || pos < 0 || pos >= a.lmax) {   // nothing issued yet
-    if (tid == 0) __hip_atomic_store(a.sync + (8 + HKV) * SHARD, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
+  {
+    bool bad = false;
+#pragma unroll
+    for (int m = 0; m < M; ++m)
+      bad |= tok_sh[m] < 0 || tok_sh[m] >= a.V || slot_sh[m] < 0 || pos_sh[m] < 0 || pos_sh[m] >= a.lmax;
+    if (bad) {                                                   // nothing issued yet
+      if (tid == 0) __hip_atomic_store(a.sync + ERR_INT, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
   }
 
-  // ---- the weight stream -------------------------------------------------------------------
-  const u32 ring0 = lds_u32(ring) + wave * PIECE;
+  // ---- the weight stream: this wave's pieces, in consumption order ---------------------------
+  const u32 ring0 = lds_u32(ring) + wave * RS * PIECE;
   const u32 voff = 16 * lane;
   const bf16_t* const lm = a.lm;
-  const char* const dummy = uniform_ptr((const char*)(lm + (long)g * rows_lm * H) + wave * PIECE);
+  const char* const dummy = uniform_ptr((const char*)(lm + (long)(g * rows_lm + wave) * H));
   auto piece = [&](int t) -> const char* {
     if (t >= T) return dummy;                                   // keeps the count uniform
-    const int lt = L * S_LAYER;
-    if (t >= lt) return (const char*)(lm + (long)(g * rows_lm + (t - lt)) * H) + wave * PIECE;
-    const int l = t / S_LAYER, u = t - l * S_LAYER;
-    long row;
-    int k;
-    if (u < S_QKV) {                                            // RoPE pair (p, p + 64) of a head
-      const int pr = g * PAIRS + (u >> 1);
-      row = (long)(pr >> 6) * HD + (pr & 63) + 64 * (u & 1);
-      k = 0;
-    } else if (u < S_QKV + S_O) {
-      row = (long)g * ROWS_O + (u - S_QKV);
-      k = 1;
-    } else if (u < S_QKV + S_O + S_GU) {
-      const int v = u - S_QKV - S_O;
-      row = v < ROWS_G ? (long)g * ROWS_G + v : (long)F + g * ROWS_G + (v - ROWS_G);
-      k = 2;
-    } else {                                                    // down: the WG's 16 rows are contiguous
-      const int v = u - S_QKV - S_O - S_GU;
-      return uniform_ptr(wtab[l][3]) + (long)g * ROWS_O * F * 2 + (long)v * STAGE + wave * PIECE;
+    const int lt = L * P_LAYER;
+    if (t >= lt) {
+      const int u = t - lt;
+      return (const char*)(lm + (long)(g * rows_lm + wave + NW * (u >> 3)) * H) + (u & 7) * PIECE;
     }
-    return uniform_ptr(wtab[l][k]) + row * (H * 2) + wave * PIECE;
+    const int l = t / P_LAYER, u = t - l * P_LAYER;
+    if (u < P_QKV) {                                            // RoPE pair (p, p + 64) of a head
+      const int i = wave + NW * (u >> 3), pr = g * PAIRS + (i >> 1);
+      const long row = (long)(pr >> 6) * HD + (pr & 63) + 64 * (i & 1);
+      return uniform_ptr(wtab[l][0]) + row * (H * 2) + (u & 7) * PIECE;
+    }
+    if (u < P_QKV + P_O) {
+      const int v = u - P_QKV;
+      const long row = (long)g * R_O + wave + NW * (v >> 3);
+      return uniform_ptr(wtab[l][1]) + row * (H * 2) + (v & 7) * PIECE;
+    }
+    if (u < P_QKV + P_O + P_GU) {
+      const int v = u - P_QKV - P_O, i = wave + NW * (v >> 3);
+      const long row = i < R_G ? (long)g * R_G + i : (long)F + g * R_G + (i - R_G);
+      return uniform_ptr(wtab[l][2]) + row * (H * 2) + (v & 7) * PIECE;
+    }
+    const int v = u - P_QKV - P_O - P_GU, seg = wave + NW * (v / PPD);
+    const long row = (long)(g / DKS) * R_D + seg;
+    return uniform_ptr(wtab[l][3]) + row * (F * 2) + (long)(g % DKS) * (KQ * 2) + (v % PPD) * PIECE;
   };
-  auto issue = [&](int t) { dma_piece(uniform_ptr(piece(t)), ring0 + (t % RS) * STAGE, voff); };
-  // stage t's piece of this wave (landed: RS - 1 younger DMAs may still be in flight); its slot
-  // is refilled with stage t + RS right after the read
+  auto issue = [&](int t) { dma_piece(uniform_ptr(piece(t)), ring0 + (t % RS) * PIECE, voff); };
+  // piece t of this wave (landed: RS - 1 younger DMAs may still be in flight); its slot is
+  // refilled with piece t + RS right after the read
   auto take = [&](int t) -> u32x4 {
     vm_wait<RS - 1>();
-    const u32x4 w = ring_read(ring0 + (t % RS) * STAGE + voff);
+    const u32x4 w = ring_read(ring0 + (t % RS) * PIECE + voff);
     issue(t + RS);
     return w;
   };
@@ -218,7 +247,7 @@ __global__ __launch_bounds__(NT) void decode_step_kernel(Args a) {
         unsigned spins = 0;
         while (__hip_atomic_load(A.sync + lane * SHARD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
           if (++spins > SPIN_LIMIT) {
-            __hip_atomic_store(A.sync + (8 + HKV) * SHARD, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(A.sync + ERR_INT, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             dead_sh = 1;
             break;
           }
@@ -230,89 +259,117 @@ __global__ __launch_bounds__(NT) void decode_step_kernel(Args a) {
     return dead_sh == 0;
   };
 
-  // ---- normalised operand: xs = bf16(r * rstd * w) over the residual in rres ----------------
+  // ---- normalised operands: xs[m] = bf16(r[m] * rstd[m] * w) over the residual rows ----------
   auto norm_into_xs = [&](const bf16_t* w) {
-    float ss = 0.f;
-    {
-      float hv[8];
-      unpack8(*reinterpret_cast<const u32x4*>(rres + 8 * tid), hv);
+    float hv[M][8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) ss += hv[e] * hv[e];
+    for (int m = 0; m < M; ++m) {
+      unpack8(*reinterpret_cast<const u32x4*>(&rres[m][8 * tid]), hv[m]);
+      float ss = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ss += hv[m][e] * hv[m][e];
+      ss = wave_sum(ss);
+      if (lane == 0) bsum[wave][m] = ss;
     }
-    ss = wave_sum(ss);
-    if (lane == 0) bsum[wave] = ss;
     __syncthreads();
-    float tot = 0.f;
-#pragma unroll
-    for (int v = 0; v < NW; ++v) tot += bsum[v];
-    const float rs = rsqrtf(tot / (float)H + A.eps);
-    float hv[8], wf[8];
-    unpack8(*reinterpret_cast<const u32x4*>(rres + 8 * tid), hv);
+    float wf[8];
     unpack8(ld16(w + 8 * tid), wf);
+#pragma unroll 2
+    for (int m = 0; m < M; ++m) {
+      float tot = 0.f;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) hv[e] = hv[e] * rs * wf[e];
-    *reinterpret_cast<u32x4*>(xs + 8 * tid) = pack8(hv);
-    __syncthreads();
-  };
-  // residual update: rres = bf16(rres + delta), delta a hand-off buffer (bf16)
-  auto residual_add = [&](const bf16_t* delta) {
-    float hv[8], dv[8];
-    unpack8(*reinterpret_cast<const u32x4*>(rres + 8 * tid), hv);
+      for (int v = 0; v < NW; ++v) tot += bsum[v][m];
+      const float rs = rsqrtf(tot / (float)H + A.eps);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const u32 v = ld_u(delta + 8 * tid + 2 * i);
-      dv[2 * i] = bflo(v);
-      dv[2 * i + 1] = bfhi(v);
-    }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) hv[e] += dv[e];
-    *reinterpret_cast<u32x4*>(rres + 8 * tid) = pack8(hv);
-    __syncthreads();
-  };
-  // K = 4096 projection: one stage per row, the wave's 512 columns of x fixed for the phase
-  auto gemv_rows = [&](int t0, int nst, float* redp) {
-    const u32x4 xv = *reinterpret_cast<const u32x4*>(xs + 512 * wave + 8 * lane);
-    for (int u = 0; u < nst; ++u) {
-      const u32x4 w = take(t0 + u);
-      const float p = wave_sum(dot8(w, xv, 0.f));
-      if (lane == 0) redp[u * NW + wave] = p;
+      for (int e = 0; e < 8; ++e) hv[m][e] = hv[m][e] * rs * wf[e];
+      *reinterpret_cast<u32x4*>(xs + m * H + 8 * tid) = pack8(hv[m]);
     }
     __syncthreads();
   };
-  auto row_total = [&](const float* redp, int r) {
-    float s = 0.f;
+  // residual update r[m] = bf16(r[m] + delta[m]); delta = bf16 hand-off rows, or (dpart) the
+  // bf16-rounded sum of the down projection's 4 K-quarter partials
+  auto residual_add = [&](const bf16_t* delta, const float* dpart) {
+#pragma unroll 1
+    for (int m = 0; m < M; ++m) {
+      float hv[8], dv[8];
+      unpack8(*reinterpret_cast<const u32x4*>(&rres[m][8 * tid]), hv);
+      if (dpart) {
 #pragma unroll
-    for (int v = 0; v < NW; ++v) s += redp[r * NW + v];
-    return s;
+        for (int e = 0; e < 8; ++e) {
+          float s = 0.f;
+#pragma unroll
+          for (int q = 0; q < DKS; ++q) s += ld_f(dpart + ((long)q * M + m) * H + 8 * tid + e);
+          dv[e] = bf2f(f2bf(s));
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const u32 v = ld_u(delta + (long)m * H + 8 * tid + 2 * i);
+          dv[2 * i] = bflo(v);
+          dv[2 * i + 1] = bfhi(v);
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) hv[e] += dv[e];
+      *reinterpret_cast<u32x4*>(&rres[m][8 * tid]) = pack8(hv);
+    }
+    __syncthreads();
+  };
+  // this wave's rows of a projection: nrows rows of ppr pieces each, the operand of piece j at
+  // xs[m * xld + 512 j + 8 lane]; row k's result -> outr[wave + 8 k][m]
+  auto gemv = [&](int t0, int nrows, int ppr, int xld) {
+#pragma unroll 1
+    for (int k = 0; k < nrows; ++k) {
+      float acc[M];
+#pragma unroll
+      for (int m = 0; m < M; ++m) acc[m] = 0.f;
+#pragma unroll 1
+      for (int j = 0; j < ppr; ++j) {
+        const u32x4 w = take(t0 + k * ppr + j);
+#pragma unroll
+        for (int m = 0; m < M; ++m)
+          acc[m] = dot8(w, *reinterpret_cast<const u32x4*>(xs + m * xld + 512 * j + 8 * lane), acc[m]);
+      }
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        const float s = wave_sum(acc[m]);
+        if (lane == 0) outr[wave + NW * k][m] = s;
+      }
+    }
+    __syncthreads();
   };
 
   int bar = 0;
   for (int l = 0; l < L; ++l) {
-    // Loop-invariant values (`tid < n` exec masks, offsets from g / pos / slot) hoisted out of
-    // the layer loop would pin ~40 SGPRs for the whole kernel and spill; made opaque once per
-    // iteration they are recomputed in the phase that uses them (a few SALU ops per layer)
-    asm volatile("" : "+v"(tid), "+s"(g), "+s"(pos), "+s"(slot));
+    // Loop-invariant values (`tid < n` exec masks, offsets from g) hoisted out of the layer loop
+    // would pin ~40 SGPRs for the whole kernel and spill; made opaque once per iteration they are
+    // recomputed in the phase that uses them (a few SALU ops per layer)
+    asm volatile("" : "+v"(tid), "+v"(lane), "+s"(g));
     const Tab& tb = A.tab[l];
-    const int t0 = l * S_LAYER;
+    const int t0 = l * P_LAYER;
     // ---- residual + norm1 -> xs; QKV rows ---------------------------------------------------
     if (l == 0) {
-      *reinterpret_cast<u32x4*>(rres + 8 * tid) = ld16(A.embed + (long)token * H + 8 * tid);
+#pragma unroll
+      for (int m = 0; m < M; ++m)
+        *reinterpret_cast<u32x4*>(&rres[m][8 * tid]) = ld16(A.embed + (long)tok_sh[m] * H + 8 * tid);
       __syncthreads();
     } else {
-      residual_add(A.db);
+      residual_add(nullptr, A.dpart);
     }
     norm_into_xs(tb.n1);
-    gemv_rows(t0, S_QKV, &red[0][0]);
-    if (tid < PAIRS / 4) {
-      // 4 consecutive RoPE pairs: rows p..p+3 and p+64..p+67 of one head
-      const int pr0 = g * PAIRS + 4 * tid, head = pr0 >> 6, p0 = pr0 & 63;
+    gemv(t0, R_QKV / NW, PPR, H);
+    if (tid < (PAIRS / 4) * M) {
+      // 4 consecutive RoPE pairs of row m: rows p..p+3 and p+64..p+67 of one head
+      const int m = tid / (PAIRS / 4), q = tid % (PAIRS / 4);
+      const int pr0 = g * PAIRS + 4 * q, head = pr0 >> 6, p0 = pr0 & 63;
+      const int ps = pos_sh[m];
       float lo[4], hi[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int u = 2 * (4 * tid + i);
-        float v0 = bf2f(f2bf(row_total(&red[0][0], u))), v1 = bf2f(f2bf(row_total(&red[0][0], u + 1)));
+        const int r = 2 * (4 * q + i);
+        float v0 = bf2f(f2bf(outr[r][m])), v1 = bf2f(f2bf(outr[r + 1][m]));
         if (head < HQ + HKV) {                                   // q and k heads rotate
-          const float c = A.cos_t[(long)pos * 64 + p0 + i], s = A.sin_t[(long)pos * 64 + p0 + i];
+          const float c = A.cos_t[(long)ps * 64 + p0 + i], s = A.sin_t[(long)ps * 64 + p0 + i];
           const float r0 = v0 * c - v1 * s, r1 = v1 * c + v0 * s;
           v0 = bf2f(f2bf(r0));
           v1 = bf2f(f2bf(r1));
@@ -320,7 +377,7 @@ __global__ __launch_bounds__(NT) void decode_step_kernel(Args a) {
         lo[i] = v0;
         hi[i] = v1;
       }
-      float* q0 = A.qkvf + head * HD + p0;
+      float* q0 = A.qkvf + (long)m * NQKV + head * HD + p0;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         st_f(q0 + i, lo[i]);
@@ -329,7 +386,7 @@ __global__ __launch_bounds__(NT) void decode_step_kernel(Args a) {
       if (head >= HQ) {                                          // K / V cache append (next steps read it)
         const bool is_v = head >= HQ + HKV;
         const int kh = is_v ? head - HQ - HKV : head - HQ;
-        bf16_t* c = (is_v ? tb.vc : tb.kc) + (((long)slot * HKV + kh) * A.lmax + pos) * HD + p0;
+        bf16_t* c = (is_v ? tb.vc : tb.kc) + (((long)slot_sh[m] * HKV + kh) * A.lmax + ps) * HD + p0;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           c[i] = f2bf(lo[i]);
@@ -339,21 +396,24 @@ __global__ __launch_bounds__(NT) void decode_step_kernel(Args a) {
     }
     if (!grid_barrier(++bar)) break;
 
-    // ---- attention: WG (kv head hk, key split j); the last split to finish merges ---------
-    {
-      const int hk = g & (HKV - 1), j = g / HKV;
+    // ---- attention: WG (row m, kv head hk, key split j); the last split to finish merges ------
+    const int ns = A.ns;
+    if (g < M * HKV * ns) {
+      const int m = g / (HKV * ns), rem = g % (HKV * ns), hk = rem % HKV, j = rem / HKV;
+      const int ps = pos_sh[m];
       float* qs = reinterpret_cast<float*>(xsb);                 // [G][HD] scaled q
       float* kcur = qs + G * HD;                                 // [HD] current key / value
       float* vcur = kcur + HD;
       float* so = vcur + HD;                                     // [NW][G][HD]
       float* sm = so + NW * G * HD;                              // [NW][G]
       float* sl = sm + NW * G;
-      qs[tid] = ld_f(A.qkvf + hk * G * HD + tid) * A.scale_log2;
-      if (tid < HD) kcur[tid] = ld_f(A.qkvf + (HQ + hk) * HD + tid);
-      else if (tid < 2 * HD) vcur[tid - HD] = ld_f(A.qkvf + (HQ + HKV + hk) * HD + tid - HD);
+      const float* qrow = A.qkvf + (long)m * NQKV;
+      qs[tid] = ld_f(qrow + hk * G * HD + tid) * A.scale_log2;
+      if (tid < HD) kcur[tid] = ld_f(qrow + (HQ + hk) * HD + tid);
+      else if (tid < 2 * HD) vcur[tid - HD] = ld_f(qrow + (HQ + HKV + hk) * HD + tid - HD);
       __syncthreads();
-      const int len = pos + 1;
-      const int chunk = ((len + NS - 1) / NS + 15) & ~15;
+      const int len = ps + 1;
+      const int chunk = ((len + ns - 1) / ns + 15) & ~15;
       const int start = j * chunk, end = min(len, start + chunk);
       const int sub = lane & 15, grp = tid >> 4;                 // 32 key streams x 16 lanes
       float qf[G][8];
@@ -361,13 +421,13 @@ __global__ __launch_bounds__(NT) void decode_step_kernel(Args a) {
       for (int h = 0; h < G; ++h)
 #pragma unroll
         for (int i = 0; i < 8; ++i) qf[h][i] = qs[h * HD + sub * 8 + i];
-      const long kvbase = ((long)slot * HKV + hk) * A.lmax * HD;
+      const long kvbase = ((long)slot_sh[m] * HKV + hk) * A.lmax * HD;
       const bf16_t* kp = tb.kc + kvbase;
       const bf16_t* vp = tb.vc + kvbase;
-      float m[G], lsum[G], acc[G][8];
+      float mx[G], lsum[G], acc[G][8];
 #pragma unroll
       for (int h = 0; h < G; ++h) {
-        m[h] = -INFINITY;
+        mx[h] = -INFINITY;
         lsum[h] = 0.f;
 #pragma unroll
         for (int i = 0; i < 8; ++i) acc[h][i] = 0.f;
@@ -376,7 +436,7 @@ __global__ __launch_bounds__(NT) void decode_step_kernel(Args a) {
         const int jk = r0 + grp;
         const bool ok = jk < end;
         float kf[8], vf[8];
-        if (ok && jk == pos) {
+        if (ok && jk == ps) {
 #pragma unroll
           for (int i = 0; i < 8; ++i) { kf[i] = kcur[sub * 8 + i]; vf[i] = vcur[sub * 8 + i]; }
         } else {
@@ -392,10 +452,10 @@ __global__ __launch_bounds__(NT) void decode_step_kernel(Args a) {
 #pragma unroll
           for (int o = 1; o < 16; o <<= 1) s += __shfl_xor(s, o, 64);
           s = ok ? s : -INFINITY;
-          const float mn = fmaxf(m[h], s);
+          const float mn = fmaxf(mx[h], s);
           if (mn == -INFINITY) continue;
-          const float al = exp2f(m[h] - mn), p = exp2f(s - mn);
-          m[h] = mn;
+          const float al = exp2f(mx[h] - mn), p = exp2f(s - mn);
+          mx[h] = mn;
           lsum[h] = fmaf(lsum[h], al, p);
 #pragma unroll
           for (int i = 0; i < 8; ++i) acc[h][i] = fmaf(acc[h][i], al, p * vf[i]);
@@ -406,13 +466,13 @@ __global__ __launch_bounds__(NT) void decode_step_kernel(Args a) {
       for (int h = 0; h < G; ++h) {
 #pragma unroll
         for (int o = 16; o < 64; o <<= 1) {
-          const float mo = __shfl_xor(m[h], o, 64), lo_ = __shfl_xor(lsum[h], o, 64);
-          const float mn = fmaxf(m[h], mo);
-          const float x0 = mn == -INFINITY ? 0.f : exp2f(m[h] - mn), x1 = mn == -INFINITY ? 0.f : exp2f(mo - mn);
+          const float mo = __shfl_xor(mx[h], o, 64), lo_ = __shfl_xor(lsum[h], o, 64);
+          const float mn = fmaxf(mx[h], mo);
+          const float x0 = mn == -INFINITY ? 0.f : exp2f(mx[h] - mn), x1 = mn == -INFINITY ? 0.f : exp2f(mo - mn);
           lsum[h] = lsum[h] * x0 + lo_ * x1;
 #pragma unroll
           for (int i = 0; i < 8; ++i) acc[h][i] = acc[h][i] * x0 + __shfl_xor(acc[h][i], o, 64) * x1;
-          m[h] = mn;
+          mx[h] = mn;
         }
       }
       if (lane < 16) {
@@ -420,57 +480,58 @@ __global__ __launch_bounds__(NT) void decode_step_kernel(Args a) {
         for (int h = 0; h < G; ++h) {
 #pragma unroll
           for (int i = 0; i < 8; ++i) so[(wave * G + h) * HD + sub * 8 + i] = acc[h][i];
-          if (sub == 0) { sm[wave * G + h] = m[h]; sl[wave * G + h] = lsum[h]; }
+          if (sub == 0) { sm[wave * G + h] = mx[h]; sl[wave * G + h] = lsum[h]; }
         }
       }
       __syncthreads();
       // this split's partial (write-through), then the ticket
-      float* pp = A.part + ((long)hk * NS + j) * G * (HD + 2);
+      float* const pbase = A.part + ((long)m * HKV + hk) * 32 * G * (HD + 2);
       {
+        float* pp = pbase + (long)j * G * (HD + 2);
         const int h = tid / HD, d = tid % HD;                   // 512 threads = G x HD
-        float M = sm[h];
+        float Mx = sm[h];
 #pragma unroll
-        for (int w = 1; w < NW; ++w) M = fmaxf(M, sm[w * G + h]);
+        for (int w = 1; w < NW; ++w) Mx = fmaxf(Mx, sm[w * G + h]);
         float o = 0.f;
-        if (M != -INFINITY) {
+        if (Mx != -INFINITY) {
 #pragma unroll
-          for (int w = 0; w < NW; ++w) o = fmaf(exp2f(sm[w * G + h] - M), so[(w * G + h) * HD + d], o);
+          for (int w = 0; w < NW; ++w) o = fmaf(exp2f(sm[w * G + h] - Mx), so[(w * G + h) * HD + d], o);
         }
         st_f(pp + h * (HD + 2) + d, o);
         if (d == 0) {
           float Ls = 0.f;
-          if (M != -INFINITY) {
+          if (Mx != -INFINITY) {
 #pragma unroll
-            for (int w = 0; w < NW; ++w) Ls = fmaf(exp2f(sm[w * G + h] - M), sl[w * G + h], Ls);
+            for (int w = 0; w < NW; ++w) Ls = fmaf(exp2f(sm[w * G + h] - Mx), sl[w * G + h], Ls);
           }
-          st_f(pp + h * (HD + 2) + HD, M);
+          st_f(pp + h * (HD + 2) + HD, Mx);
           st_f(pp + h * (HD + 2) + HD + 1, Ls);
         }
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid == 0) {
-        const int old = __hip_atomic_fetch_add(A.sync + (8 + hk) * SHARD, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        flag_sh = old == NS * (l + 1) - 1;
+        const int old = __hip_atomic_fetch_add(A.sync + (8 + m * HKV + hk) * SHARD, 1, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+        flag_sh = old == ns * (l + 1) - 1;
       }
       __syncthreads();
       if (flag_sh) {
-        // merge the NS splits of this kv head: weights per (split, head), then every output
-        float* wt = sm;                                          // [NS][G] (reuses the scratch)
-        float* den = wt + NS * G;
-        const float* pk = A.part + (long)hk * NS * G * (HD + 2);
-        if (tid < NS * G) wt[tid] = ld_f(pk + (long)tid * (HD + 2) + HD);
+        // merge the ns splits of this (row, kv head): weights per (split, head), then every output
+        float* wt = sm + 2 * NW * G;                             // [32][G]
+        float* den = wt + 32 * G;
+        if (tid < ns * G) wt[tid] = ld_f(pbase + (long)tid * (HD + 2) + HD);
         __syncthreads();
         if (tid < G) {
-          float M = -INFINITY;
+          float Mx = -INFINITY;
 #pragma unroll 1
-          for (int s = 0; s < NS; ++s) M = fmaxf(M, wt[s * G + tid]);
+          for (int s = 0; s < ns; ++s) Mx = fmaxf(Mx, wt[s * G + tid]);
           float D = 0.f;
 #pragma unroll 1
-          for (int s = 0; s < NS; ++s) {
+          for (int s = 0; s < ns; ++s) {
             const float ms = wt[s * G + tid];
-            const float w = (M == -INFINITY || ms == -INFINITY) ? 0.f : exp2f(ms - M);
-            D = fmaf(w, ld_f(pk + (long)(s * G + tid) * (HD + 2) + HD + 1), D);
+            const float w = (Mx == -INFINITY || ms == -INFINITY) ? 0.f : exp2f(ms - Mx);
+            D = fmaf(w, ld_f(pbase + (long)(s * G + tid) * (HD + 2) + HD + 1), D);
             wt[s * G + tid] = w;
           }
           den[tid] = D;
@@ -480,106 +541,100 @@ __global__ __launch_bounds__(NT) void decode_step_kernel(Args a) {
           const int h = (2 * tid) / HD, d = (2 * tid) % HD;
           float o0 = 0.f, o1 = 0.f;
 #pragma unroll 4
-          for (int s = 0; s < NS; ++s) {
+          for (int s = 0; s < ns; ++s) {
             const float w = wt[s * G + h];
-            const float* ps = pk + (long)(s * G + h) * (HD + 2) + d;
-            o0 = fmaf(w, ld_f(ps), o0);
-            o1 = fmaf(w, ld_f(ps + 1), o1);
+            const float* ps_ = pbase + (long)(s * G + h) * (HD + 2) + d;
+            o0 = fmaf(w, ld_f(ps_), o0);
+            o1 = fmaf(w, ld_f(ps_ + 1), o1);
           }
           const float inv = den[h] > 0.f ? 1.f / den[h] : 0.f;
-          st_u(A.ob + (hk * G + h) * HD + d, pack2(o0 * inv, o1 * inv));
+          st_u(A.ob + (long)m * H + (hk * G + h) * HD + d, pack2(o0 * inv, o1 * inv));
         }
       }
     }
     if (!grid_barrier(++bar)) break;
 
     // ---- O projection -----------------------------------------------------------------------
-    for (int i = tid; i < H / 2; i += NT) reinterpret_cast<u32*>(xs)[i] = ld_u(A.ob + 2 * i);
+    for (int i = tid; i < M * H / 2; i += NT) reinterpret_cast<u32*>(xs)[i] = ld_u(A.ob + 2 * i);
     __syncthreads();
-    gemv_rows(t0 + S_QKV, S_O, &red[0][0]);
-    if (tid < ROWS_O / 2)
-      st_u(A.dab + g * ROWS_O + 2 * tid, pack2(row_total(&red[0][0], 2 * tid), row_total(&red[0][0], 2 * tid + 1)));
+    gemv(t0 + P_QKV, R_O / NW, PPR, H);
+    if (tid < (R_O / 2) * M) {
+      const int m = tid / (R_O / 2), k = tid % (R_O / 2);
+      st_u(A.dab + (long)m * H + g * R_O + 2 * k, pack2(outr[2 * k][m], outr[2 * k + 1][m]));
+    }
     if (!grid_barrier(++bar)) break;
 
     // ---- residual + norm2 -> xs; gate/up rows + SwiGLU --------------------------------------
-    residual_add(A.dab);
+    residual_add(A.dab, nullptr);
     norm_into_xs(tb.n2);
-    gemv_rows(t0 + S_QKV + S_O, S_GU, &red[0][0]);
-    if (tid < ROWS_G / 2) {
+    gemv(t0 + P_QKV + P_O, 2 * R_G / NW, PPR, H);
+    if (tid < (R_G / 2) * M) {
+      const int m = tid / (R_G / 2), k = tid % (R_G / 2);
       float o[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const float gt = row_total(&red[0][0], 2 * tid + i), up = row_total(&red[0][0], ROWS_G + 2 * tid + i);
+        const float gt = outr[2 * k + i][m], up = outr[R_G + 2 * k + i][m];
         o[i] = gt * sigmoidf_(gt) * up;
       }
-      st_u(A.sb + g * ROWS_G + 2 * tid, pack2(o[0], o[1]));
+      st_u(A.sb + (long)m * F + g * R_G + 2 * k, pack2(o[0], o[1]));
     }
     if (!grid_barrier(++bar)) break;
 
-    // ---- down projection: 16 contiguous rows of K = F, 3.5 stages per row ----------------
-    for (int i = tid; i < F / 2; i += NT) reinterpret_cast<u32*>(xs)[i] = ld_u(A.sb + 2 * i);
-    __syncthreads();
+    // ---- down projection: 64 rows x this WG's K quarter; fp32 partials per quarter ----------
     {
-      int cur = -1;
-      float acc = 0.f;
-      for (int u = 0; u < S_D; ++u) {
-        const int e0 = u * 4096 + 512 * wave;                    // wave-uniform: a piece never
-        const int row = e0 / F, col = e0 - row * F + 8 * lane;  // straddles rows (F % 512 == 0)
-        const u32x4 w = take(t0 + S_QKV + S_O + S_GU + u);
-        const u32x4 xv = *reinterpret_cast<const u32x4*>(xs + col);
-        if (row != cur) {
-          if (cur >= 0) {
-            const float p = wave_sum(acc);
-            if (lane == 0) red[cur][wave] = p;
-          }
-          cur = row;
-          acc = 0.f;
-        }
-        acc = dot8(w, xv, acc);
+      const int kq = g % DKS;
+      for (int i = tid; i < M * KQ / 2; i += NT) {
+        const int m = i / (KQ / 2), c = i % (KQ / 2);
+        reinterpret_cast<u32*>(xs)[m * (KQ / 2) + c] = ld_u(A.sb + (long)m * F + kq * KQ + 2 * c);
       }
-      const float p = wave_sum(acc);
-      if (lane == 0) red[cur][wave] = p;
       __syncthreads();
+      gemv(t0 + P_QKV + P_O + P_GU, R_D / NW, PPD, KQ);
+      if (tid < (R_D / 4) * M) {
+        const int m = tid / (R_D / 4), k = tid % (R_D / 4);
+        float* dp = A.dpart + ((long)kq * M + m) * H + (g / DKS) * R_D + 4 * k;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) st_f(dp + i, outr[4 * k + i][m]);
+      }
     }
-    if (tid < ROWS_O / 2)
-      st_u(A.db + g * ROWS_O + 2 * tid, pack2(row_total(&red[0][0], 2 * tid), row_total(&red[0][0], 2 * tid + 1)));
     if (!grid_barrier(++bar)) break;
   }
 
   if (dead_sh == 0) {
     // ---- final norm + LM head: this WG's V / 256 rows ------------------------------------
-    residual_add(A.db);
+    residual_add(nullptr, A.dpart);
     norm_into_xs(A.fnorm);
-    float* redl = reinterpret_cast<float*>(xsb + 2 * H);        // [rows_lm][NW] after x
-    gemv_rows(L * S_LAYER, rows_lm, redl);
-    for (int r = tid; r < rows_lm; r += NT) A.logits[(long)g * rows_lm + r] = f2bf(row_total(redl, r));
+    gemv(L * P_LAYER, nlm, PPR, H);
+    for (int i = tid; i < rows_lm * M; i += NT) {
+      const int m = i / rows_lm, r = i % rows_lm;
+      A.logits[(long)m * A.V + (long)g * rows_lm + r] = f2bf(outr[r][m]);
+    }
   }
   vm_wait<0>();                                                  // no DMA may outlive the LDS
+}
+
+template <int M>
+constexpr long ws_bytes_m() {
+  return (long)M * NQKV * 4 + (long)M * H * 2 * 2 + (long)M * F * 2 + (long)DKS * M * H * 4 +
+         (long)M * HKV * 32 * G * (HD + 2) * 4;
 }
 
 }  // namespace ds
 
 using namespace ds;
 
-extern "C" long kf_decode_step_ws_bytes() {
-  return (long)NQKV * 4 + 2L * H * 2 + (long)F * 2 + (long)H * 2 + (long)HKV * NS * G * (HD + 2) * 4 +
-         (long)SYNC_INTS * 4 + 1024;
-}
+// workspace for up to MAXM rows: hand-off buffers, then the sync words (zeroed every launch)
+extern "C" long kf_decode_step_ws_bytes() { return ws_bytes_m<MAXM>() + (long)SYNC_INTS * 4 + 1024; }
+extern "C" long kf_decode_step_err_offset() { return ws_bytes_m<MAXM>() + (long)ERR_INT * 4; }
 
-// Returns 0 when launched; non-zero (nothing launched) when the model / device is not the shape
-// this kernel is built for.  ws: kf_decode_step_ws_bytes() bytes, 16-B aligned; its sync words
-// are zeroed here (a memset node when captured).  err word: kf_decode_step_err_offset().
-extern "C" long kf_decode_step_err_offset() {
-  const long off = kf_decode_step_ws_bytes() - 1024 - (long)SYNC_INTS * 4;
-  return off + (long)(8 + HKV) * SHARD * 4;
-}
-
-extern "C" int kf_decode_step(const void* tab, int L, int hidden, int ffn, int hq, int hkv, int hd, int V,
+// Rows 1..4 (M): token int64 [M], slot / pos int32 [M], logits bf16 [M, V].  Returns 0 when
+// launched; non-zero (nothing launched) when the model / device is not the shape this kernel is
+// built for.  ws: kf_decode_step_ws_bytes() bytes, 16-B aligned.
+extern "C" int kf_decode_step(const void* tab, int L, int M, int hidden, int ffn, int hq, int hkv, int hd, int V,
                               const void* embed, const void* fnorm, const void* lm, const float* cos_t,
                               const float* sin_t, const long* token, const int* slot, const int* pos, int lmax,
                               float eps, float scale, void* ws, void* logits, hipStream_t st) {
   if (hidden != H || ffn != F || hq != HQ || hkv != HKV || hd != HD) return 1;
-  if (L < 1 || L > MAXL || V % NWG != 0 || V / NWG > (XS_BYTES - 2 * H) / (NW * 4)) return 2;
+  if (M < 1 || M > MAXM || L < 1 || L > MAXL || V % NWG != 0 || V / NWG > MAXROWS_LM) return 2;
   if (((uintptr_t)ws & 15) || ((uintptr_t)embed & 15) || ((uintptr_t)lm & 15)) return 3;
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 4;
@@ -590,6 +645,7 @@ extern "C" int kf_decode_step(const void* tab, int L, int hidden, int ffn, int h
   a.L = L;
   a.V = V;
   a.lmax = lmax;
+  a.ns = NWG / (M * HKV) > 32 ? 32 : NWG / (M * HKV);
   a.embed = static_cast<const bf16_t*>(embed);
   a.fnorm = static_cast<const bf16_t*>(fnorm);
   a.lm = static_cast<const bf16_t*>(lm);
@@ -601,21 +657,26 @@ extern "C" int kf_decode_step(const void* tab, int L, int hidden, int ffn, int h
   a.eps = eps;
   a.scale_log2 = scale * 1.4426950408889634f;
   a.qkvf = reinterpret_cast<float*>(w);
-  w += (long)NQKV * 4;
+  w += (long)MAXM * NQKV * 4;
   a.ob = reinterpret_cast<bf16_t*>(w);
-  w += (long)H * 2;
+  w += (long)MAXM * H * 2;
   a.dab = reinterpret_cast<bf16_t*>(w);
-  w += (long)H * 2;
+  w += (long)MAXM * H * 2;
   a.sb = reinterpret_cast<bf16_t*>(w);
-  w += (long)F * 2;
-  a.db = reinterpret_cast<bf16_t*>(w);
-  w += (long)H * 2;
+  w += (long)MAXM * F * 2;
+  a.dpart = reinterpret_cast<float*>(w);
+  w += (long)DKS * MAXM * H * 4;
   a.part = reinterpret_cast<float*>(w);
-  w += (long)HKV * NS * G * (HD + 2) * 4;
+  w += (long)MAXM * HKV * 32 * G * (HD + 2) * 4;
   a.sync = reinterpret_cast<int*>(w);
   a.logits = static_cast<bf16_t*>(logits);
   if (hipMemsetAsync(a.sync, 0, (size_t)SYNC_INTS * 4, st) != hipSuccess) return 6;
-  hipLaunchKernelGGL(decode_step_kernel, dim3(NWG), dim3(NT), 0, st, a);
+  switch (M) {
+    case 1: hipLaunchKernelGGL(decode_step_kernel<1>, dim3(NWG), dim3(NT), 0, st, a); break;
+    case 2: hipLaunchKernelGGL(decode_step_kernel<2>, dim3(NWG), dim3(NT), 0, st, a); break;
+    case 3: hipLaunchKernelGGL(decode_step_kernel<3>, dim3(NWG), dim3(NT), 0, st, a); break;
+    default: hipLaunchKernelGGL(decode_step_kernel<4>, dim3(NWG), dim3(NT), 0, st, a); break;
+  }
   KF_CHECK_LAUNCH();
   return 0;
 }

@@ -57,8 +57,8 @@ BGEMM_MIN_ROWS, BGEMM_MAX_ROWS = 33, 128   # at 32 rows its reduce launch costs 
 # prompts admitted in one scheduler iteration are prefilled together up to this many tokens
 PREFILL_MAX_TOKENS = int(os.environ.get("KFAMD_PREFILL_MAX_TOKENS", "16384"))
 PREFILL_PAD_RATIO = 1.25      # ... in length groups padded to at most 1.25x
-# batch 1: the whole decode step as ONE persistent kernel (ops/csrc/decode_step.hip) where the
-# model is its shape; KFAMD_DECODE_PERSISTENT=0 keeps the kernel-per-op graph (A/B, fallback)
+# batches 1-4: the whole decode step as ONE persistent kernel (ops/csrc/decode_step.hip) where
+# the model is its shape; KFAMD_DECODE_PERSISTENT=0 keeps the kernel-per-op graph (A/B, fallback)
 PERSISTENT_DECODE = os.environ.get("KFAMD_DECODE_PERSISTENT", "1") != "0"
 # hipBLASLt/rocBLAS solutions for the decode GEMM shapes above SKINNY_MAX_ROWS where the library
 # heuristic picks a poor kernel (tools/tune_decode_gemm.py; only the shapes that measured >= 5 %
@@ -83,11 +83,14 @@ def _load_tuned_decode_gemms(dev, cfg, tp: int) -> bool:
 
 
 class PersistentDecode:
-    """Batch-1 decode step as one persistent launch (ops/csrc/decode_step.hip): 256 workgroups,
-    one per CU, stream every weight byte of the step once by LDS-DMA while grid barriers order
-    the layer's phases.  Built for Llama-3-8B at TP 1 on a 256-CU MI355X; ``build`` returns
-    None for anything else.  The kernel's grid barriers are bounded: a timed-out step sets the
-    error word (``failed()``), the engine disables this path and recomputes the step."""
+    """Decode step for 1-4 rows as one persistent launch (ops/csrc/decode_step.hip): 256
+    workgroups, one per CU, stream every weight byte of the step once by LDS-DMA while grid
+    barriers order the layer's phases.  Built for Llama-3-8B at TP 1 on a 256-CU MI355X;
+    ``build`` returns None for anything else.  The kernel's grid barriers are bounded: a
+    timed-out step sets the error word (``failed()``), the engine disables this path and
+    recomputes the step kernel-per-op."""
+
+    MAX_ROWS = 4
 
     def __init__(self, engine: "Engine"):
         from ..ops import _ext
@@ -103,7 +106,8 @@ class PersistentDecode:
         self.ws = torch.zeros(int(self.k.decode_step_ws_bytes()), dtype=torch.uint8, device=dev)
         off = int(self.k.decode_step_err_offset())
         self.err = self.ws[off:off + 4].view(torch.int32)
-        self.logits = torch.empty(m.P("lm_head").shape[0], dtype=torch.bfloat16, device=dev)
+        self.V = m.P("lm_head").shape[0]
+        self.logits = {}                # rows -> bf16 [rows, V] (graph-static per bucket)
         self.cfg, self.m, self.lmax = cfg, m, engine.max_len
 
     @staticmethod
@@ -118,13 +122,18 @@ class PersistentDecode:
         return cls(engine) if cls.supported(engine) else None
 
     def __call__(self, tokens, slots, pos):
-        """Launch one step for row 0 (token, slot, pos: device [1] tensors); returns logits
-        [1, V] or None when the kernel refused the shape / device (nothing launched)."""
+        """Launch one step for the M = len(tokens) <= 4 rows (token, slot, pos: device [M]
+        tensors); returns logits [M, V] or None when the kernel refused the shape / device
+        (nothing launched)."""
         m, cfg = self.m, self.cfg
+        M = tokens.shape[0]
+        out = self.logits.get(M)
+        if out is None:
+            out = self.logits[M] = torch.empty((M, self.V), dtype=torch.bfloat16, device=self.ws.device)
         rc = self.k.decode_step(self.tab, cfg.hidden, cfg.ffn, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim,
                                 m.P("embed"), m.P("final_norm"), m.P("lm_head"), m.cos, m.sin, tokens, slots, pos,
-                                self.lmax, float(cfg.norm_eps), 1.0 / math.sqrt(cfg.head_dim), self.ws, self.logits)
-        return self.logits.view(1, -1) if rc == 0 else None
+                                self.lmax, float(cfg.norm_eps), 1.0 / math.sqrt(cfg.head_dim), self.ws, out)
+        return out if rc == 0 else None
 
     def failed(self) -> bool:
         return int(self.err.item()) != 0
@@ -276,7 +285,7 @@ class Engine:
 
     def _decode_body(self, tokens, slots, pos, lengths):
         m, cfg = self.m, self.cfg
-        if self.persist is not None and tokens.shape[0] == 1:
+        if self.persist is not None and tokens.shape[0] <= PersistentDecode.MAX_ROWS:
             out = self.persist(tokens, slots, pos)
             if out is not None:
                 return out
@@ -335,7 +344,7 @@ class Engine:
             p = torch.tensor(pos, dtype=torch.int32, device=dev)
             out = self._decode_body(t, sl, p, p + 1)
             self._check_comm()
-            if B == 1 and self.persist is not None and self.persist.failed():
+            if B <= PersistentDecode.MAX_ROWS and self.persist is not None and self.persist.failed():
                 self.persist = None
                 return self.decode(tokens, slots, pos)
             return out
@@ -366,11 +375,12 @@ class Engine:
         gl.copy_(dev_rows[2] + 1)
         graph.replay()
         self._check_comm()
-        if Bb == 1 and self.persist is not None and self.persist.failed():
+        if Bb <= PersistentDecode.MAX_ROWS and self.persist is not None and self.persist.failed():
             # a grid barrier timed out (a CU never arrived): drop the persistent path, rebuild the
             # bucket's graph kernel-per-op and recompute this step (it rewrites the step's K/V)
             self.persist = None
-            self._graphs.pop(1, None)
+            for b in [b for b in self._graphs if b <= PersistentDecode.MAX_ROWS]:
+                self._graphs.pop(b)
             return self.decode(tokens, slots, pos)
         return out[:B]
 

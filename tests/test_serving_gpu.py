@@ -321,27 +321,34 @@ def _llama8b_engine(n_layers, use_graphs, max_len=4096):
     return build_engine("llama3-8b", device=DEV, n_slots=2, max_len=max_len, n_layers=n_layers, use_graphs=use_graphs)
 
 
-@pytest.mark.parametrize("ctx", [64, 3000])
-def test_persistent_decode_step_matches_kernel_per_op(ctx):
-    """The batch-1 persistent decode kernel (ops/csrc/decode_step.hip) against the kernel-per-op
-    decode path on the same KV cache, Llama-3-8B shapes (2 layers), short and long context."""
+@pytest.mark.parametrize("ctxs", [[64], [3000], [40, 700, 1500], [100, 2900, 33, 1200]],
+                         ids=["b1-64", "b1-3000", "b3", "b4"])
+def test_persistent_decode_step_matches_kernel_per_op(ctxs):
+    """The persistent decode kernel (ops/csrc/decode_step.hip) against the kernel-per-op decode
+    path on the same KV cache, Llama-3-8B shapes (2 layers): batch 1 at short and long context,
+    and 3 / 4 sequences of different lengths in one step."""
+    B = len(ctxs)
     e = _llama8b_engine(2, use_graphs=False)
     assert e.persist is not None, "persistent decode path not selected for Llama-3-8B at TP 1"
     persist = e.persist
-    g = torch.Generator().manual_seed(ctx)
-    prompt = torch.randint(0, e.cfg.vocab_size, (ctx,), generator=g).tolist()
-    tok = int(e.prefill(0, prompt).float().argmax())
-    for step in range(4):
-        pos = ctx + step
+    g = torch.Generator().manual_seed(sum(ctxs))
+    toks = []
+    for b, c in enumerate(ctxs):
+        prompt = torch.randint(0, e.cfg.vocab_size, (c,), generator=g).tolist()
+        toks.append(int(e.prefill(b, prompt).float().argmax()))
+    slots = list(range(B))
+    for step in range(3):
+        pos = [c + step for c in ctxs]
         e.persist = None
-        ref = e.decode([tok], [0], [pos]).float()
+        ref = e.decode(toks, slots, pos).float()
         e.persist = persist
-        got = e.decode([tok], [0], [pos]).float()
+        got = e.decode(toks, slots, pos).float()
         assert e.persist is persist and not persist.failed()
-        cos = torch.nn.functional.cosine_similarity(got.flatten(), ref.flatten(), dim=0)
-        assert cos > 0.999, (step, float(cos))
-        assert (got - ref).abs().max() <= 0.05 * ref.abs().max(), (step, float((got - ref).abs().max()))
-        tok = int(ref.argmax())
+        for b in range(B):
+            cos = torch.nn.functional.cosine_similarity(got[b], ref[b], dim=0)
+            assert cos > 0.999, (step, b, float(cos))
+            assert (got[b] - ref[b]).abs().max() <= 0.05 * ref[b].abs().max(), (step, b)
+        toks = ref.argmax(-1).tolist()
 
 
 def test_persistent_decode_step_in_a_graph_replays_identically():
@@ -361,3 +368,17 @@ def test_persistent_decode_step_in_a_graph_replays_identically():
         assert torch.equal(lg, le), step
         tg = te = int(le.float().argmax())
     assert not eg.persist.failed()
+    # two sequences: bucket 2 (graph) vs eager, then 3 sequences in the padded bucket 4
+    for B in (2, 3):
+        slots = list(range(B))
+        toks = [tg] * B
+        for step in range(3):
+            pos = [len(prompt) + 6 + step] * B
+            lg = eg.decode(toks, slots, pos).clone()
+            le = ee.decode(toks, slots, pos).clone()
+            if B == 2:
+                assert torch.equal(lg, le), (B, step)
+            else:                         # M = 4 (padded) vs M = 3 kernels: same rows, other schedule
+                assert torch.nn.functional.cosine_similarity(lg.float().flatten(), le.float().flatten(), dim=0) > 0.999
+            toks = le.float().argmax(-1).tolist()
+    assert not eg.persist.failed() and not ee.persist.failed()

@@ -76,14 +76,14 @@ def _train_body(rank, world, kind, sp):
     from service_account_auth_improvements_amd.parallel.state import init_distributed
     from service_account_auth_improvements_amd.runtime.trainer import TrainConfig, Trainer
     st = init_distributed(tp=world, pp=1, device="cuda")
-    tr = Trainer(TrainConfig(model="tiny", seq_len=64, micro_batch=2, n_layers=2, lr=1e-3, sequence_parallel=sp,
+    tr = Trainer(TrainConfig(model="tiny", seq_len=128, micro_batch=2, n_layers=2, lr=1e-3, sequence_parallel=sp,
                              tp_comm_chunks=2, tp_comm=kind), st, full_init=True)
     assert type(st.tp_comm).__name__ == "TwoShot"
     g = torch.Generator().manual_seed(11)
     v = tr.mcfg.vocab_size
     losses = []
     for _ in range(2):
-        b = [(torch.randint(0, v, (2, 64), generator=g).cuda(), torch.randint(0, v, (2, 64), generator=g).cuda())]
+        b = [(torch.randint(0, v, (2, 128), generator=g).cuda(), torch.randint(0, v, (2, 128), generator=g).cuda())]
         losses.append(float(tr.train_step(b)))
     torch.cuda.synchronize()
     st.tp_comm.check()
@@ -98,13 +98,13 @@ def test_two_shot_tp2_training_matches_one_rank(sp):
     from service_account_auth_improvements_amd.parallel.state import ParallelState
     from service_account_auth_improvements_amd.runtime.trainer import TrainConfig, Trainer
     res = run_ranks(_train_body, world=2, args=("twoshot", sp), timeout=300)
-    tr = Trainer(TrainConfig(model="tiny", seq_len=64, micro_batch=2, n_layers=2, lr=1e-3),
+    tr = Trainer(TrainConfig(model="tiny", seq_len=128, micro_batch=2, n_layers=2, lr=1e-3),
                  ParallelState(device=torch.device("cuda", 0)), full_init=True)
     g = torch.Generator().manual_seed(11)
     v = tr.mcfg.vocab_size
     ref = []
     for _ in range(2):
-        b = [(torch.randint(0, v, (2, 64), generator=g).cuda(), torch.randint(0, v, (2, 64), generator=g).cuda())]
+        b = [(torch.randint(0, v, (2, 128), generator=g).cuda(), torch.randint(0, v, (2, 128), generator=g).cuda())]
         ref.append(float(tr.train_step(b)))
     (l0, c0), (l1, c1) = res
     assert l0 == l1                       # both ranks computed the same bits
