@@ -22,12 +22,13 @@ def main():
     ap.add_argument("--model", default="llama3-8b")
     ap.add_argument("--layers", type=int, default=None)
     ap.add_argument("--ctx", type=int, default=1024, help="prompt length")
-    ap.add_argument("--batches", default="1,8,32,64")
+    ap.add_argument("--batches", nargs="+", default=["1,8,32,64"],
+                    help="batch sizes: comma-separated and/or space-separated")
     ap.add_argument("--steps", type=int, default=32)
     ap.add_argument("--max-len", type=int, default=2048)
     ap.add_argument("--prefill-batch", type=int, default=16, help="prompts per batched prefill pass")
     a = ap.parse_args()
-    batches = [int(x) for x in a.batches.split(",")]
+    batches = [int(x) for b in a.batches for x in b.split(",") if x]
     nb = max(batches)
     t0 = time.time()
     e = build_engine(a.model, device="cuda", n_slots=nb, max_len=a.max_len, n_layers=a.layers)
