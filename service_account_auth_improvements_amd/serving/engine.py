@@ -58,8 +58,11 @@ BGEMM_MIN_ROWS, BGEMM_MAX_ROWS = 33, 128   # at 32 rows its reduce launch costs 
 PREFILL_MAX_TOKENS = int(os.environ.get("KFAMD_PREFILL_MAX_TOKENS", "16384"))
 PREFILL_PAD_RATIO = 1.25      # ... in length groups padded to at most 1.25x
 # batches 1-4: the whole decode step as ONE persistent kernel (ops/csrc/decode_step.hip) where
-# the model is its shape; KFAMD_DECODE_PERSISTENT=0 keeps the kernel-per-op graph (A/B, fallback)
-PERSISTENT_DECODE = os.environ.get("KFAMD_DECODE_PERSISTENT", "1") != "0"
+# the model is its shape.  Opt-in (KFAMD_DECODE_PERSISTENT=1 or Engine(persistent=True)): on
+# MI355X it measures 3.54-3.65 ms/token at batch 1 against 3.15 for the kernel-per-op graph --
+# its 160 software grid barriers per token cost more than the launches they replace
+# (profiles/decode_step_ablation_r4p.txt, docs/ROUND4.md)
+PERSISTENT_DECODE = os.environ.get("KFAMD_DECODE_PERSISTENT", "0") == "1"
 # hipBLASLt/rocBLAS solutions for the decode GEMM shapes above SKINNY_MAX_ROWS where the library
 # heuristic picks a poor kernel (tools/tune_decode_gemm.py; only the shapes that measured >= 5 %
 # faster HBM-cold are kept, profiles/serve_large_batch.md).  Loaded into PyTorch TunableOp with
@@ -113,7 +116,7 @@ class PersistentDecode:
     @staticmethod
     def supported(engine: "Engine") -> bool:
         m, cfg = engine.m, engine.cfg
-        return (PERSISTENT_DECODE and engine.dev.type == "cuda" and m.tp == 1 and m.first and m.last
+        return (engine.dev.type == "cuda" and m.tp == 1 and m.first and m.last
                 and (cfg.hidden, cfg.ffn, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim) == (4096, 14336, 32, 8, 128)
                 and len(m.layers) <= 32 and m.P("lm_head").shape[0] % 256 == 0)
 
@@ -133,14 +136,27 @@ class PersistentDecode:
         rc = self.k.decode_step(self.tab, cfg.hidden, cfg.ffn, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim,
                                 m.P("embed"), m.P("final_norm"), m.P("lm_head"), m.cos, m.sin, tokens, slots, pos,
                                 self.lmax, float(cfg.norm_eps), 1.0 / math.sqrt(cfg.head_dim), self.ws, out)
+        self.last_rc = int(rc)
         return out if rc == 0 else None
 
+    def sync_words(self) -> dict:
+        """The launch's barrier shard counters, attention tickets and error word (diagnostics)."""
+        off = int(self.k.decode_step_err_offset())
+        shard = 32
+        base = off - (8 + 4 * 8) * shard * 4
+        w = self.ws[base:off + shard * 4 + 4].view(torch.int32).cpu()
+        return {"barrier_shards": w[0:8 * shard:shard].tolist(),
+                "tickets": w[8 * shard:(8 + 32) * shard:shard].tolist(), "err": int(w[40 * shard]),
+                "exit": int(w[41 * shard])}
+
     def failed(self) -> bool:
-        return int(self.err.item()) != 0
+        self.last_err = int(self.err.item())
+        return self.last_err != 0
 
 
 class Engine:
-    def __init__(self, model: Llama, n_slots: int = 64, max_len: int = 4096, use_graphs: Optional[bool] = None):
+    def __init__(self, model: Llama, n_slots: int = 64, max_len: int = 4096, use_graphs: Optional[bool] = None,
+                 persistent: Optional[bool] = None):
         self.m = model
         cfg = model.cfg
         self.cfg = cfg
@@ -161,7 +177,10 @@ class Engine:
         if model.tp > 1 and self.dev.type == "cuda":
             from ..parallel.custom_ar import OneShotAllReduce
             self.car = OneShotAllReduce(model.st.tp_group)
-        self.persist = PersistentDecode.build(self)
+        want = PERSISTENT_DECODE if persistent is None else bool(persistent)
+        self.persist = PersistentDecode.build(self) if want else None
+        # "active" / "off" / why the persistent path was dropped (reported by tools/bench_serve.py)
+        self.persist_status = "active" if self.persist is not None else "off"
         self._graphs: Dict[int, tuple] = {}
         self._staging: Dict[int, tuple] = {}   # bucket -> (pinned host [3, Bb], device [3, Bb], copy-done event)
 
@@ -289,7 +308,8 @@ class Engine:
             out = self.persist(tokens, slots, pos)
             if out is not None:
                 return out
-            self.persist = None             # refused (device / shape): kernel-per-op from now on
+            # refused (device / shape): kernel-per-op from now on
+            self._drop_persist(f"refused rc={self.persist.last_rc}")
         r = self._embed(tokens)
         d = None
         for li, i in enumerate(m.layers):
@@ -345,7 +365,7 @@ class Engine:
             out = self._decode_body(t, sl, p, p + 1)
             self._check_comm()
             if B <= PersistentDecode.MAX_ROWS and self.persist is not None and self.persist.failed():
-                self.persist = None
+                self._drop_persist(f"failed err={self.persist.last_err} {self.persist.sync_words()}")
                 return self.decode(tokens, slots, pos)
             return out
         Bb = next((b for b in BUCKETS if b >= B), None)
@@ -378,11 +398,18 @@ class Engine:
         if Bb <= PersistentDecode.MAX_ROWS and self.persist is not None and self.persist.failed():
             # a grid barrier timed out (a CU never arrived): drop the persistent path, rebuild the
             # bucket's graph kernel-per-op and recompute this step (it rewrites the step's K/V)
-            self.persist = None
+            self._drop_persist(f"failed err={self.persist.last_err} {self.persist.sync_words()}")
             for b in [b for b in self._graphs if b <= PersistentDecode.MAX_ROWS]:
                 self._graphs.pop(b)
             return self.decode(tokens, slots, pos)
         return out[:B]
+
+    def _drop_persist(self, why: str):
+        import sys
+        self.persist = None
+        self.persist_status = why
+        print(f"serving: persistent decode kernel disabled ({why}); kernel-per-op decode from now on",
+              file=sys.stderr, flush=True)
 
     def _check_comm(self):
         """TP decode: fail the step (and the engine) when a one-shot all-reduce timed out on a
@@ -549,7 +576,7 @@ class Scheduler:
 def build_engine(model_name: str = "llama3-8b", device=None, n_slots: int = 64, max_len: int = 4096,
                  checkpoint: Optional[str] = None, n_layers: Optional[int] = None, seed: int = 1234,
                  st: Optional[ParallelState] = None, use_graphs: Optional[bool] = None,
-                 full_init: bool = False) -> Engine:
+                 full_init: bool = False, persistent: Optional[bool] = None) -> Engine:
     cfg = LlamaConfig.preset(model_name)
     if n_layers:
         cfg = cfg.with_(n_layers=n_layers)
@@ -560,4 +587,4 @@ def build_engine(model_name: str = "llama3-8b", device=None, n_slots: int = 64, 
     if checkpoint:
         from ..runtime.checkpoint import load_params
         load_params(model, checkpoint)
-    return Engine(model, n_slots=n_slots, max_len=max_len, use_graphs=use_graphs)
+    return Engine(model, n_slots=n_slots, max_len=max_len, use_graphs=use_graphs, persistent=persistent)

@@ -318,7 +318,8 @@ def test_bgemm_decode_shapes_and_strided_rows():
 
 def _llama8b_engine(n_layers, use_graphs, max_len=4096):
     from service_account_auth_improvements_amd.serving.engine import build_engine
-    return build_engine("llama3-8b", device=DEV, n_slots=4, max_len=max_len, n_layers=n_layers, use_graphs=use_graphs)
+    return build_engine("llama3-8b", device=DEV, n_slots=4, max_len=max_len, n_layers=n_layers, use_graphs=use_graphs,
+                        persistent=True)
 
 
 @pytest.mark.parametrize("ctxs", [[64], [3000], [40, 700, 1500], [100, 2900, 33, 1200]],

@@ -33,7 +33,17 @@
 //
 // Shape: Llama-3-8B (hidden 4096, ffn 14336, 32 q / 8 kv heads of 128, vocab % 256 == 0), TP 1,
 // 256 CUs.  Anything else keeps the kernel-per-op path (kf_decode_step returns non-zero).
+// LAB COPY of ops/csrc/decode_step.hip with ablation knobs (tools/kbench/make_ds_lab.py); never shipped.
 #include "common.h"
+#ifndef KF_DS_NOBAR
+#define KF_DS_NOBAR 0
+#endif
+#ifndef KF_DS_NOATT
+#define KF_DS_NOATT 0
+#endif
+#ifndef KF_DS_NODMA
+#define KF_DS_NODMA 0
+#endif
 
 #include <type_traits>
 
@@ -69,10 +79,34 @@ static_assert(R_QKV % NW == 0 && R_O % NW == 0 && (2 * R_G) % NW == 0 && R_D % N
 // PF, pieces per wave each workgroup prefetches towards the caches while it waits at a grid
 // barrier (the ring is full then; PF = 0: none)
 template <int M> struct Cfg;
-template <> struct Cfg<1> { static constexpr int RS = 16, PF = 0; };
-template <> struct Cfg<2> { static constexpr int RS = 16, PF = 0; };
-template <> struct Cfg<3> { static constexpr int RS = 16, PF = 0; };
-template <> struct Cfg<4> { static constexpr int RS = 14, PF = 0; };
+#ifndef KF_DS_RS1
+#define KF_DS_RS1 16
+#endif
+#ifndef KF_DS_PF1
+#define KF_DS_PF1 0
+#endif
+template <> struct Cfg<1> { static constexpr int RS = KF_DS_RS1, PF = KF_DS_PF1; };
+#ifndef KF_DS_RS2
+#define KF_DS_RS2 16
+#endif
+#ifndef KF_DS_PF2
+#define KF_DS_PF2 0
+#endif
+template <> struct Cfg<2> { static constexpr int RS = KF_DS_RS2, PF = KF_DS_PF2; };
+#ifndef KF_DS_RS3
+#define KF_DS_RS3 16
+#endif
+#ifndef KF_DS_PF3
+#define KF_DS_PF3 0
+#endif
+template <> struct Cfg<3> { static constexpr int RS = KF_DS_RS3, PF = KF_DS_PF3; };
+#ifndef KF_DS_RS4
+#define KF_DS_RS4 14
+#endif
+#ifndef KF_DS_PF4
+#define KF_DS_PF4 0
+#endif
+template <> struct Cfg<4> { static constexpr int RS = KF_DS_RS4, PF = KF_DS_PF4; };
 
 struct Tab {                 // per layer, device memory (built once by the engine)
   const bf16_t *wqkv, *wo, *wgu, *wd, *n1, *n2;
@@ -133,6 +167,7 @@ __device__ __forceinline__ const char* uniform_ptr(const char* p) {
 #pragma clang diagnostic ignored "-Winline-asm"
 // one 1 KB piece: lane l fetches 16 B at src + 16 l into LDS lds + 16 l (non-temporal: read once)
 __device__ __forceinline__ void dma_piece(const char* src, u32 lds, u32 voff) {
+  if (KF_DS_NODMA) return;
   asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2 nt" : : "s"(lds), "v"(voff), "s"(src)
                : "memory", "m0");
 }
@@ -277,8 +312,15 @@ __global__ __launch_bounds__(NT) void decode_step_kernel(Args a) {
 
   // ---- grid barrier k (1, 2, ...): 8-way sharded monotonic counter ---------------------------
   auto grid_barrier = [&](int k) -> bool {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // every wave drains its stores
+#if KF_DS_NOBAR == 2
     __syncthreads();
+    return true;
+#endif
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+#if KF_DS_NOBAR == 1
+    return true;
+#endif
     if (PF > 0 && wave != 0) {
       // the ring is full: pull this wave's next PF pieces past it towards the L2 / MALL while the
       // barrier settles (default cache policy; the bytes land in a shared LDS sink nobody reads).
@@ -467,7 +509,7 @@ __global__ __launch_bounds__(NT) void decode_step_kernel(Args a) {
 
     // ---- attention: WG (row m, kv head hk, key split j); the last split to finish merges ------
     const int ns = A.ns;
-    if (g < M * HKV * ns) {
+    if (!KF_DS_NOATT && g < M * HKV * ns) {
       const int m = g / (HKV * ns), rem = g % (HKV * ns), hk = rem % HKV, j = rem / HKV;
       const int ps = pos_sh[m];
       float* qs = reinterpret_cast<float*>(xsb);                 // [G][HD] scaled q
@@ -708,14 +750,14 @@ constexpr long ws_bytes_m() {
 using namespace ds;
 
 // workspace for up to MAXM rows: hand-off buffers, then the sync words (re-armed in-kernel)
-extern "C" long kf_decode_step_ws_bytes() { return ws_bytes_m<MAXM>() + (long)SYNC_INTS * 4 + 1024; }
-extern "C" long kf_decode_step_err_offset() { return ws_bytes_m<MAXM>() + (long)ERR_INT * 4; }
+extern "C" __attribute__((weak)) long kf_decode_step_ws_bytes() { return ws_bytes_m<MAXM>() + (long)SYNC_INTS * 4 + 1024; }
+extern "C" __attribute__((weak)) long kf_decode_step_err_offset() { return ws_bytes_m<MAXM>() + (long)ERR_INT * 4; }
 
 // Rows 1..4 (M): token int64 [M], slot / pos int32 [M], logits bf16 [M, V].  Returns 0 when
 // launched; non-zero (nothing launched) when the model / device is not the shape this kernel is
 // built for.  ws: kf_decode_step_ws_bytes() bytes, 16-B aligned, ZEROED before the first launch
 // (every clean launch leaves its sync words zero again; a non-zero error word is sticky).
-extern "C" int kf_decode_step(const void* tab, int L, int M, int hidden, int ffn, int hq, int hkv, int hd, int V,
+extern "C" __attribute__((weak)) int kf_decode_step(const void* tab, int L, int M, int hidden, int ffn, int hq, int hkv, int hd, int V,
                               const void* embed, const void* fnorm, const void* lm, const float* cos_t,
                               const float* sin_t, const long* token, const int* slot, const int* pos, int lmax,
                               float eps, float scale, void* ws, void* logits, hipStream_t st) {
