@@ -351,11 +351,14 @@ at::Tensor decode_attn(const at::Tensor& q2d, const at::Tensor& kc, const at::Te
     return v ? std::atoi(v) : 0;
   }();
   auto f32 = q2d.options().dtype(at::kFloat);
-  // small batches: split-K + merge in one launch (kf_decode_attn_fused), whose arrival tickets
-  // live in a per-device zeroed buffer that every launch leaves zero (allocated on first use,
-  // outside any graph capture; KFAMD_DECODE_FUSED=0 keeps the two-kernel form)
+  // small batches, opt-in (KFAMD_DECODE_FUSED=1): split-K + merge in one launch
+  // (kf_decode_attn_fused), whose arrival tickets live in a per-device zeroed buffer that every
+  // launch leaves zero (allocated on first use, outside any graph capture).  Measured slower than
+  // the two kernels on MI355X -- 13.6 vs 10.1 us at batch 1 / 1024 keys, decode step 3.14 vs
+  // 3.06 ms (profiles/serve_decode_attn_fused_ab_r4.txt): the last arriver's merge is a serial
+  // tail inside the launch, the combine kernel's boundary costs less
   const char* fv = std::getenv("KFAMD_DECODE_FUSED");      // read per call (tests compare both forms)
-  const bool fused_on = !(fv && fv[0] == '0');
+  const bool fused_on = fv && fv[0] == '1';
   if (fused_on && B <= 4 && B * Hkv <= 4096 && Hq / Hkv <= 8) {
     int* tickets = decode_tickets(q2d.device().index());
     if (tickets != nullptr) {

@@ -70,9 +70,10 @@ def test_decode_attn_fused_matches_two_kernel_and_fp32(B, Lmax, lens, monkeypatc
     assert (fused.float() - two.float()).abs().max().item() < 2e-2
 
 
-def test_decode_attn_fused_in_a_graph_rearms_its_tickets():
+def test_decode_attn_fused_in_a_graph_rearms_its_tickets(monkeypatch):
     """Captured once, replayed many times with changing lengths: each replay's last-arriving
     block re-arms the tickets, so every replay matches an eager call."""
+    monkeypatch.setenv("KFAMD_DECODE_FUSED", "1")                # opt-in form
     Hq, Hkv, Lmax = 32, 8, 2048
     g = torch.Generator(device="cpu").manual_seed(9)
     kc = torch.randn(2, Hkv, Lmax, 128, generator=g).to(DEV, torch.bfloat16)
