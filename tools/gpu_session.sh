@@ -8,7 +8,7 @@
 #   tests[:K_EXPR]          pytest -m gpu (optionally -k K_EXPR)              -> OUTDIR/pytest.log
 #   smoke                   __graft_entry__.smoke()                             -> OUTDIR/smoke.log
 #   bench[:STEPS[:WARMUP]]  python bench.py (+ $BENCH_ARGS)                     -> OUTDIR/bench*.log
-#   prof[:STEPS]            rocprofv3 --kernel-trace --stats of bench.py, per-category summary
+#   prof[:STEPS]            rocprofv3 --kernel-trace --stats of bench.py (STEPS + 2 warm-up steps traced), per-step summary
 #                                                                               -> OUTDIR/prof/summary.md
 #   kbench:BIN[:A,B,..]     tools/kbench/bin/BIN A B ..                         -> OUTDIR/kbench.txt
 #   pmc:BIN[:A,B,..]        two PMC passes over a kbench binary (tools/kbench/pmc.sh)
@@ -51,7 +51,7 @@ for step in "$@"; do
       timeout -k 10 700 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof" -o run -- \
         python3 bench.py --steps "${a1:-3}" --warmup 2 --crd-jobs 0 $BENCH_ARGS > "$log" 2>&1 || fail "$step" $? "$log"
       f=$(find "$O/prof" -name "*kernel_stats.csv" | head -1)
-      python tools/prof_summary.py "$f" "${a1:-3}" > "$O/prof/summary.md" && cp "$f" "$O/prof/kernel_stats.csv"
+      python tools/prof_summary.py "$f" "$(( ${a1:-3} + 2 ))" > "$O/prof/summary.md" && cp "$f" "$O/prof/kernel_stats.csv"
       head -18 "$O/prof/summary.md" ;;
     kbench)
       log=$O/kbench.txt
