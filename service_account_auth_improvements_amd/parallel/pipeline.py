@@ -541,6 +541,8 @@ class PipelineTrainer:
         self.opt.step(grad_scale=1.0 / self.st.dp)
         self.reducer.all_gather_params(overlap=self.overlap_allgather)
         self.step_idx += 1
+        if self.st.tp_comm is not None:
+            self.st.tp_comm.check()          # two-shot TP collectives: fail loudly on a lost peer
         return loss
 
     def sync_params(self):

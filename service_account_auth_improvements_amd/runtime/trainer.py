@@ -192,6 +192,10 @@ class Trainer:
         self.opt.step(grad_scale=1.0 / self.st.dp, segments=self._segments, stream=self._opt_stream)
         self.reducer.all_gather_params(overlap=self.tcfg.overlap_allgather)
         self.step_idx += 1
+        if self.st.tp_comm is not None:
+            # a two-shot collective whose peer never arrived produced garbage: fail the step
+            # (and the job) instead of training on it
+            self.st.tp_comm.check()
         return total
 
 

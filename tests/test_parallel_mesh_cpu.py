@@ -253,6 +253,9 @@ class _RecordingComm:
         self.calls["ag"] += 1
         return dist.all_gather_into_tensor(out, x, group=self.group, async_op=async_op)
 
+    def check(self):
+        self.calls["check"] = self.calls.get("check", 0) + 1
+
 
 def _comm_body(rank, world, sp, install):
     from service_account_auth_improvements_amd.parallel.custom_ar import make_tp_comm
@@ -282,6 +285,7 @@ def test_tp_collectives_route_through_the_tp_communicator(sp):
         for name in a["params"]:
             assert torch.equal(a["params"][name], b["params"][name]), name
         c = b["calls"]
+        assert c["check"] == STEPS          # the trainer checks the communicator after every step
         if sp:
             assert c["rs"] > 0 and c["ag"] > 0
         else:
