@@ -61,6 +61,18 @@ __global__ __launch_bounds__(NT) void decode_split_kernel(
   }
   const int n = end - start;
 
+  // Latency, not bandwidth, bounds a batch-1 split (32 keys at 1024 / 32 splits): every global
+  // load below is issued before the first one is needed -- q, the first round's K rows and the
+  // first two rounds' V rows together, each next K row one round ahead -- so a short split pays
+  // about one memory round trip instead of one per phase (8.3 us per layer before, gpurun_out/r4u)
+  const long kvbase = (long)slots[b] * slot_stride + (long)hk * head_stride;
+  const bf16_t* kp = kc + kvbase + (long)start * D + sub * 8;
+  const bf16_t* vp = vc + kvbase + (long)start * D + sub * 8;
+  const u32x4 zero = u32x4{0u, 0u, 0u, 0u};
+  u32x4 kcur = grp < n ? ld16(kp + (long)grp * D) : zero;
+  const u32x4 v0 = grp < n ? ld16(vp + (long)grp * D) : zero;
+  const u32x4 v1 = grp + 16 < n ? ld16(vp + (long)(grp + 16) * D) : zero;
+
   // q for the G heads of this kv head: 8 dims per lane, pre-scaled into the log2 domain
   float qf[G][8];
 #pragma unroll
@@ -71,20 +83,13 @@ __global__ __launch_bounds__(NT) void decode_split_kernel(
     for (int i = 0; i < 8; ++i) qf[h][i] *= scale_log2;
   }
 
-  const long kvbase = (long)slots[b] * slot_stride + (long)hk * head_stride;
-  const bf16_t* kp = kc + kvbase;
-  const bf16_t* vp = vc + kvbase;
-
   // ---- phase 1: scores
   for (int j0 = 0; j0 < n; j0 += 16) {
     const int j = j0 + grp;
+    const u32x4 knext = j + 16 < n ? ld16(kp + (long)(j + 16) * D) : zero;
     float kf_[8];
-    if (j < n) {
-      unpack8(ld16(kp + (long)(start + j) * D + sub * 8), kf_);
-    } else {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) kf_[i] = 0.f;
-    }
+    unpack8(kcur, kf_);
+    kcur = knext;
 #pragma unroll
     for (int h = 0; h < G; ++h) {
       float a = 0.f;
@@ -123,7 +128,7 @@ __global__ __launch_bounds__(NT) void decode_split_kernel(
     for (int i = 0; i < 8; ++i) acc[h][i] = 0.f;
   for (int j = grp; j < n; j += 16) {
     float vf[8];
-    unpack8(ld16(vp + (long)(start + j) * D + sub * 8), vf);
+    unpack8(j < 16 ? v0 : j < 32 ? v1 : ld16(vp + (long)j * D), vf);
 #pragma unroll
     for (int h = 0; h < G; ++h) {
       const float p = sc[h][j];
@@ -177,6 +182,18 @@ __global__ __launch_bounds__(CB_NT) void decode_combine_kernel(const float* __re
   const int bh = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b = bh / hq, h = bh % hq;
   const float* ml = part_ml + (long)bh * splits * 2;
+  const int d = tid & (D - 1), half = tid / D;
+  const float* po = part_o + (long)bh * splits * D + d;
+  // up to 32 splits (every batch-1 launch): this thread's 16 partial values are loaded up front,
+  // together with the (max, sum) pairs, so the merge costs one memory round trip, not three
+  constexpr int PRE = 16;
+  float pre[PRE];
+  const bool preload = splits <= 2 * PRE;
+#pragma unroll
+  for (int i = 0; i < PRE; ++i) {
+    const int s = half + 2 * i;
+    pre[i] = (preload && s < splits) ? po[(long)s * D] : 0.f;
+  }
   float mloc = -INFINITY;
   for (int s = tid; s < splits; s += CB_NT) mloc = fmaxf(mloc, ml[2 * s]);
   mloc = wave_max(mloc);
@@ -199,11 +216,18 @@ __global__ __launch_bounds__(CB_NT) void decode_combine_kernel(const float* __re
   float den = 0.f;
 #pragma unroll
   for (int w = 0; w < CB_NT / 64; ++w) den += red[w];
-  const int d = tid & (D - 1), half = tid / D;
-  const float* po = part_o + (long)bh * splits * D + d;
+  __syncthreads();                                   // ws complete
   float num = 0.f;
+  if (preload) {
+#pragma unroll
+    for (int i = 0; i < PRE; ++i) {
+      const int s = half + 2 * i;
+      if (s < splits) num = fmaf(ws[s], pre[i], num);
+    }
+  } else {
 #pragma unroll 8
-  for (int s = half; s < splits; s += 2) num = fmaf(ws[s], po[(long)s * D], num);
+    for (int s = half; s < splits; s += 2) num = fmaf(ws[s], po[(long)s * D], num);
+  }
   if (half == 1) half_num[d] = num;
   __syncthreads();
   if (half == 0) {

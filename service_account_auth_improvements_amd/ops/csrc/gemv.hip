@@ -71,19 +71,19 @@ struct GvRope {
   int hq, hkv, lmax;
 };
 
-template <int M, int R, bool SWIGLU, bool NORM, bool ROPE = false, int KS = 1>
-__global__ __launch_bounds__(64 * GV_WAVES) void gemv_kernel(const bf16_t* __restrict__ x, long ldx,
+template <int M, int R, bool SWIGLU, bool NORM, bool ROPE = false, int KS = 1, int WV = GV_WAVES>
+__global__ __launch_bounds__(64 * WV) void gemv_kernel(const bf16_t* __restrict__ x, long ldx,
                                                             const bf16_t* __restrict__ w, int N, int K,
                                                             bf16_t* __restrict__ y, long ldy, int up_off,
                                                             GvNorm na, GvRope ra) {
   static_assert(!ROPE || (R == 4 && !SWIGLU), "rope epilogue: 4 rows = two rotation pairs per wave");
   extern __shared__ __attribute__((aligned(16))) bf16_t xs[];   // NORM: M x K normalised rows
-  __shared__ float ssq[GV_WAVES][M];
+  __shared__ float ssq[WV][M];
   constexpr int NR = SWIGLU ? 2 * R : R;
-  static_assert(KS == 1 || KS == GV_WAVES, "K split: 1 or all waves of the workgroup");
+  static_assert(KS == 1 || (KS == GV_WAVES && WV == GV_WAVES), "K split: 1 or all waves of the workgroup");
   __shared__ float red[KS > 1 ? GV_WAVES : 1][NR][M];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int gw = KS > 1 ? (int)blockIdx.x : (int)blockIdx.x * GV_WAVES + wave;   // owner of R rows
+  const int gw = KS > 1 ? (int)blockIdx.x : (int)blockIdx.x * WV + wave;   // owner of R rows
   // ROPE: wave gw owns rotation pairs (p, p + 64) and (p + 1, p + 65) of head gw / 32
   const int r0 = ROPE ? (gw >> 5) * 128 + (gw & 31) * 2 : gw * R;
   const int nch = K >> 3;                       // 16-byte chunks per row
@@ -120,7 +120,7 @@ __global__ __launch_bounds__(64 * GV_WAVES) void gemv_kernel(const bf16_t* __res
     float ss[M];
 #pragma unroll
     for (int m = 0; m < M; ++m) ss[m] = 0.f;
-    for (int c = tid; c < nch; c += 64 * GV_WAVES) {
+    for (int c = tid; c < nch; c += 64 * WV) {
 #pragma unroll
       for (int m = 0; m < M; ++m) {
         float hv[8];
@@ -150,10 +150,10 @@ __global__ __launch_bounds__(64 * GV_WAVES) void gemv_kernel(const bf16_t* __res
     for (int m = 0; m < M; ++m) {
       float tot = 0.f;
 #pragma unroll
-      for (int v = 0; v < GV_WAVES; ++v) tot += ssq[v][m];
+      for (int v = 0; v < WV; ++v) tot += ssq[v][m];
       rs[m] = rsqrtf(tot / (float)K + na.eps);
     }
-    for (int c = tid; c < nch; c += 64 * GV_WAVES) {
+    for (int c = tid; c < nch; c += 64 * WV) {
       float wf[8];
       unpack8(ld16(na.w + 8 * c), wf);
 #pragma unroll
@@ -298,6 +298,15 @@ template <int M>
 int gv_rope_launch(const bf16_t* x, long ldx, const bf16_t* w, int N, int K, bf16_t* y, long ldy, GvNorm na,
                    GvRope ra, hipStream_t st) {
   const int blocks = N / (4 * GV_WAVES);
+  // Llama-3-8B qkv (6144 rows = 1536 four-row waves): 4-wave workgroups make 384, i.e. 1.5 per CU,
+  // so half the CUs stream twice the bytes (12.1 us, 4.2 TB/s, gpurun_out/r4u); 6-wave workgroups
+  // make exactly one per CU
+  if ((N / 4) % (6 * 256) == 0 && !use_ksplit(blocks, M, K, true)) {
+    hipLaunchKernelGGL((gemv_kernel<M, 4, false, true, true, 1, 6>), dim3(N / 24), dim3(64 * 6), (size_t)M * K * 2,
+                       st, x, ldx, w, N, K, y, ldy, 0, na, ra);
+    KF_CHECK_LAUNCH();
+    return 0;
+  }
   if (use_ksplit(blocks, M, K, true))
     hipLaunchKernelGGL((gemv_kernel<M, 4, false, true, true, GV_WAVES>), dim3(N / 4), dim3(64 * GV_WAVES),
                        (size_t)M * K * 2, st, x, ldx, w, N, K, y, ldy, 0, na, ra);
