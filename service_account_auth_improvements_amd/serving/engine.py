@@ -112,6 +112,8 @@ class PersistentDecode:
         self.V = m.P("lm_head").shape[0]
         self.logits = {}                # rows -> bf16 [rows, V] (graph-static per bucket)
         self.cfg, self.m, self.lmax = cfg, m, engine.max_len
+        self.last_rc = 0                # the last launch's return code (0 = launched)
+        self.last_err = 0               # the error word read by the last failed() check
 
     @staticmethod
     def supported(engine: "Engine") -> bool:
