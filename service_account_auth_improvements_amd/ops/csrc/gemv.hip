@@ -71,7 +71,7 @@ struct GvRope {
   int hq, hkv, lmax;
 };
 
-template <int M, int R, bool SWIGLU, bool NORM, bool ROPE = false, int KS = 1, int WV = GV_WAVES>
+template <int M, int R, bool SWIGLU, bool NORM, bool ROPE = false, int KS = 1, int WV = GV_WAVES, int U = GV_U>
 __global__ __launch_bounds__(64 * WV) void gemv_kernel(const bf16_t* __restrict__ x, long ldx,
                                                             const bf16_t* __restrict__ w, int N, int K,
                                                             bf16_t* __restrict__ y, long ldy, int up_off,
@@ -96,48 +96,104 @@ __global__ __launch_bounds__(64 * WV) void gemv_kernel(const bf16_t* __restrict_
     if constexpr (ROPE) return r0 + (i & 1) + (i >> 1) * 64;
     return i < R ? r0 + i : r0 + (i - R);
   };
+  // Every load below is unconditional (rows past N read row N - 1, chunks past the row its last
+  // chunk; neither sum is ever stored): with no load under a branch the compiler's vmcnt
+  // bookkeeping stays exact, so each wait covers only the loads it needs.
   auto row_ptr = [&](int i) -> const bf16_t* {
-    const int rr = (SWIGLU && i >= R) ? r0 + (i - R) + up_off : row_of(i);
-    return w + (long)rr * K + 8 * lane;
+    const int rc = min(row_of(i), N - 1);
+    return w + (long)((SWIGLU && i >= R) ? rc + up_off : rc) * K;
   };
-  auto row_ok = [&](int i) { return row_of(i) < N; };
 
-  u32x4 wv[NR][GV_U];
+  // Loads that do not depend on the product go out ahead of the weights, so none of them is a
+  // round trip of its own later: the epilogue's (position, slot), the norm prologue's x,
+  // residual and gain chunks; the RoPE cos/sin (which need the position) right behind them.
+  const int ep_i = lane / M;
+  int ep_m = lane % M;
+  // a per-lane (VGPR) index keeps these vector loads: as wave-uniform scalar loads (M = 1) the
+  // compiler waited for them before issuing anything else
+  asm volatile("" : "+v"(ep_m));
+  int ep_pos = 0, ep_slot = 0;
+  if constexpr (ROPE) {
+    ep_pos = ra.pos[ep_m];
+    ep_slot = ra.slots[ep_m];
+  }
+  constexpr int PW = 2;   // prologue passes whose operands are loaded up front (K <= 1024 WV)
+  u32x4 wn[PW], xq[PW][M], rq[PW][M];
+  const bf16_t* resp = na.res ? na.res : x;   // no residual: a harmless duplicate load of x
+  if constexpr (NORM) {
+#pragma unroll
+    for (int p = 0; p < PW; ++p) {
+      const int c = min(tid + p * 64 * WV, nch - 1);
+      wn[p] = ld16(na.w + 8 * c);
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        xq[p][m] = ld16(x + (long)m * ldx + 8 * c);
+        rq[p][m] = ld16(resp + (long)m * ldx + 8 * c);
+      }
+    }
+  }
+  u32x4 wv[NR][U];
   auto load_w = [&](int j0) {
 #pragma unroll
     for (int i = 0; i < NR; ++i)
 #pragma unroll
-      for (int u = 0; u < GV_U; ++u) {
-        const int c = lane + 64 * (j0 + u);
-        wv[i][u] = (row_ok(i) && j0 + u < je && c < nch)
-                       ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(row_ptr(i) + 512 * (j0 + u)))
-                       : u32x4{0, 0, 0, 0};
+      for (int u = 0; u < U; ++u) {
+        const int c = min(lane + 64 * (j0 + u), nch - 1);
+        wv[i][u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(row_ptr(i) + 8 * c));
       }
   };
   load_w(jb);
+  float ep_cos = 1.f, ep_sin = 0.f;
+  if constexpr (ROPE) {
+    // the position is consumed only here, behind the weight loads (the memory clobber keeps
+    // them ahead of this wait)
+    asm volatile("" : "+v"(ep_pos) : : "memory");
+    const int pr = row_of(ep_i) & 63;
+    ep_cos = ra.cos_t[(long)ep_pos * 64 + pr];
+    ep_sin = ra.sin_t[(long)ep_pos * 64 + pr];
+  }
 
   if constexpr (NORM) {
     float ss[M];
 #pragma unroll
     for (int m = 0; m < M; ++m) ss[m] = 0.f;
-    for (int c = tid; c < nch; c += 64 * WV) {
+    // h = x + res (kept, and normed, in bf16), its sum of squares, h staged in LDS.  The
+    // up-front passes compute unconditionally (a pass past the row repeats its last chunk and
+    // counts nothing): with the operands' uses under a branch hipcc sank their loads into it,
+    // behind a wait for every weight load
+    const bool has_res = na.res != nullptr;
+    auto absorb = [&](int c_raw, const u32x4* xc, const u32x4* rc) {
+      const bool valid = c_raw < nch;
+      const int c = min(c_raw, nch - 1);
 #pragma unroll
       for (int m = 0; m < M; ++m) {
-        float hv[8];
-        unpack8(ld16(x + (long)m * ldx + 8 * c), hv);
-        if (na.res) {
-          float t[8];
-          unpack8(ld16(na.res + (long)m * ldx + 8 * c), t);
+        float hv[8], t[8];
+        unpack8(xc[m], hv);
+        unpack8(rc[m], t);
+        // selects, not a branch on na.res (hipcc sank the residual load into it); without a
+        // residual h = x, which the bf16 round trip leaves unchanged
 #pragma unroll
-          for (int e = 0; e < 8; ++e) hv[e] += t[e];
-          const u32x4 hb = pack8(hv);     // residual stream kept (and normed) in bf16
-          if (blockIdx.x == 0) st16(na.h_out + (long)m * na.ldh + 8 * c, hb);
-          unpack8(hb, hv);
-        }
+        for (int e = 0; e < 8; ++e) hv[e] += has_res ? t[e] : 0.f;
+        const u32x4 hb = pack8(hv);
+        if (has_res && blockIdx.x == 0 && valid) st16(na.h_out + (long)m * na.ldh + 8 * c, hb);
+        unpack8(hb, hv);
+        float s = 0.f;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) ss[m] += hv[e] * hv[e];
-        *reinterpret_cast<u32x4*>(xs + (long)m * K + 8 * c) = pack8(hv);
+        for (int e = 0; e < 8; ++e) s += hv[e] * hv[e];
+        ss[m] += valid ? s : 0.f;
+        if (valid) *reinterpret_cast<u32x4*>(xs + (long)m * K + 8 * c) = pack8(hv);
       }
+    };
+#pragma unroll
+    for (int p = 0; p < PW; ++p) absorb(tid + p * 64 * WV, xq[p], rq[p]);
+    for (int c = tid + PW * 64 * WV; c < nch; c += 64 * WV) {
+      u32x4 xc[M], rc[M];
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        xc[m] = ld16(x + (long)m * ldx + 8 * c);
+        rc[m] = ld16(resp + (long)m * ldx + 8 * c);
+      }
+      absorb(c, xc, rc);
     }
 #pragma unroll
     for (int m = 0; m < M; ++m) {
@@ -153,18 +209,23 @@ __global__ __launch_bounds__(64 * WV) void gemv_kernel(const bf16_t* __restrict_
       for (int v = 0; v < WV; ++v) tot += ssq[v][m];
       rs[m] = rsqrtf(tot / (float)K + na.eps);
     }
-    for (int c = tid; c < nch; c += 64 * WV) {
+    // (in place, so only the owner of a chunk writes it back)
+    auto apply = [&](int c_raw, u32x4 wq) {
+      const int c = min(c_raw, nch - 1);
       float wf[8];
-      unpack8(ld16(na.w + 8 * c), wf);
+      unpack8(wq, wf);
 #pragma unroll
       for (int m = 0; m < M; ++m) {
         float hv[8];
         unpack8(*reinterpret_cast<const u32x4*>(xs + (long)m * K + 8 * c), hv);
 #pragma unroll
         for (int e = 0; e < 8; ++e) hv[e] = hv[e] * rs[m] * wf[e];
-        *reinterpret_cast<u32x4*>(xs + (long)m * K + 8 * c) = pack8(hv);
+        if (c_raw < nch) *reinterpret_cast<u32x4*>(xs + (long)m * K + 8 * c) = pack8(hv);
       }
-    }
+    };
+#pragma unroll
+    for (int p = 0; p < PW; ++p) apply(tid + p * 64 * WV, wn[p]);
+    for (int c = tid + PW * 64 * WV; c < nch; c += 64 * WV) apply(c, ld16(na.w + 8 * c));
     __syncthreads();
   }
 
@@ -174,10 +235,10 @@ __global__ __launch_bounds__(64 * WV) void gemv_kernel(const bf16_t* __restrict_
 #pragma unroll
     for (int m = 0; m < M; ++m) acc[i][m] = 0.f;
 
-  for (int j0 = jb; j0 < je; j0 += GV_U) {
+  for (int j0 = jb; j0 < je; j0 += U) {
     if (j0 > jb) load_w(j0);
 #pragma unroll
-    for (int u = 0; u < GV_U; ++u) {
+    for (int u = 0; u < U; ++u) {
       const int c = lane + 64 * (j0 + u);
       if (j0 + u >= je || c >= nch) continue;
 #pragma unroll
@@ -217,7 +278,7 @@ __global__ __launch_bounds__(64 * WV) void gemv_kernel(const bf16_t* __restrict_
       for (int m = 0; m < M; ++m) acc[i][m] = red[0][i][m] + red[1][i][m] + red[2][i][m] + red[3][i][m];
   }
   if (lane < R * M) {
-    const int i = lane / M, m = lane % M;
+    const int i = ep_i, m = ep_m;
     float g = 0.f, u = 0.f;
 #pragma unroll
     for (int a = 0; a < R; ++a)
@@ -233,10 +294,10 @@ __global__ __launch_bounds__(64 * WV) void gemv_kernel(const bf16_t* __restrict_
       if constexpr (SWIGLU) g = g * sigmoidf_(g) * u;
       if constexpr (ROPE) {
         // same arithmetic as rope_append_kernel on the bf16 GEMM output
-        const int head = row >> 7, d = row & 127, pr = d & 63, ps = ra.pos[m];
+        const int head = row >> 7, d = row & 127, ps = ep_pos;
         float v = bf2f(f2bf(g));
         if (head < ra.hq + ra.hkv) {
-          const float o = bf2f(f2bf(u)), c = ra.cos_t[(long)ps * 64 + pr], sn = ra.sin_t[(long)ps * 64 + pr];
+          const float o = bf2f(f2bf(u)), c = ep_cos, sn = ep_sin;
           v = d < 64 ? v * c - o * sn : v * c + o * sn;
         }
         const bf16_t vb = f2bf(v);
@@ -244,7 +305,7 @@ __global__ __launch_bounds__(64 * WV) void gemv_kernel(const bf16_t* __restrict_
         if (head >= ra.hq) {
           const bool is_v = head >= ra.hq + ra.hkv;
           const int kh = is_v ? head - ra.hq - ra.hkv : head - ra.hq;
-          (is_v ? ra.vc : ra.kc)[(((long)ra.slots[m] * ra.hkv + kh) * ra.lmax + ps) * 128 + d] = vb;
+          (is_v ? ra.vc : ra.kc)[(((long)ep_slot * ra.hkv + kh) * ra.lmax + ps) * 128 + d] = vb;
         }
       } else {
         y[(long)m * ldy + row] = f2bf(g);
@@ -302,8 +363,12 @@ int gv_rope_launch(const bf16_t* x, long ldx, const bf16_t* w, int N, int K, bf1
   // so half the CUs stream twice the bytes (12.1 us, 4.2 TB/s, gpurun_out/r4u); 6-wave workgroups
   // make exactly one per CU
   if ((N / 4) % (6 * 256) == 0 && !use_ksplit(blocks, M, K, true)) {
-    hipLaunchKernelGGL((gemv_kernel<M, 4, false, true, true, 1, 6>), dim3(N / 24), dim3(64 * 6), (size_t)M * K * 2,
-                       st, x, ldx, w, N, K, y, ldy, 0, na, ra);
+    if (K <= 8 * 512)   // the whole row in one round of loads (8 chunks per lane)
+      hipLaunchKernelGGL((gemv_kernel<M, 4, false, true, true, 1, 6, 8>), dim3(N / 24), dim3(64 * 6),
+                         (size_t)M * K * 2, st, x, ldx, w, N, K, y, ldy, 0, na, ra);
+    else
+      hipLaunchKernelGGL((gemv_kernel<M, 4, false, true, true, 1, 6>), dim3(N / 24), dim3(64 * 6), (size_t)M * K * 2,
+                         st, x, ldx, w, N, K, y, ldy, 0, na, ra);
     KF_CHECK_LAUNCH();
     return 0;
   }
