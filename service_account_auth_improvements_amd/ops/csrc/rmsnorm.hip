@@ -14,6 +14,10 @@
 
 using namespace kf;
 
+// Every load of the row (a, b and w) is issued up front and unconditionally (a chunk past the
+// row re-reads its last chunk and counts nothing): with the loads under per-chunk branches hipcc
+// waited for each one in turn, 16 dependent round trips per row -- invisible on a training-sized
+// launch, but 10 us for the 8 rows of a decode step.
 template <int VPT>
 __global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(
     const bf16_t* __restrict__ a, const bf16_t* __restrict__ b, bf16_t* __restrict__ h_out,
@@ -24,26 +28,36 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(
   if (row >= rows) return;
   const int nv = H >> 3;
   const size_t base = (size_t)row * H;
-  float x[VPT][8];
+  const bool has_b = b != nullptr;
+  const bf16_t* bp = has_b ? b : a;
+  u32x4 av[VPT], bv[VPT], wv[VPT];
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int v = min(i * 64 + lane, nv - 1);
+    av[i] = ld16(a + base + v * 8);
+    bv[i] = ld16(bp + base + v * 8);
+  }
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) wv[i] = ld16(w + min(i * 64 + lane, nv - 1) * 8);
+  u32x4 hq[VPT];
   float ss = 0.f;
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
     const int v = i * 64 + lane;
-    if (v < nv) {
-      unpack8(ld16(a + base + v * 8), x[i]);
-      if (b) {
-        float t[8];
-        unpack8(ld16(b + base + v * 8), t);
+    float x[8], t[8];
+    unpack8(av[i], x);
+    unpack8(bv[i], t);
+    // the residual sum rounded to bf16 exactly as it is stored, so fwd/bwd agree (without a
+    // residual h = a, which the round trip leaves unchanged)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) x[i][j] += t[j];
-        // round the residual sum to bf16 exactly as it is stored, so fwd/bwd agree
-        u32x4 hv = pack8(x[i]);
-        st16(h_out + base + v * 8, hv);
-        unpack8(hv, x[i]);
-      }
+    for (int j = 0; j < 8; ++j) x[j] += has_b ? t[j] : 0.f;
+    hq[i] = pack8(x);
+    if (has_b && v < nv) st16(h_out + base + v * 8, hq[i]);
+    unpack8(hq[i], x);
+    float s = 0.f;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) ss += x[i][j] * x[i][j];
-    }
+    for (int j = 0; j < 8; ++j) s += x[j] * x[j];
+    ss += v < nv ? s : 0.f;
   }
   ss = wave_sum(ss);
   const float r = rsqrtf(ss / (float)H + eps);
@@ -52,10 +66,11 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(
   for (int i = 0; i < VPT; ++i) {
     const int v = i * 64 + lane;
     if (v < nv) {
-      float wf[8], o[8];
-      unpack8(ld16(w + v * 8), wf);
+      float x[8], wf[8], o[8];
+      unpack8(hq[i], x);
+      unpack8(wv[i], wf);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = x[i][j] * r * wf[j];
+      for (int j = 0; j < 8; ++j) o[j] = x[j] * r * wf[j];
       st16(y + base + v * 8, pack8(o));
     }
   }
