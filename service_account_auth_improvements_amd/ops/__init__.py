@@ -114,7 +114,8 @@ def bgemm(x, w, swiglu: bool = False, splits: int = 0):
 
 def skinny_gemm_norm_ok(x, K: int) -> bool:
     """True when the fused residual+RMSNorm decode GEMM handles these rows."""
-    return x.is_cuda and x.shape[0] <= 4 and x.shape[0] * K <= 32768 and K % 256 == 0
+    M = x.shape[0]
+    return x.is_cuda and 1 <= M <= 8 and (4 if M <= 4 else 8) * K <= 32768 and K % 256 == 0
 
 
 def skinny_gemm_norm(x, residual, norm_w, eps, w, swiglu: bool = False):

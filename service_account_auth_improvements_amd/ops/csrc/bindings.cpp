@@ -582,7 +582,8 @@ std::tuple<at::Tensor, at::Tensor> skinny_gemm_norm(const at::Tensor& x, const s
   TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && w.dim() == 2 && w.is_contiguous(), "skinny_gemm_norm: 2-D operands");
   const int64_t M = x.size(0), K = x.size(1), Nw = w.size(0);
   TORCH_CHECK(w.size(1) == K && nw.numel() == K && nw.is_contiguous(), "skinny_gemm_norm: K mismatch");
-  TORCH_CHECK(M >= 1 && M <= 8 && M * K <= 32768 && K % 256 == 0, "skinny_gemm_norm: needs M <= 8, M*K <= 32768, K % 256 == 0");
+  TORCH_CHECK(M >= 1 && M <= 8 && (M <= 4 ? 4 : 8) * K <= 32768 && K % 256 == 0,
+              "skinny_gemm_norm: needs M <= 8, K % 256 == 0 and K <= 8192 (M <= 4) / 4096 (M <= 8)");
   TORCH_CHECK(!swiglu || Nw % 2 == 0, "skinny_gemm_norm: swiglu needs an even number of rows");
   const int64_t N = swiglu ? Nw / 2 : Nw;
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());

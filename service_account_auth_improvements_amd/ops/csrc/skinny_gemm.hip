@@ -47,11 +47,13 @@ struct NormArgs {
 constexpr int NORM_MAX_ROWS = 8;
 constexpr int NORM_LDS = 64 * 1024;   // staged normalised X: rows * K * 2 bytes
 
-template <int NT, bool SWIGLU, int UNROLL, bool NORM>
+// MR: row slots of the norm prologue's LDS image (0 = no prologue; 4 or 8, >= M)
+template <int NT, bool SWIGLU, int UNROLL, int MR>
 __global__ __launch_bounds__(64 * WAVES) void skinny_gemm_kernel(const bf16_t* __restrict__ x, long ldx, int M,
                                                                  const bf16_t* __restrict__ w, int K,
                                                                  bf16_t* __restrict__ y, long ldy, int up_off,
                                                                  NormArgs na) {
+  constexpr bool NORM = MR > 0;
   __shared__ float red[WAVES][SWIGLU ? 2 : 1][NT][16 * 16];
   extern __shared__ __attribute__((aligned(16))) bf16_t xs[];   // NORM: staged X, M * K (dynamic)
   __shared__ float ssq[NORM ? WAVES * NORM_MAX_ROWS : 1];
@@ -76,58 +78,93 @@ __global__ __launch_bounds__(64 * WAVES) void skinny_gemm_kernel(const bf16_t* _
       if (SWIGLU) au[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wu + k + 32 * i));
     }
   };
-  load_w(0);   // the weight stream starts before the (NORM) prologue
   if constexpr (NORM) {
-    // h = bf16(x + res) -> sum of squares per row -> y = bf16(h * rstd * w) into LDS
+    // h = bf16(x + res) -> sum of squares per row -> y = bf16(h * rstd * w) into LDS.  The first
+    // pass's x, residual and gain chunks are loaded AHEAD of the weight stream and
+    // unconditionally (rows past M repeat row M - 1, a chunk past the row its last chunk; none
+    // of them is stored), so the prologue waits for them alone while the weights stream in; under
+    // per-row branches hipcc waited for every load in flight.
     const int nch = K / 8;                   // 16-byte chunks per row
-    float ss[NORM_MAX_ROWS];
+    const bool has_res = na.res != nullptr;
+    const bf16_t* resp = has_res ? na.res : x;
+    u32x4 xq[MR], rq[MR];
+    const int c0 = min(tid, nch - 1);
 #pragma unroll
-    for (int m = 0; m < NORM_MAX_ROWS; ++m) ss[m] = 0.f;
-    for (int c = tid; c < nch; c += 64 * WAVES) {
+    for (int m = 0; m < MR; ++m) {
+      // row offsets in VGPRs: 16 wave-uniform row pointers held in SGPRs spilled
+      long off = (long)min(m, M - 1) * ldx + 8 * c0;
+      asm volatile("" : "+v"(off));
+      xq[m] = ld16(x + off);
+      rq[m] = ld16(resp + off);
+    }
+    const u32x4 wn0 = ld16(na.w + 8 * c0);
+    load_w(0);
+    float ss[MR];
 #pragma unroll
-      for (int m = 0; m < NORM_MAX_ROWS; ++m) {
-        if (m >= M) break;
-        float hv[8];
-        unpack8(ld16(x + (long)m * ldx + 8 * c), hv);
-        if (na.res) {
-          float t[8];
-          unpack8(ld16(na.res + (long)m * ldx + 8 * c), t);
+    for (int m = 0; m < MR; ++m) ss[m] = 0.f;
+    auto absorb = [&](int c, const u32x4* xc, const u32x4* rc, bool valid) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) hv[j] += t[j];
-          const u32x4 hb = pack8(hv);        // the residual stream is stored (and normed) as bf16
-          if (blockIdx.x == 0) st16(na.h_out + (long)m * na.ldh + 8 * c, hb);
-          unpack8(hb, hv);
-        }
+      for (int m = 0; m < MR; ++m) {
+        float hv[8], tv[8];
+        unpack8(xc[m], hv);
+        unpack8(rc[m], tv);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) ss[m] += hv[j] * hv[j];
-        st16(xs + (long)m * K + 8 * c, pack8(hv));   // un-normalised h for now
+        for (int j = 0; j < 8; ++j) hv[j] += has_res ? tv[j] : 0.f;
+        const u32x4 hb = pack8(hv);          // the residual stream is stored (and normed) as bf16
+        if (has_res && valid && m < M && blockIdx.x == 0) st16(na.h_out + (long)m * na.ldh + 8 * c, hb);
+        unpack8(hb, hv);
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += hv[j] * hv[j];
+        ss[m] += valid ? s : 0.f;
+        // (the LDS image has MR >= M row slots: rows past M hold duplicates, never read)
+        if (valid) *reinterpret_cast<u32x4*>(xs + (long)m * K + 8 * c) = hb;   // un-normalised h for now
       }
+    };
+    absorb(c0, xq, rq, tid < nch);
+    for (int c = tid + 64 * WAVES; c < nch; c += 64 * WAVES) {
+      u32x4 xc[MR], rc[MR];
+#pragma unroll
+      for (int m = 0; m < MR; ++m) {
+        long off = (long)min(m, M - 1) * ldx + 8 * c;
+        asm volatile("" : "+v"(off));
+        xc[m] = ld16(x + off);
+        rc[m] = ld16(resp + off);
+      }
+      absorb(c, xc, rc, true);
     }
 #pragma unroll
-    for (int m = 0; m < NORM_MAX_ROWS; ++m) {
-      if (m >= M) break;
+    for (int m = 0; m < MR; ++m) {
       const float v = wave_sum(ss[m]);
-      if (l == 0) ssq[wave * NORM_MAX_ROWS + m] = v;
+      if (l == 0) ssq[wave * MR + m] = v;
     }
     __syncthreads();
-    for (int c = tid; c < nch; c += 64 * WAVES) {
+    float rs[MR];
+#pragma unroll
+    for (int m = 0; m < MR; ++m) {
+      float tot = 0.f;
+#pragma unroll
+      for (int v = 0; v < WAVES; ++v) tot += ssq[v * MR + m];
+      rs[m] = rsqrtf(tot / (float)K + na.eps);
+    }
+    // in place, so only the owner of a chunk reads and writes it
+    auto apply = [&](int c, u32x4 wq) {
       float wf[8];
-      unpack8(ld16(na.w + 8 * c), wf);
+      unpack8(wq, wf);
 #pragma unroll
-      for (int m = 0; m < NORM_MAX_ROWS; ++m) {
-        if (m >= M) break;
-        float tot = 0.f;
-#pragma unroll
-        for (int v = 0; v < WAVES; ++v) tot += ssq[v * NORM_MAX_ROWS + m];
-        const float rs = rsqrtf(tot / (float)K + na.eps);
+      for (int m = 0; m < MR; ++m) {
         float hv[8];
         unpack8(*reinterpret_cast<const u32x4*>(xs + (long)m * K + 8 * c), hv);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) hv[j] = hv[j] * rs * wf[j];
+        for (int j = 0; j < 8; ++j) hv[j] = hv[j] * rs[m] * wf[j];
         *reinterpret_cast<u32x4*>(xs + (long)m * K + 8 * c) = pack8(hv);
       }
-    }
+    };
+    if (tid < nch) apply(tid, wn0);
+    for (int c = tid + 64 * WAVES; c < nch; c += 64 * WAVES) apply(c, ld16(na.w + 8 * c));
     __syncthreads();
+  } else {
+    load_w(0);
   }
 
   for (int k = 0; k < kw; k += 32 * UNROLL) {
@@ -176,19 +213,19 @@ __global__ __launch_bounds__(64 * WAVES) void skinny_gemm_kernel(const bf16_t* _
   }
 }
 
-template <int NT, bool SWIGLU, bool NORM = false>
+template <int NT, bool SWIGLU, int MR = 0>
 int launch(const bf16_t* x, long ldx, int M, const bf16_t* w, int N, int K, bf16_t* y, long ldy, int up_off,
            hipStream_t st, NormArgs na = NormArgs{}) {
   dim3 grid(N / 16), block(64 * WAVES);
-  const size_t dyn = NORM ? (size_t)M * K * 2 : 0;   // LDS sized to the rows: B = 1 keeps occupancy
+  const size_t dyn = (size_t)MR * K * 2;   // the norm prologue's staged X (MR row slots)
   if (K % (WAVES * 32 * 8) == 0)
-    hipLaunchKernelGGL((skinny_gemm_kernel<NT, SWIGLU, 8, NORM>), grid, block, dyn, st, x, ldx, M, w, K, y, ldy, up_off, na);
+    hipLaunchKernelGGL((skinny_gemm_kernel<NT, SWIGLU, 8, MR>), grid, block, dyn, st, x, ldx, M, w, K, y, ldy, up_off, na);
   else if (K % (WAVES * 32 * 4) == 0)
-    hipLaunchKernelGGL((skinny_gemm_kernel<NT, SWIGLU, 4, NORM>), grid, block, dyn, st, x, ldx, M, w, K, y, ldy, up_off, na);
+    hipLaunchKernelGGL((skinny_gemm_kernel<NT, SWIGLU, 4, MR>), grid, block, dyn, st, x, ldx, M, w, K, y, ldy, up_off, na);
   else if (K % (WAVES * 32 * 2) == 0)
-    hipLaunchKernelGGL((skinny_gemm_kernel<NT, SWIGLU, 2, NORM>), grid, block, dyn, st, x, ldx, M, w, K, y, ldy, up_off, na);
+    hipLaunchKernelGGL((skinny_gemm_kernel<NT, SWIGLU, 2, MR>), grid, block, dyn, st, x, ldx, M, w, K, y, ldy, up_off, na);
   else
-    hipLaunchKernelGGL((skinny_gemm_kernel<NT, SWIGLU, 1, NORM>), grid, block, dyn, st, x, ldx, M, w, K, y, ldy, up_off, na);
+    hipLaunchKernelGGL((skinny_gemm_kernel<NT, SWIGLU, 1, MR>), grid, block, dyn, st, x, ldx, M, w, K, y, ldy, up_off, na);
   KF_CHECK_LAUNCH();
   return 0;
 }
@@ -196,15 +233,23 @@ int launch(const bf16_t* x, long ldx, int M, const bf16_t* w, int N, int K, bf16
 }  // namespace
 
 // y = (rmsnorm(x + res) * w_norm) . W^T  [SwiGLU epilogue when swiglu]; h_out = x + res.
-// Needs M <= NORM_MAX_ROWS and M * K * 2 <= NORM_LDS (the staged X); returns 1 otherwise.
+// Needs M <= NORM_MAX_ROWS and the staged X (4 row slots up to M = 4, else 8) x K x 2 bytes
+// <= NORM_LDS; returns 1 otherwise.
 extern "C" int kf_skinny_gemm_norm(const void* x, long ldx, int M, const void* res, const void* nw, float eps,
                                    void* h_out, long ldh, const void* w, int N, int K, void* y, long ldy,
                                    int swiglu, int up_off, hipStream_t st) {
-  if (M <= 0 || M > NORM_MAX_ROWS || (long)M * K * 2 > NORM_LDS || N % 16 != 0 || K % (WAVES * 32) != 0) return 1;
+  const int mr = M <= 4 ? 4 : NORM_MAX_ROWS;
+  if (M <= 0 || M > NORM_MAX_ROWS || (long)mr * K * 2 > NORM_LDS || N % 16 != 0 || K % (WAVES * 32) != 0) return 1;
   if (res && !h_out) return 1;
   const NormArgs na{(const bf16_t*)res, (const bf16_t*)nw, (bf16_t*)h_out, ldh, eps};
-  if (swiglu) return launch<1, true, true>((const bf16_t*)x, ldx, M, (const bf16_t*)w, N, K, (bf16_t*)y, ldy, up_off, st, na);
-  return launch<1, false, true>((const bf16_t*)x, ldx, M, (const bf16_t*)w, N, K, (bf16_t*)y, ldy, 0, st, na);
+  auto X = (const bf16_t*)x;
+  auto W = (const bf16_t*)w;
+  auto Y = (bf16_t*)y;
+  if (mr == 4)
+    return swiglu ? launch<1, true, 4>(X, ldx, M, W, N, K, Y, ldy, up_off, st, na)
+                  : launch<1, false, 4>(X, ldx, M, W, N, K, Y, ldy, 0, st, na);
+  return swiglu ? launch<1, true, NORM_MAX_ROWS>(X, ldx, M, W, N, K, Y, ldy, up_off, st, na)
+                : launch<1, false, NORM_MAX_ROWS>(X, ldx, M, W, N, K, Y, ldy, 0, st, na);
 }
 
 // swiglu: W holds [gate (up_off rows); up (up_off rows)], N = up_off, Y = silu(X.Wg^T) * (X.Wu^T)

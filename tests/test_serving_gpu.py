@@ -202,7 +202,11 @@ def test_gemv_odd_shapes(M, N, K, swiglu):
 
 
 @pytest.mark.parametrize("M,N,K,swiglu,res", [(1, 6144, 4096, False, True), (1, 14336, 4096, True, True),
-                                              (4, 6144, 4096, False, False), (8, 2048, 4096, True, True)])
+                                              (4, 6144, 4096, False, False), (8, 2048, 4096, True, True),
+                                              # MFMA kernel, 4 row slots (TP-shard sizes, K up to 8192)
+                                              (3, 768, 4096, False, True), (4, 1024, 8192, True, False),
+                                              # 8 row slots: the batch 5-8 decode projections
+                                              (6, 6144, 4096, False, True), (5, 14336, 4096, True, False)])
 def test_skinny_gemm_norm_matches_unfused(M, N, K, swiglu, res):
     """Residual-add + RMSNorm prologue fused into the decode GEMM == rmsnorm_fwd + skinny_gemm."""
     from service_account_auth_improvements_amd import ops
