@@ -114,8 +114,10 @@ def bgemm(x, w, swiglu: bool = False, splits: int = 0):
 
 def skinny_gemm_norm_ok(x, K: int) -> bool:
     """True when the fused residual+RMSNorm decode GEMM handles these rows."""
-    M = x.shape[0]
-    return x.is_cuda and 1 <= M <= 8 and (4 if M <= 4 else 8) * K <= 32768 and K % 256 == 0
+    # up to 4 rows: at 5-8 the MFMA kernel with the prologue holds 131-163 VGPRs (one workgroup per
+    # CU) and the unfused RMSNorm + skinny GEMM pair is faster: batch 8 4.77 vs 5.27 ms per step
+    # (profiles/serve_gemv_upfront_loads_r4.txt)
+    return x.is_cuda and 1 <= x.shape[0] <= 4 and 4 * K <= 32768 and K % 256 == 0
 
 
 def skinny_gemm_norm(x, residual, norm_w, eps, w, swiglu: bool = False):
