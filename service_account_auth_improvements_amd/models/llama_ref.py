@@ -26,14 +26,29 @@ def _rope(x, cos, sin):
     return torch.cat([a * c - b * s, b * c + a * s], -1)
 
 
+def _weights(model, dtype):
+    assert model.tp == 1
+    names = [s.name for g in model.groups for s in g.specs]
+    return {n: model.P(n).detach().to(dtype).clone().requires_grad_(True) for n in names}
+
+
 def reference_loss(model, tokens, labels, dtype=torch.float32):
     """Returns (mean loss, {name: fp32 leaf weight}) -- call .backward() for grads."""
+    W = _weights(model, dtype)
+    logits = _logits(model, tokens, W, dtype)
+    loss = F.cross_entropy(logits.reshape(-1, logits.shape[-1]), labels.reshape(-1))
+    return loss, W
+
+
+@torch.no_grad()
+def reference_last_logits(model, tokens, dtype=torch.float32):
+    """fp32 logits of the LAST position of each row of ``tokens`` [B, S] (decode oracle)."""
+    W = _weights(model, dtype)
+    return _logits(model, tokens, W, dtype, last_only=True)
+
+
+def _logits(model, tokens, W, dtype, last_only=False):
     cfg = model.cfg
-    assert model.tp == 1
-    W = {}
-    names = [s.name for g in model.groups for s in g.specs]
-    for n in names:
-        W[n] = model.P(n).detach().to(dtype).clone().requires_grad_(True)
     B, S = tokens.shape
     H, D, Hq, Hkv = cfg.hidden, cfg.head_dim, cfg.n_heads, cfg.n_kv_heads
     cos, sin = model.cos[:S].to(dtype), model.sin[:S].to(dtype)
@@ -58,7 +73,7 @@ def reference_loss(model, tokens, labels, dtype=torch.float32):
         gu = m @ W[f"l{i}.wgu"].t()
         g, u = gu[..., : cfg.ffn], gu[..., cfg.ffn:]
         x = x + (F.silu(g) * u) @ W[f"l{i}.wd"].t()
+    if last_only:
+        x = x[:, -1]
     y = _rms(x, W["final_norm"], cfg.norm_eps)
-    logits = y @ W["lm_head"].t()
-    loss = F.cross_entropy(logits.reshape(-1, logits.shape[-1]), labels.reshape(-1))
-    return loss, W
+    return y @ W["lm_head"].t()

@@ -357,6 +357,37 @@ def test_persistent_decode_step_matches_kernel_per_op(ctxs):
         toks = ref.argmax(-1).tolist()
 
 
+@pytest.mark.parametrize("ctxs", [[1024], [8000], [7000, 100, 4000, 1]], ids=["b1-1k", "b1-8k", "b4-to-7k"])
+def test_persistent_and_kernel_per_op_decode_match_fp32(ctxs):
+    """Both decode paths (persistent kernel, kernel-per-op) against the fp32 autograd-free
+    oracle (models/llama_ref.py) on the full prompt + new token, Llama-3-8B shapes (2 layers),
+    contexts 1k / 8k at batch 1 and mixed lengths up to 7k at batch 4."""
+    from service_account_auth_improvements_amd.models.llama_ref import reference_last_logits
+    B = len(ctxs)
+    e = _llama8b_engine(2, use_graphs=False, max_len=8192)
+    persist = e.persist
+    assert persist is not None
+    g = torch.Generator().manual_seed(sum(ctxs) + 1)
+    prompts = [torch.randint(0, e.cfg.vocab_size, (c,), generator=g).tolist() for c in ctxs]
+    for b, p in enumerate(prompts):
+        e.prefill(b, p)
+    toks = [int(x) for x in torch.randint(0, e.cfg.vocab_size, (B,), generator=g)]
+    slots, pos = list(range(B)), list(ctxs)
+    kc0, vc0 = e.kc.clone(), e.vc.clone()
+    got_p = e.decode(toks, slots, pos).float()
+    assert e.persist is persist and not persist.failed()
+    e.kc.copy_(kc0)
+    e.vc.copy_(vc0)
+    e.persist = None
+    got_k = e.decode(toks, slots, pos).float()
+    for b in range(B):
+        ref = reference_last_logits(e.m, torch.tensor([prompts[b] + [toks[b]]], device=DEV))[0].float()
+        for name, got in (("persistent", got_p[b]), ("kernel-per-op", got_k[b])):
+            cos = torch.nn.functional.cosine_similarity(got, ref, dim=0)
+            assert cos > 0.995, (name, b, float(cos))
+            assert (got - ref).abs().max() <= 0.08 * ref.abs().max(), (name, b)
+
+
 def test_persistent_decode_step_in_a_graph_replays_identically():
     """Captured in the bucket-1 HIP graph (memset + kernel nodes), replays give the eager
     persistent kernel's logits bit for bit, step after step."""
