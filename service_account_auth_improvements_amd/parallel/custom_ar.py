@@ -185,6 +185,8 @@ class TwoShot:
         """``dist.reduce_scatter_tensor(out, x)``: out = rank r's 1/N block of the sum."""
         if not (out.is_contiguous() and self.supports(x.numel(), x)):
             return dist.reduce_scatter_tensor(out, x, group=self.group, async_op=async_op)
+        if out.numel() * self.world != x.numel() or out.dtype != x.dtype or out.device != x.device:
+            raise ValueError(f"reduce_scatter: out {tuple(out.shape)} is not 1/{self.world} of x {tuple(x.shape)}")
         w = self._run(1, x, out, async_op)
         return w if async_op else None
 
@@ -192,6 +194,8 @@ class TwoShot:
         """``dist.all_gather_into_tensor(out, x)``: out = every rank's x in rank order."""
         if not (out.is_contiguous() and self.supports(out.numel(), x)):
             return dist.all_gather_into_tensor(out, x, group=self.group, async_op=async_op)
+        if x.numel() * self.world != out.numel() or out.dtype != x.dtype or out.device != x.device:
+            raise ValueError(f"all_gather: out {tuple(out.shape)} is not {self.world} x {tuple(x.shape)}")
         w = self._run(2, x, out, async_op)
         return w if async_op else None
 
