@@ -121,7 +121,10 @@ def _preflight(a) -> None:
 
 
 def _crd_gate_path() -> str:
-    tag = f"{os.environ.get('MASTER_PORT', '0')}_{os.environ.get('TORCHELASTIC_RUN_ID', 'none')}"
+    # one marker per launch: the local ranks of one torchrun share its agent as their parent, and
+    # back-to-back launches (N = 2, 4, 8 on one port) must never see a previous launch's marker
+    tag = (f"{os.environ.get('MASTER_PORT', '0')}_{os.environ.get('TORCHELASTIC_RUN_ID', 'none')}"
+           f"_{os.getppid()}")
     return os.path.join(os.environ.get("TMPDIR", "/tmp"), f"kfamd_bench_crd_{tag}.json")
 
 
@@ -249,6 +252,8 @@ def main():
     dog = progress.Watchdog(a.hang_timeout + (0 if rank == 0 else 15),
                             lambda: {"metric": BASELINE_METRIC, "value": None, "n_gpus": a.gpus, "rank": rank},
                             to_stdout=rank == 0).start()
+    gate = _crd_gate_path() if (env_world is not None and int(env_world) > 1 and rank == 0
+                                and CRD_ENV not in os.environ and a.crd_jobs > 0) else None
     try:
         _run(a, rank, crd)
     except SystemExit:
@@ -261,6 +266,8 @@ def main():
         raise
     finally:
         dog.stop()
+        if gate is not None and os.path.exists(gate):
+            os.remove(gate)
 
 
 def _run(a, rank: int, crd):

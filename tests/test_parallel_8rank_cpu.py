@@ -93,7 +93,7 @@ def test_bench_refuses_more_gpus_than_visible():
 
 
 @pytest.mark.parametrize("launcher", ["self", "torchrun"])
-def test_bench_crd_jobs_run_at_the_bench_world_size(launcher):
+def test_bench_crd_jobs_run_at_the_bench_world_size(launcher, tmp_path):
     """The CRD-to-first-step half at N > 1 submits N-rank PyTorchJobs (nprocPerNode = N, so
     the N-rank rendezvous is inside the clock).  Under an external torchrun rank 0 measures while
     the other ranks wait, and the job's pods must not inherit rank 0's launcher identity
@@ -104,9 +104,15 @@ def test_bench_crd_jobs_run_at_the_bench_world_size(launcher):
     if launcher == "torchrun":
         args = ["-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}", "--master-addr", "127.0.0.1",
                 "--master-port", "29937", *args]
-    r = subprocess.run([sys.executable, *args], capture_output=True, text=True, timeout=600, env=_cpu_env(),
+    env = _cpu_env()
+    env["TMPDIR"] = str(tmp_path)
+    # a previous launch's marker (same port, another launcher process) must not release the ranks
+    (tmp_path / "kfamd_bench_crd_29937_none.json").write_text("{}")
+    r = subprocess.run([sys.executable, *args], capture_output=True, text=True, timeout=600, env=env,
                        cwd="/tmp")
     assert r.returncode == 0, r.stderr[-3000:]
+    # rank 0 removes its own marker: nothing is left for the next launch on this port
+    assert sorted(p.name for p in tmp_path.glob("kfamd_bench_crd_*")) == ["kfamd_bench_crd_29937_none.json"]
     rec = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")][-1]
     crd = rec["crd_to_first_step"]
     assert "error" not in crd, crd
