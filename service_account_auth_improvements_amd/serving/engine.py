@@ -281,6 +281,13 @@ class Engine:
     def _mm(self, x, w):
         """Decode GEMM: the skinny weight-streaming kernels for small batches on the GPU, the
         batched-decode GEMM up to 256 rows, hipBLASLt beyond."""
+        # 9-16 rows, deep narrow weights (wd: K = 14336, N = 4096): the skinny kernel's 256
+        # workgroups walk K in 7 serial rounds; the batched-decode GEMM splits K over the CUs
+        # (batch 16: 5.43 -> 5.30 ms per step; batch 8 and the K = 4096 projections: no gain or
+        # worse, profiles/serve_gemv_upfront_loads_r4.txt)
+        if (x.is_cuda and 8 < x.shape[0] <= SKINNY_MAX_ROWS and w.shape[1] >= 8192 and BGEMM and self.m.tp == 1
+                and w.shape[0] <= BGEMM_MAX_N and ops.bgemm_ok(x, w)):
+            return ops.bgemm(x, w)
         if x.is_cuda and (x.shape[0] <= GEMV_MAX_ROWS or (
                 x.shape[0] <= SKINNY_MAX_ROWS and w.shape[0] <= SKINNY_MAX_N and w.shape[1] % 256 == 0)):
             return ops.skinny_gemm(x, w)
