@@ -138,7 +138,9 @@ __global__ __launch_bounds__(64 * WV) void gemv_kernel(const bf16_t* __restrict_
     for (int i = 0; i < NR; ++i)
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int c = min(lane + 64 * (j0 + u), nch - 1);
+        // slots past this wave's K range repeat its last slot (never another wave's: with a K
+        // split that would stream the neighbour's weights a second time)
+        const int c = min(lane + 64 * min(j0 + u, je - 1), nch - 1);
         wv[i][u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(row_ptr(i) + 8 * c));
       }
   };
