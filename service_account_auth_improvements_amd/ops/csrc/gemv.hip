@@ -335,7 +335,11 @@ int gv_launch(const bf16_t* x, long ldx, const bf16_t* w, int N, int K, bf16_t* 
   constexpr int R = SWIGLU ? (GV_R_CFG > 1 ? GV_R_CFG / 2 : 1) : GV_R_CFG;
   const int blocks = (N + R * GV_WAVES - 1) / (R * GV_WAVES);
   const size_t dyn = NORM ? (size_t)M * K * 2 : 0;
-  if (use_ksplit(blocks, M, K, NORM))
+  const int jw = ((K / 8 + 63) / 64 + GV_WAVES - 1) / GV_WAVES;   // K-split: chunk slots per wave
+  if (use_ksplit(blocks, M, K, NORM) && jw <= 2)   // (wo: 2 slots, no round of repeated loads)
+    hipLaunchKernelGGL((gemv_kernel<M, R, SWIGLU, NORM, false, GV_WAVES, GV_WAVES, 2>), dim3((N + R - 1) / R),
+                       dim3(64 * GV_WAVES), dyn, st, x, ldx, w, N, K, y, ldy, up_off, na, GvRope{});
+  else if (use_ksplit(blocks, M, K, NORM))
     hipLaunchKernelGGL((gemv_kernel<M, R, SWIGLU, NORM, false, GV_WAVES>), dim3((N + R - 1) / R),
                        dim3(64 * GV_WAVES), dyn, st, x, ldx, w, N, K, y, ldy, up_off, na, GvRope{});
   else
