@@ -369,12 +369,10 @@ int gv_rope_launch(const bf16_t* x, long ldx, const bf16_t* w, int N, int K, bf1
   // so half the CUs stream twice the bytes (12.1 us, 4.2 TB/s, gpurun_out/r4u); 6-wave workgroups
   // make exactly one per CU
   if ((N / 4) % (6 * 256) == 0 && !use_ksplit(blocks, M, K, true)) {
-    if (K <= 8 * 512)   // the whole row in one round of loads (8 chunks per lane)
-      hipLaunchKernelGGL((gemv_kernel<M, 4, false, true, true, 1, 6, 8>), dim3(N / 24), dim3(64 * 6),
-                         (size_t)M * K * 2, st, x, ldx, w, N, K, y, ldy, 0, na, ra);
-    else
-      hipLaunchKernelGGL((gemv_kernel<M, 4, false, true, true, 1, 6>), dim3(N / 24), dim3(64 * 6), (size_t)M * K * 2,
-                         st, x, ldx, w, N, K, y, ldy, 0, na, ra);
+    // (the whole row in one round of 8 loads per lane: equal at 1 row, 0.6-0.7 % slower at 2-4,
+    // gpurun_out/r4an)
+    hipLaunchKernelGGL((gemv_kernel<M, 4, false, true, true, 1, 6>), dim3(N / 24), dim3(64 * 6), (size_t)M * K * 2,
+                       st, x, ldx, w, N, K, y, ldy, 0, na, ra);
     KF_CHECK_LAUNCH();
     return 0;
   }
