@@ -14,6 +14,9 @@
 #   pmc:BIN[:A,B,..]        two PMC passes over a kbench binary (tools/kbench/pmc.sh)
 #   tool:SCRIPT[:A,B,..]    python -u tools/SCRIPT A B ..                       -> OUTDIR/SCRIPT.log
 #   env:VAR=VALUE           export VAR=VALUE for the steps after it (env:VAR= unsets it)
+#   ext:FILE                install the prebuilt extension FILE as ops/_kfamd_ops.so for the steps
+#                           after it (A/B of two builds in one session; the tree's own build is put
+#                           back when the session ends)
 # Counter runs never combine --pmc with trace domains; nothing here sets GPU_MAX_HW_QUEUES.
 set -o pipefail
 export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
@@ -21,6 +24,10 @@ O=${1:?usage: gpu_session.sh OUTDIR STEP...}
 shift
 mkdir -p "$O"
 n=0
+EXT=service_account_auth_improvements_amd/ops/_kfamd_ops.so
+EXT_SAVED=""
+restore_ext() { [ -n "$EXT_SAVED" ] && cp "$EXT_SAVED" "$EXT"; }
+trap restore_ext EXIT
 
 fail() { echo "step '$1' failed rc=$2"; [ -f "$3" ] && tail -40 "$3"; exit "$2"; }
 
@@ -65,6 +72,11 @@ for step in "$@"; do
       log=$O/${a1%.py}_$n.log
       timeout -k 10 600 python -u "tools/$a1" "${args[@]}" > "$log" 2>&1 || fail "$step" $? "$log"
       grep -v amdgpu.ids "$log" | tail -8 | cut -c1-300 ;;
+    ext)
+      [ -f "$a1" ] || { echo "ext: no file $a1"; exit 2; }
+      if [ -z "$EXT_SAVED" ]; then EXT_SAVED=$O/.ext_saved.so; cp "$EXT" "$EXT_SAVED"; fi
+      cp "$a1" "$EXT"
+      echo "ext $a1" ;;
     env)
       v=${step#env:}
       if [ -z "${v#*=}" ]; then unset "${v%%=*}"; else export "$v"; fi
