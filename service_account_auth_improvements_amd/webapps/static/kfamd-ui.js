@@ -305,21 +305,32 @@
     var pages = {
       index: function () {
         if (poller) poller.stop();
-        var list = el("div");
+        var list = el("div"), names = [];
         var name = el("input", { placeholder: "name" }), size = el("input", { value: "10Gi", size: 6 });
-        var mode = el("select", {}, ["ReadWriteOnce", "ReadWriteMany", "ReadOnlyMany"].map(function (m) { return el("option", { value: m }, m); }));
+        var mode = el("select", {}, ["ReadWriteOnce", "ReadOnlyMany", "ReadWriteMany"].map(function (m) { return el("option", { value: m }, m); }));
+        // storage class (form-default: "None" = {none}, the cluster's classes, the default one
+        // preselected; until the backend answers, {empty} leaves the class to the cluster default)
+        var sclass = el("select", { "data-cy": "storage class" }, el("option", { value: "{empty}" }, "(cluster default)"),
+                        el("option", { value: "{none}" }, "None"));
+        api("GET", "api/storageclasses").then(function (j) {
+          (j.storageClasses || []).forEach(function (c) { sclass.append(el("option", { value: c }, c)); });
+          return api("GET", "api/storageclasses/default");
+        }).then(function (j) { if (j && j.defaultStorageClass) sclass.value = j.defaultStorageClass; }, function () {});
         var create = el("button", { onclick: function () {
-          var err = L.dns1123Name(name.value) || L.quantity(size.value);
+          var err = L.dns1123Name(name.value) || L.quantity(size.value) ||
+                    (names.indexOf(name.value) >= 0 ? "Volume " + name.value + " already exists" : "");
           if (err) { snack(err, true); return; }
-          api("POST", "api/namespaces/" + ns + "/pvcs", { name: name.value, mode: mode.value, class: "{empty}",
+          api("POST", "api/namespaces/" + ns + "/pvcs", { name: name.value, mode: mode.value, class: sclass.value,
                                                           size: size.value, type: "new" })
             .then(function () { poller.reset(); }, function (e) { snack(e.message, true); });
         } }, "+ New volume");
-        main.replaceChildren(el("div", { class: "card" }, el("label", {}, "New volume"), el("div", {}, name, " ", size, " ", mode, " ", create)), list);
+        main.replaceChildren(el("div", { class: "card" }, el("label", {}, "New volume"),
+                                el("div", {}, name, " ", size, " ", mode, " ", sclass, " ", create)), list);
         poller = KF.poll(function () {
           if (!ns) return [];
           return api("GET", "api/namespaces/" + ns + "/pvcs").then(function (j) {
             var pvcs = j.pvcs;
+            names = pvcs.map(function (p) { return p.name; });
             list.replaceChildren(KF.table([
               ["Status", function (p) { return KF.status(p.status); }],
               ["Name", function (p) { return el("a", { href: "#/details/" + p.namespace + "/" + p.name }, p.name); }, function (p) { return p.name; }],

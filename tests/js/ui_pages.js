@@ -176,6 +176,9 @@ Promise.resolve()
   // ---------------------------------------------------------------- VWA: index + delete dialog
   .then(function () {
     return boot("volumes", { "GET api/namespaces": fx("namespaces"), "GET api/namespaces/kubeflow-user/pvcs": fx("pvcs"),
+                             "GET api/storageclasses": { storageClasses: ["fast-nvme", "standard"], success: true },
+                             "GET api/storageclasses/default": { defaultStorageClass: "standard", success: true },
+                             "POST api/namespaces/kubeflow-user/pvcs": { success: true, status: 200 },
                              "DELETE api/namespaces/kubeflow-user/pvcs/datasets": { status: 409, body: { success: false, status: 409,
                                log: "PVC datasets is used by pod zeta-trainer-0" } } }, { search: "?ns=kubeflow-user" });
   })
@@ -187,6 +190,23 @@ Promise.resolve()
     return shim.flush().then(function () {
       o.dialogStillOpen = !!env.q('[role="dialog"]');
       o.dialogError = env.text('[data-cy="dialog-error"]');
+      // the create form: storage classes from the backend, its default preselected
+      var sc = env.q('[data-cy="storage class"]');
+      o.classOptions = sc.children.map(function (c) { return c.getAttribute("value"); });
+      o.classSelected = sc.value;
+      var newBtn = env.qa("button").filter(function (b) { return b.textContent === "+ New volume"; })[0];
+      env.q('input[placeholder="name"]').type_("datasets");          // an existing volume's name
+      newBtn.click();
+      return shim.flush().then(function () {
+        o.dupSnacks = env.snacks();
+        o.dupPosts = env.requests.filter(function (r) { return r.method === "POST"; }).length;
+        env.q('input[placeholder="name"]').value = "";
+        env.q('input[placeholder="name"]').type_("scratch");
+        newBtn.click();
+        return shim.flush();
+      }).then(function () {
+        o.posts = env.requests.filter(function (r) { return r.method === "POST"; }).map(function (r) { return r.body; });
+      });
     });
   })
   // ---------------------------------------------------------------- TWA: create

@@ -163,6 +163,16 @@ def test_delete_goes_through_the_confirm_dialog(pages):
     assert v["buttons"][:2] == ["Browse", "Delete"] and "Open viewer" in v["buttons"]
 
 
+def test_vwa_form_storage_classes_and_existing_names(pages):
+    """Volume form (ref volumes/frontend pages/form/form-default): the cluster's storage classes
+    with the backend's default preselected and "None" as {none}; an existing name is refused in
+    the page (no request); a new one POSTs the body the VWA backend takes."""
+    v = pages["vwa"]
+    assert v["classOptions"] == ["{empty}", "{none}", "fast-nvme", "standard"] and v["classSelected"] == "standard"
+    assert v["dupPosts"] == 0 and any("already exists" in s[1] for s in v["dupSnacks"])
+    assert v["posts"] == [{"name": "scratch", "mode": "ReadWriteOnce", "class": "standard", "size": "10Gi", "type": "new"}]
+
+
 def test_jwa_form_drives_names_and_mounts_and_posts_the_body(pages):
     f = pages["jwaForm"]
     assert f["title"] == "New notebook"
