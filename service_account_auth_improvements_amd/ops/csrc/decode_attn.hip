@@ -186,16 +186,18 @@ __global__ __launch_bounds__(CB_NT) void decode_combine_kernel(const float* __re
   const float* po = part_o + (long)bh * splits * D + d;
   // up to 32 splits (every batch-1 launch): this thread's 16 partial values are loaded up front,
   // together with the (max, sum) pairs, so the merge costs one memory round trip, not three
+  // Loads are unconditional (indices clamped; what is past the splits is never used): under
+  // per-split branches hipcc waited for every load in flight at each one.  Up to CB_NT splits
+  // this thread's (max, sum) pair stays in registers for the weight pass below (no second read).
   constexpr int PRE = 16;
   float pre[PRE];
   const bool preload = splits <= 2 * PRE;
+  const bool one = splits <= CB_NT;
+  const f32x2_t ml_own = *reinterpret_cast<const f32x2_t*>(ml + 2 * min(tid, splits - 1));
 #pragma unroll
-  for (int i = 0; i < PRE; ++i) {
-    const int s = half + 2 * i;
-    pre[i] = (preload && s < splits) ? po[(long)s * D] : 0.f;
-  }
-  float mloc = -INFINITY;
-  for (int s = tid; s < splits; s += CB_NT) mloc = fmaxf(mloc, ml[2 * s]);
+  for (int i = 0; i < PRE; ++i) pre[i] = po[(long)min(half + 2 * i, splits - 1) * D];
+  float mloc = tid < splits ? ml_own[0] : -INFINITY;
+  for (int s = tid + CB_NT; s < splits; s += CB_NT) mloc = fmaxf(mloc, ml[2 * s]);
   mloc = wave_max(mloc);
   if (lane == 0) red[wave] = mloc;
   __syncthreads();
@@ -204,11 +206,19 @@ __global__ __launch_bounds__(CB_NT) void decode_combine_kernel(const float* __re
   for (int w = 1; w < CB_NT / 64; ++w) M = fmaxf(M, red[w]);
   __syncthreads();
   float dl = 0.f;
-  for (int s = tid; s < splits; s += CB_NT) {
-    const float m = ml[2 * s];
-    const float w = m == -INFINITY ? 0.f : exp2f(m - M);
-    ws[s] = w;
-    dl = fmaf(w, ml[2 * s + 1], dl);
+  if (one) {
+    if (tid < splits) {
+      const float w = ml_own[0] == -INFINITY ? 0.f : exp2f(ml_own[0] - M);
+      ws[tid] = w;
+      dl = w * ml_own[1];
+    }
+  } else {
+    for (int s = tid; s < splits; s += CB_NT) {
+      const float m = ml[2 * s];
+      const float w = m == -INFINITY ? 0.f : exp2f(m - M);
+      ws[s] = w;
+      dl = fmaf(w, ml[2 * s + 1], dl);
+    }
   }
   dl = wave_sum(dl);
   if (lane == 0) red[wave] = dl;
