@@ -248,6 +248,12 @@ def main():
         if env_world is not None and int(env_world) > 1 and a.crd_jobs > 0:
             crd = _crd_gate(a, rank, crd)
     os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+    # a stale in-tree kernel library is rebuilt HERE, before the no-progress watchdog is armed: a
+    # cold build of every .hip file can outlast --hang-timeout and must not read as a hang (CPU
+    # only, nothing touches the GPU; a no-op hash compare when the library is current)
+    if os.environ.get("KFAMD_NO_BUILD") != "1":
+        from service_account_auth_improvements_amd.ops import _build
+        _build.build()
     # rank 0 reports first: the other ranks' watchdogs give it 15 s before they exit themselves
     dog = progress.Watchdog(a.hang_timeout + (0 if rank == 0 else 15),
                             lambda: {"metric": BASELINE_METRIC, "value": None, "n_gpus": a.gpus, "rank": rank},

@@ -468,6 +468,8 @@ class PyTorchJobReconciler(_JobBase):
             for kv in ep.get("rdzvConf") or []:
                 if kv.get("key") == "last_call_timeout":
                     over["KFAMD_RDZV_LAST_CALL"] = str(kv.get("value"))
+                elif kv.get("key") == "join_timeout":       # torch elastic's name: how long an
+                    over["KFAMD_RDZV_TIMEOUT"] = str(kv.get("value"))   # agent waits for a round
             env = [e for e in env if e["name"] not in over] + [{"name": k, "value": v} for k, v in over.items()]
         return env
 

@@ -12,9 +12,21 @@
 //    round, so all nodes restart their workers together.
 //    Elastic (--nnodes MIN:MAX, PyTorchJob elasticPolicy): a round closes when MAX agents
 //    have joined, or when at least MIN have and no new one has joined for --rdzv-last-call
-//    seconds.  Rank offsets follow node-rank order among the members, so after a node is
-//    lost the survivors' restart re-forms the group at the smaller world size; a
-//    replacement agent joins at the next round.
+//    seconds -- and never without node 0: its local rank 0 is global rank 0, which hosts the
+//    TCPStore at MASTER_ADDR:MASTER_PORT, so a round without it would be a second world
+//    pointed at the running one's store.  Rank offsets follow node-rank order among the
+//    members, so after a node is lost the survivors' restart re-forms the group at the
+//    smaller world size.
+//    Membership changes (torchrun's "nodes waiting" rule): while its workers run, every agent
+//    of a multi-node job polls the server about once a second; as soon as any agent has
+//    joined the NEXT round (a replacement pod, a late node, or a member whose workers failed)
+//    the running agents stop their workers and re-join, without using up a --max-restarts
+//    attempt.  A replacement node is thereby admitted at once instead of after the running
+//    group's collectives time out.
+//    Node 0 hosts the rendezvous server: if its pod is lost the survivors' workers fail (rank
+//    0 and its store are gone) and their agents wait up to --rdzv-timeout for node 0 to come
+//    back; a replacement node-0 pod (restartPolicy OnFailure / ExitCode) starts a new server
+//    and the job continues, with restartPolicy Never the survivors exit 3 after the timeout.
 // 2. Spawn: P workers per node, each with RANK, LOCAL_RANK, WORLD_SIZE,
 //    LOCAL_WORLD_SIZE, GROUP_RANK, NODE_RANK, MASTER_ADDR, MASTER_PORT (and the OpenMPI
 //    OMPI_COMM_WORLD_{RANK,SIZE,LOCAL_RANK,LOCAL_SIZE} names), the ROCm IPC
@@ -120,6 +132,7 @@ Args parse(int argc, char** argv) {
     if (c != std::string::npos) a.rdzv_port = std::stoi(e.substr(c + 1));
   }
   if (const char* v = getenv("KFAMD_RDZV_LAST_CALL")) a.last_call = std::stod(v);
+  if (const char* v = getenv("KFAMD_RDZV_TIMEOUT")) a.rdzv_timeout = std::stod(v);
   int i = 1;
   for (; i < argc; ++i) {
     std::string s = argv[i];
@@ -240,17 +253,18 @@ struct RdzvServer {
     th.detach();
   }
   // a round is complete with all nnodes members, or (elastic) with >= min_nodes and no join
-  // for last_call seconds
-  bool complete(size_t n, double last_join) const {
-    if ((int)n >= nnodes) return true;
-    return (int)n >= min_nodes && min_nodes < nnodes && now_s() - last_join >= last_call;
+  // for last_call seconds; never without node 0 (global rank 0 and its store live there)
+  bool complete(const std::map<int, std::pair<int, int>>& m, double last_join) const {
+    if (!m.count(0)) return false;
+    if ((int)m.size() >= nnodes) return true;
+    return (int)m.size() >= min_nodes && min_nodes < nnodes && now_s() - last_join >= last_call;
   }
   void loop() {
     int round = 0;
     while (!g_stop) {
       std::map<int, std::pair<int, int>> members;  // node_rank -> (nproc, fd)
       double last_join = now_s();
-      while (!complete(members.size(), last_join) && !g_stop) {
+      while (!complete(members, last_join) && !g_stop) {
         pollfd pfd{fd, POLLIN, 0};
         if (::poll(&pfd, 1, 100) <= 0) continue;
         int c = ::accept(fd, nullptr, nullptr);
@@ -261,6 +275,13 @@ struct RdzvServer {
         std::string tag;
         int nr = -1, np = 0;
         is >> tag >> nr >> np;
+        if (tag == "POLL") {
+          // a running agent asks whether to restart: agents waiting for the next round, and the
+          // last round closed (an agent of an older round is stale and must re-join too)
+          send_line(c, "WAIT " + std::to_string(members.size()) + " " + std::to_string(round));
+          ::close(c);
+          continue;
+        }
         if (tag != "JOIN" || nr < 0 || nr >= nnodes || np < 1) { send_line(c, "ERR bad join"); ::close(c); continue; }
         if (members.count(nr)) ::close(members[nr].second);   // a restarted agent re-joins
         members[nr] = {np, c};
@@ -292,6 +313,24 @@ bool rendezvous(const Args& a, Assignment& out) {
   std::string tag;
   is >> tag >> out.rank_offset >> out.world >> out.round;
   return tag == "OK";
+}
+
+// Running agent: should this round's workers stop so the agent can re-join?  True when another
+// agent waits for the next round or a newer round has closed.  An unreachable server (node 0
+// lost) says nothing: the workers find out through their collectives.
+bool membership_changed(const Args& a, int my_round) {
+  int fd = connect_to(a.node_rank == 0 ? "127.0.0.1" : a.master_addr, a.rdzv_port, 1.0);
+  if (fd < 0) return false;
+  send_line(fd, "POLL " + std::to_string(a.node_rank) + " " + std::to_string(my_round));
+  std::string line;
+  const bool ok = recv_line(fd, line, 2.0);
+  ::close(fd);
+  if (!ok) return false;
+  std::istringstream is(line);
+  std::string tag;
+  int waiting = 0, closed = 0;
+  is >> tag >> waiting >> closed;
+  return tag == "WAIT" && (waiting > 0 || closed > my_round);
 }
 
 // ------------------------------------------------------------------ workers
@@ -380,7 +419,10 @@ int exit_code(int st) {
   return 1;
 }
 
-// run one round; returns 0 on success, else the failing exit code
+constexpr int kMembershipChange = -1;
+
+// run one round; returns 0 on success, kMembershipChange when the agent must re-join for a
+// membership change, else the failing exit code
 int run_round(const Args& a, const Assignment& as) {
   std::vector<Worker> ws(a.nproc);
   char tmpl[] = "/tmp/kfamd-hb-XXXXXX";
@@ -395,8 +437,19 @@ int run_round(const Args& a, const Assignment& as) {
   logf("round %d: started %d workers (ranks %d..%d of %d)", as.round, a.nproc, as.rank_offset,
        as.rank_offset + a.nproc - 1, as.world);
   int rc = 0;
+  double next_poll = now_s() + 1.0;
   while (true) {
     if (g_stop) { kill_all(ws, a.grace); rc = 143; break; }
+    if (a.nnodes > 1 && now_s() >= next_poll) {
+      next_poll = now_s() + 1.0;
+      if (membership_changed(a, as.round)) {
+        logf("round %d: membership change (an agent is waiting for the next round): restarting workers",
+             as.round);
+        kill_all(ws, a.grace);
+        rc = kMembershipChange;
+        break;
+      }
+    }
     bool all_done = true, failed = false;
     for (auto& w : ws) {
       if (w.done) continue;
@@ -450,12 +503,14 @@ int main(int argc, char** argv) {
   RdzvServer server;
   if (a.node_rank == 0) server.start(a.rdzv_port, a.nnodes, a.min_nodes, a.last_call);
   int rc = 1;
-  for (int attempt = 0; attempt <= a.max_restarts; ++attempt) {
+  for (int attempt = 0; attempt <= a.max_restarts;) {
     Assignment as;
     if (!rendezvous(a, as)) { rc = 3; break; }
     rc = run_round(a, as);
     if (rc == 0 || g_stop) break;
+    if (rc == kMembershipChange) { rc = 1; continue; }   // not a failure: no restart used
     if (attempt < a.max_restarts) logf("restarting workers (%d of %d restarts used)", attempt + 1, a.max_restarts);
+    ++attempt;
   }
   logf("exit %d", rc);
   return rc;

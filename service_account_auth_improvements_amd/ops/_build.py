@@ -81,13 +81,48 @@ def _run(cmd):
     return p.stderr
 
 
-def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -> Path:
-    kernel, binding, link = _flags()
+def _toolchain_key() -> list[str]:
+    """Everything the compile and link flags are derived from, WITHOUT importing
+    ``torch.utils.cpp_extension`` (0.2-0.3 s per worker process): the flags come from torch's
+    install directory, version and C++ ABI, the ROCm root and this module's own constants, so
+    hashing those identifies them.  ``_flags()`` runs only when a rebuild is needed."""
+    import torch
+
+    return [ARCH, HIPCC, torch.__version__, os.path.dirname(torch.__file__),
+            str(int(torch._C._GLIBCXX_USE_CXX11_ABI)), os.environ.get("ROCM_HOME", "/opt/rocm"),
+            hashlib.sha256(Path(__file__).read_bytes()).hexdigest()[:16],
+            *(f"{k}:{v}" for k, v in sorted(FILE_FLAGS.items()))]
+
+
+def current_digest() -> str:
     hips, bind = _sources()
-    digest = _digest(hips + [bind], kernel + binding + link + [f"{k}:{v}" for k, v in sorted(FILE_FLAGS.items())])
+    return _digest(hips + [bind], _toolchain_key())
+
+
+def up_to_date() -> bool:
+    """True when the in-tree library was built from exactly these sources and toolchain."""
+    stamp = HERE / (LIB_NAME + ".stamp")
+    return LIB_PATH.exists() and stamp.exists() and stamp.read_text().strip() == current_digest()
+
+
+def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -> Path:
+    hips, bind = _sources()
+    digest = current_digest()
     stamp = HERE / (LIB_NAME + ".stamp")
     if not force and LIB_PATH.exists() and stamp.exists() and stamp.read_text().strip() == digest:
         return LIB_PATH
+    # several ranks of one node may find the library stale together: one builds, the others
+    # wait on the lock and then see the fresh stamp
+    import fcntl
+    with open(HERE / (LIB_NAME + ".lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        if not force and LIB_PATH.exists() and stamp.exists() and stamp.read_text().strip() == digest:
+            return LIB_PATH
+        return _build_locked(hips, bind, digest, stamp, jobs, verbose)
+
+
+def _build_locked(hips, bind, digest, stamp, jobs, verbose) -> Path:
+    kernel, binding, link = _flags()
     BUILD.mkdir(exist_ok=True)
     jobs = jobs or min(8, os.cpu_count() or 4)
     cmds, objs = [], []

@@ -46,7 +46,7 @@ typedef __attribute__((ext_vector_type(4))) float f4;
 
 namespace fa {
 constexpr int D = 128;
-constexpr int BQ = 128;           // query rows per forward / dQ workgroup (4 waves x 32)
+constexpr int BQ = 128;           // sequence-length granule the launchers require (S % BQ == 0)
 constexpr int BK = 64;            // keys per tile (forward / dQ)
 constexpr int TILE = BK * D * 2;  // 16 KB
 constexpr int BKV = 128;          // keys per dK/dV workgroup (4 waves x 32)

@@ -13,8 +13,8 @@
 //    are shared by the R rows of the wave (read once per chunk from L1/L2, or from LDS when
 //    the norm prologue staged them).  At M = 8 the MFMA skinny kernel wins again (gate/up
 //    52 vs 56 us, wd 30 vs 38 us: X re-reads and VALU work grow with M), hence M <= 4.
-//  * Tuning knobs GV_U_CFG / GV_R_CFG (chunks in flight, rows per wave): a sweep of
-//    R in {1, 2, 4, 8} x U in {2, 4, 8} (tools/kbench/gemv_bench.hip) kept R = 4, U = 4.
+//  * Chunks in flight GV_U and rows per wave GV_R: a round-4 sweep of R in {1, 2, 4, 8} x
+//    U in {2, 4, 8} (tools/kbench/gemv_bench.hip, then -D knobs) kept R = 4, U = 4.
 //  * SWIGLU: the wave's R gate rows n.. and the matching up rows n + up_off.. are streamed
 //    together and the wave writes silu(gate) * up.
 //  * NORM prologue (decode layer norms fused in, as in skinny_gemm.hip): each workgroup
@@ -44,13 +44,8 @@ using namespace kf;
 namespace {
 
 constexpr int GV_WAVES = 4;       // 256-thread workgroups
-#ifndef GV_U_CFG
-#define GV_U_CFG 4
-#endif
-#ifndef GV_R_CFG
-#define GV_R_CFG 4
-#endif
-constexpr int GV_U = GV_U_CFG;    // chunks per row in flight per lane
+constexpr int GV_U = 4;           // chunks per row in flight per lane
+constexpr int GV_R = 4;           // rows per wave
 typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
 // acc + a.lo * b.lo + a.hi * b.hi for packed bf16 pairs (v_dot2c_f32_bf16)
 __device__ __forceinline__ float dot2_bf16(uint32_t a, uint32_t b, float acc) {
@@ -338,7 +333,7 @@ bool use_ksplit(int blocks_unsplit, int M, int K, bool norm) {
 template <int M, bool SWIGLU, bool NORM>
 int gv_launch(const bf16_t* x, long ldx, const bf16_t* w, int N, int K, bf16_t* y, long ldy, int up_off,
               GvNorm na, hipStream_t st) {
-  constexpr int R = SWIGLU ? (GV_R_CFG > 1 ? GV_R_CFG / 2 : 1) : GV_R_CFG;
+  constexpr int R = SWIGLU ? GV_R / 2 : GV_R;
   const int blocks = (N + R * GV_WAVES - 1) / (R * GV_WAVES);
   const size_t dyn = NORM ? (size_t)M * K * 2 : 0;
   const int jw = ((K / 8 + 63) / 64 + GV_WAVES - 1) / GV_WAVES;   // K-split: chunk slots per wave

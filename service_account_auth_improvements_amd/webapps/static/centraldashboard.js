@@ -279,7 +279,7 @@
       }
     }
     root.addEventListener("message", function (ev) {          // library.js protocol, own origin only
-      if (ev.origin && ev.origin !== origin()) return;
+      if (ev.origin !== origin()) return;                    // an empty origin is not ours either
       if (ev.data && ev.data.type === "iframe-connected") post();
     });
     sel.addEventListener("change", function () {

@@ -123,7 +123,7 @@
       }
       ns.listeners.push(post);
       root.addEventListener("message", function (ev) {
-        if (ev.origin && ev.origin !== ownOrigin()) return;
+        if (ev.origin !== ownOrigin()) return;               // an empty origin is not ours either
         if (ev.data && ev.data.type === "iframe-connected") post();
       });
 

@@ -222,7 +222,9 @@
       if (opts.all) sel.append(el("option", { value: ALL_NS, "data-cy": "all-namespaces" }, "All namespaces"));
       if (qs && (nss.indexOf(qs) >= 0 || (opts.all && qs === ALL_NS))) sel.value = qs;
       sel.addEventListener("change", function () { sessionStorage.setItem("kf-ns", sel.value); onChange(sel.value); });
-      window.addEventListener("message", function (ev) {        // central dashboard iframe protocol
+      window.addEventListener("message", function (ev) {        // central dashboard iframe protocol:
+        // only the embedding dashboard (our parent frame, our own origin) may switch the namespace
+        if (ev.source !== window.parent || ev.origin !== (location.origin || new URL(location.href).origin)) return;
         if (ev.data && ev.data.type === "namespace-selected") { sel.value = ev.data.value; onChange(sel.value); }
       });
       // the dashboard and the apps share one origin (behind the gateway): never post elsewhere

@@ -56,6 +56,8 @@ Promise.resolve()
                       stored: env.localStorage["selectedNamespace/.alice@example.com"] };
       var got = [];
       frame.contentWindow = { postMessage: function (m) { got.push(m); }, location: {} };
+      env.message({ type: "iframe-connected" }, "https://evil.example");   // ignored: foreign origin
+      env.message({ type: "iframe-connected" }, "");                       // ignored: no origin
       env.message({ type: "iframe-connected" });
       out.connected = got.slice();
       // the namespace selector: new ?ns, the iframe is told

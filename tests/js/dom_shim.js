@@ -266,7 +266,12 @@ function makeEnv(opts) {
   return { ctx: ctx, document: document, window: window, app: app, requests: requests, timers: timers, posted: posted,
            localStorage: lstore,
            winListeners: winListeners,
-           message: function (data) { (winListeners.message || []).forEach(function (f) { f({ data: data }); }); } };
+           // a postMessage arriving here: from this origin and the parent frame unless a test says otherwise
+           message: function (data, origin, source) {
+             var ev = { data: data, origin: origin === undefined ? new URL(loc.href).origin : origin,
+                        source: source === undefined ? window.parent : source };
+             (winListeners.message || []).forEach(function (f) { f(ev); });
+           } };
 }
 
 function flush(n) {

@@ -86,6 +86,14 @@ Promise.resolve()
         out.jwaDelete = { dialogTitle: title, afterCancel: afterCancel, dialogOpen: !!env.q('[role="dialog"]'),
                           deletes: env.requests.filter(function (r) { return r.method === "DELETE"; }).map(function (r) { return r.path; }) };
       });
+    }).then(function () {
+      // the dashboard's iframe protocol: only the parent frame, on this origin, switches the namespace
+      env.message({ type: "namespace-selected", value: "team-b" }, "https://evil.example");
+      env.message({ type: "namespace-selected", value: "team-b" }, "");
+      env.message({ type: "namespace-selected", value: "team-b" }, undefined, { postMessage: function () {} });
+      var ignored = env.q("select#ns").value;
+      env.message({ type: "namespace-selected", value: "team-b" });
+      return shim.flush().then(function () { out.jwaIframeNs = { ignored: ignored, accepted: env.q("select#ns").value }; });
     });
   })
   // ---------------------------------------------------------------- JWA form (form-page.cy.ts)

@@ -153,6 +153,13 @@ def test_jwa_all_namespaces_and_sorting(pages):
     assert o["namesDesc"] == sorted(o["names"], reverse=True)
 
 
+def test_app_takes_namespace_only_from_its_parent_frame_origin(pages):
+    """kf-common.js iframe protocol: a namespace-selected message from another origin, with an
+    empty origin, or from a window that is not the embedding dashboard is ignored."""
+    o = pages["jwaIframeNs"]
+    assert o["ignored"] == "kubeflow-user" and o["accepted"] == "team-b"
+
+
 def test_delete_goes_through_the_confirm_dialog(pages):
     d = pages["jwaDelete"]
     assert d["dialogTitle"] == "Delete Notebook zeta-trainer?" and d["afterCancel"] == 0

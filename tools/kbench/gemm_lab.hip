@@ -9,7 +9,7 @@
 // stages (no copies); a 4-deep ring keeps the buffer index and the register parity aligned over
 // a 4-stage unroll.  Past the last stage the "next stage" reads and DMA are issued anyway from
 // valid addresses (results unused) so every wait count stays a compile-time constant.
-#include "../../service_account_auth_improvements_amd/ops/csrc/gemm.hip"
+#include "gemm_prod_lab.hip"   // the production kernel with its anatomy / tuning knobs
 
 namespace g4 {
 template <int I, int N, typename F>

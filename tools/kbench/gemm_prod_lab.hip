@@ -1,3 +1,7 @@
+// LAB COPY of ops/csrc/gemm.hip with the measured tuning knobs (KF_GEMM_NBUF, KF_GEMM_GROUP_M,
+// KF_GEMM_DMA_STAGGER) and the anatomy switches (KF_ABL_*: numerics deliberately broken) that the
+// shipped source no longer carries.  Defaults reproduce the shipped kernel.
+//
 // Weight-gradient GEMM for gfx950: C[M,N] (+)= A^T . B with A = [K, M] and B = [K, N], both
 // row-major with the REDUCTION index K on the rows (dW = dY^T . X, K = tokens).
 //
@@ -40,7 +44,7 @@
 //    loads + ds_write_b128 one stage ahead) measured 1220 TF, i.e. worse; a fifth ring buffer
 //    (one more stage of DMA lookahead) +4.6 %; staggering the two halves' DMA issue +1 % alone
 //    and -2 % on top of the fifth buffer (profiles/gemm_dw_r3.md).
-#include "common.h"
+#include "common.h"   // (tools/kbench/build.sh puts ops/csrc on the include path)
 
 using namespace kf;
 
@@ -48,16 +52,26 @@ typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 #define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
 
 namespace gm {
-// K rows are staged BK at a time into an NBUF-deep LDS ring: 5 = the full 160 KB with the DMA
-// one stage further ahead than 4 (128 KB): 1,316-1,319 vs 1,256-1,262 TF over the step's dW
-// shapes at K = 32768 on one box, bit-identical output (profiles/gemm_dw_r3.md).  The knobs
-// and anatomy switches of those measurements live in tools/kbench/gemm_prod_lab.hip.
-constexpr int BM = 256, BN = 256, BK = 32, NBUF = 5;
+// K rows are staged BK at a time into an NBUF-deep LDS ring (KF_GEMM_NBUF: 4 = 128 KB, 5 = the
+// full 160 KB with the DMA one stage further ahead: 1,316-1,319 vs 1,256-1,262 TF over the
+// step's dW shapes at K = 32768 on one box, bit-identical output; profiles/gemm_dw_r3.md)
+#ifndef KF_GEMM_NBUF
+#define KF_GEMM_NBUF 5
+#endif
+constexpr int BM = 256, BN = 256, BK = 32, NBUF = KF_GEMM_NBUF;
+static_assert(NBUF == 4 || NBUF == 5, "ring depth");
 constexpr int IMG = BK * 256;               // one [32][128] bf16 image: 8 KB
 constexpr int SMEM = 4 * NBUF * IMG;        // images laid out [image][buffer]: 128 / 160 KB
 // M-tiles per raster group: 4 measured 1.0-1.3 % faster than 8 over the step's dW shapes on
-// two boxes (16 / 32: -3 % / -6 %)
-constexpr int GROUP_M = 4;
+// two boxes (16 / 32: -3 % / -6 %; tools/gpu_r2_gemm.sh); -DKF_GEMM_GROUP_M overrides
+#ifndef KF_GEMM_GROUP_M
+#define KF_GEMM_GROUP_M 4
+#endif
+constexpr int GROUP_M = KF_GEMM_GROUP_M;
+// 1 = waves 4-7 issue their stage's DMA pieces four MFMA groups after waves 0-3 (see kernel)
+#ifndef KF_GEMM_DMA_STAGGER
+#define KF_GEMM_DMA_STAGGER 0
+#endif
 
 __device__ __forceinline__ int blk_x(int row) { return (row & 3) | ((row >> 1) & 4); }
 
@@ -208,6 +222,9 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_kernel(TnGroup grp, int K) {
   u32 dmo[4];
   dma_offsets(lda, ldb, wave, lane, dmo);
   const u32 lds_w = __builtin_amdgcn_readfirstlane(lds_addr(smem) + 1024 * wave);
+  // DMA issue point (KF_GEMM_DMA_STAGGER): waves 4-7 issue four MFMA groups after waves 0-3,
+  // so the two waves sharing a SIMD do not stall on DMA issue at the same time
+  const bool late = KF_GEMM_DMA_STAGGER && __builtin_amdgcn_readfirstlane(wave) >= 4;
   // prologue: stages 0..NBUF-2 in flight, publish stage 0, first operand reads
 #pragma unroll
   for (int s = 0; s < NBUF - 1; ++s)
@@ -238,18 +255,37 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_kernel(TnGroup grp, int K) {
       if constexpr (t == 3) {
         // publish stage s+1 (its DMA went out NBUF-2 stages ago): wait until only the pieces
         // of the stages after it that exist are outstanding
-        if (s + 3 < nk) vm_wait<8>(); else if (s + 2 < nk) vm_wait<4>(); else vm_wait<0>();
+        // (KF_ABL_* : anatomy builds for tools/kbench only -- numerics deliberately broken)
+#ifndef KF_ABL_NOVMW
+        if constexpr (NBUF == 5) {
+          if (s + 3 < nk) vm_wait<8>(); else if (s + 2 < nk) vm_wait<4>(); else vm_wait<0>();
+        } else {
+          if (s + 2 < nk) vm_wait<4>(); else vm_wait<0>();
+        }
+#endif
+#ifndef KF_ABL_NOBAR
         barrier();
-        // refill the buffer every wave has finished with (stage s-1's) with stage s+NBUF-1
-        if (s + NBUF - 1 < nk) {
+#endif
+      }
+      // refill the buffer every wave has finished with (stage s-1's) with stage s+NBUF-1
+      if constexpr (t == 3 || t == 7) {
+        if ((t == 3) != late && s + NBUF - 1 < nk) {
+#ifndef KF_ABL_NODMA
+#ifdef KF_ABL_DMASAME
+          stage_dma(Ap, Bp, dmo, lds_w + OF);   // always the (L2-resident) first panel rows
+#else
           stage_dma(dA, dB, dmo, lds_w + OF);
+#endif
+#endif
           dA += astep;
           dB += bstep;
         }
       }
+#ifndef KF_ABL_NOREAD
       if constexpr (t >= 4) nb[t - 4] = tr_frag<ON>(bad[t - 4]);
       if constexpr (t < 4) a[t + 4] = tr_frag<OC>(aad[t + 4]);
       else a[t - 4] = tr_frag<ON>(aad[t - 4]);
+#endif
     };
     group(std::integral_constant<int, 0>());
     group(std::integral_constant<int, 1>());
@@ -268,13 +304,15 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_kernel(TnGroup grp, int K) {
     stage(std::integral_constant<int, 1>(), s + 1);
     stage(std::integral_constant<int, 2>(), s + 2);
     stage(std::integral_constant<int, 3>(), s + 3);
-    stage(std::integral_constant<int, 4>(), s + 4);
+    if constexpr (NBUF == 5) stage(std::integral_constant<int, 4 % NBUF>(), s + 4);
   }
-  const int rem = nk - s;
-  if (rem >= 1) stage(std::integral_constant<int, 0>(), s);
-  if (rem >= 2) stage(std::integral_constant<int, 1>(), s + 1);
-  if (rem >= 3) stage(std::integral_constant<int, 2>(), s + 2);
-  if (rem >= 4) stage(std::integral_constant<int, 3>(), s + 3);
+  if constexpr (NBUF == 5) {
+    const int rem = nk - s;
+    if (rem >= 1) stage(std::integral_constant<int, 0>(), s);
+    if (rem >= 2) stage(std::integral_constant<int, 1>(), s + 1);
+    if (rem >= 3) stage(std::integral_constant<int, 2>(), s + 2);
+    if (rem >= 4) stage(std::integral_constant<int, 3>(), s + 3);
+  }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 
   // acc[u][t] = C^T fragment: lane l, reg r -> n = 16u + 4(l>>4) + r, m = 16t + (l&15)
@@ -300,7 +338,7 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_kernel(TnGroup grp, int K) {
 
 static bool tn_shape_ok(const void* A, long lda, const void* B, long ldb, const void* C, long ldc, int M, int N,
                         int K) {
-  if (M % BM || N % BN || K % BK || K < BK || lda % 8 || ldb % 8 || ldc % 4) return false;
+  if (M % BM || N % BN || K % (NBUF == 4 ? BK * NBUF : BK) || K < BK || lda % 8 || ldb % 8 || ldc % 4) return false;
   return !(((uintptr_t)A | (uintptr_t)B) & 15) && !((uintptr_t)C & 7);
 }
 
