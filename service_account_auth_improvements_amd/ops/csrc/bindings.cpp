@@ -68,7 +68,7 @@ int kf_car_alloc(long, void**, void*);
 int kf_car_open(const void*, void**);
 int kf_car_close(void*);
 int kf_car_free(void*);
-int kf_car_allreduce(void* const*, int, int, const void*, void*, long, long, int, hipStream_t);
+int kf_car_allreduce(void* const*, int, int, const void*, void*, long, long, int, double, hipStream_t);
 int kf_car_error(void*, hipStream_t);
 long kf_ts_header_bytes();
 long kf_decode_step_ws_bytes();
@@ -77,8 +77,9 @@ int kf_decode_step(const void*, int, int, int, int, int, int, int, int, const vo
                    const float*, const float*, const long*, const int*, const int*, int, float, float, void*, void*,
                    hipStream_t);
 int kf_ts_alloc(long, int, void**, void*);
-int kf_ts_run(int, void* const*, int, int, const void*, void*, long, long, int, hipStream_t);
+int kf_ts_run(int, void* const*, int, int, const void*, void*, long, long, int, double, hipStream_t);
 int kf_ts_error(void*, hipStream_t);
+int kf_ts_error_async(void*, int*, hipStream_t);
 }
 
 namespace {
@@ -641,7 +642,8 @@ void car_close(int64_t p) { kf_car_close(reinterpret_cast<void*>(p)); }
 void car_free(int64_t p) { kf_car_free(reinterpret_cast<void*>(p)); }
 
 // in place, like dist.all_reduce (the engine's TP code relies on all-reduce being in place)
-void car_allreduce_(const std::vector<int64_t>& ptrs, int64_t rank, at::Tensor& x, int64_t slot_bytes, int64_t blocks) {
+void car_allreduce_(const std::vector<int64_t>& ptrs, int64_t rank, at::Tensor& x, int64_t slot_bytes, int64_t blocks,
+                    double timeout_s) {
   check_bf16_cuda(x, "x");
   TORCH_CHECK(x.is_contiguous() && x.numel() % 8 == 0 && 2 * x.numel() <= slot_bytes,
               "car_allreduce: contiguous bf16 with numel % 8 == 0 that fits the slot");
@@ -649,7 +651,7 @@ void car_allreduce_(const std::vector<int64_t>& ptrs, int64_t rank, at::Tensor& 
   std::vector<void*> pv;
   for (auto v : ptrs) pv.push_back(reinterpret_cast<void*>(v));
   check_rc(kf_car_allreduce(pv.data(), (int)pv.size(), (int)rank, x.data_ptr(), x.data_ptr(), x.numel(), slot_bytes,
-                            (int)blocks, cur_stream()),
+                            (int)blocks, timeout_s, cur_stream()),
            "car_allreduce");
 }
 
@@ -667,7 +669,7 @@ std::tuple<int64_t, at::Tensor> ts_alloc(int64_t slot_bytes, int64_t world) {
 // mode 0: all-reduce x in place (out is x); 1: reduce-scatter x[n] -> out[n / world];
 // 2: all-gather x[n / world] -> out[n].  Runs on the current stream.
 void ts_run(int64_t mode, const std::vector<int64_t>& ptrs, int64_t rank, const at::Tensor& x, at::Tensor& out,
-            int64_t slot_bytes, int64_t blocks) {
+            int64_t slot_bytes, int64_t blocks, double timeout_s) {
   check_bf16_cuda(x, "x");
   check_bf16_cuda(out, "out");
   const long w = (long)ptrs.size();
@@ -681,11 +683,17 @@ void ts_run(int64_t mode, const std::vector<int64_t>& ptrs, int64_t rank, const 
   std::vector<void*> pv;
   for (auto v : ptrs) pv.push_back(reinterpret_cast<void*>(v));
   check_rc(kf_ts_run((int)mode, pv.data(), (int)w, (int)rank, x.data_ptr(), out.data_ptr(), n, slot_bytes,
-                     (int)blocks, cur_stream()),
+                     (int)blocks, timeout_s, cur_stream()),
            "ts_run");
 }
 
 int64_t ts_error(int64_t own) { return kf_ts_error(reinterpret_cast<void*>(own), cur_stream()); }
+// queue a copy of the error word into `host` (a pinned int32 CPU tensor) on the current stream
+void ts_error_async(int64_t own, at::Tensor& host) {
+  TORCH_CHECK(!host.is_cuda() && host.scalar_type() == at::kInt && host.numel() >= 1 && host.is_pinned(),
+              "ts_error_async: pinned int32 host tensor");
+  check_rc(kf_ts_error_async(reinterpret_cast<void*>(own), host.data_ptr<int>(), cur_stream()), "ts_error_async");
+}
 
 // Weight-gradient GEMM: C[M, N] (+)= a^T . b with a = [K, M], b = [K, N] (row stride may
 // exceed the width: views into fused activations); C may be a view into the flat grad buffer.
@@ -806,11 +814,14 @@ TORCH_LIBRARY(kfamd, m) {
   m.def("car_open", &car_open);
   m.def("car_close", &car_close);
   m.def("car_free", &car_free);
-  m.def("car_allreduce_(int[] ptrs, int rank, Tensor(a!) x, int slot_bytes, int blocks) -> ()", &car_allreduce_);
+  m.def("car_allreduce_(int[] ptrs, int rank, Tensor(a!) x, int slot_bytes, int blocks, float timeout_s) -> ()",
+        &car_allreduce_);
   m.def("car_error", &car_error);
   m.def("ts_alloc", &ts_alloc);
-  m.def("ts_run(int mode, int[] ptrs, int rank, Tensor x, Tensor(a!) out, int slot_bytes, int blocks) -> ()", &ts_run);
+  m.def("ts_run(int mode, int[] ptrs, int rank, Tensor x, Tensor(a!) out, int slot_bytes, int blocks, float timeout_s) -> ()",
+        &ts_run);
   m.def("ts_error", &ts_error);
+  m.def("ts_error_async(int own, Tensor(a!) host) -> ()", &ts_error_async);
   m.def("gemm_tn_ok", &gemm_tn_ok);
   m.def("gemm_tn_(Tensor a, Tensor b, Tensor(a!) c, bool accumulate) -> ()", &gemm_tn_);
   m.def("gemm_tn2_(Tensor a0, Tensor b0, Tensor(a!) c0, Tensor a1, Tensor b1, Tensor(b!) c1, bool accumulate) -> ()",

@@ -15,8 +15,10 @@
 //   e = ++epoch[b] (block-private counter, so HIP-graph replays need no host epoch);
 //   slot = e & 1; copy my chunk of x into data[slot];
 //   release (system scope) -> write e into flags[slot][b][my_rank] of EVERY peer;
-//   spin until flags[slot][b][p] == e for all p in my buffer (bounded: on timeout set err
-//   and give up instead of hanging the GPU) -> acquire;
+//   spin until flags[slot][b][p] == e for all p in my buffer -> acquire.  The wait is bounded
+//   in WALL TIME (s_memrealtime, 100 MHz), by a budget the caller passes per call (the decode
+//   engine a few seconds, a training communicator its process-group timeout): a late peer is
+//   waited for, a dead one sets err and the kernel gives up instead of hanging the GPU;
 //   out[chunk] = sum_p peer_p.data[slot][chunk], accumulated in fp32 in rank order, so every
 //   rank produces bit-identical results.  out may be x (in place, like dist.all_reduce): a
 //   block reads its chunk of x before the flag exchange and writes it after.
@@ -36,7 +38,21 @@ constexpr long FLAG_BYTES = 2L * MAXB * MAXW * 4;
 constexpr long EPOCH_OFF = FLAG_BYTES;
 constexpr long ERR_OFF = EPOCH_OFF + MAXB * 4;
 constexpr long DATA_OFF = 8192;  // header padded to 8 KB
-constexpr unsigned SPIN_LIMIT = 1u << 24;   // x s_sleep(2) ~ seconds: a dead peer errors out, never hangs
+constexpr double RT_HZ = 1e8;    // s_memrealtime ticks per second
+
+// Wait until *f == e; false once `budget` ticks of the constant 100 MHz realtime counter
+// have passed (a clock that does not move with the shader clock, so the budget is seconds).
+__device__ __forceinline__ bool wait_flag(int* f, int e, unsigned long long budget) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != e) {
+    if (__builtin_amdgcn_s_memrealtime() - t0 > budget) return false;
+    __builtin_amdgcn_s_sleep(2);
+  }
+  return true;
+}
+__host__ inline unsigned long long budget_ticks(double timeout_s) {
+  return (unsigned long long)(std::max(timeout_s, 1e-3) * RT_HZ);
+}
 
 struct Peers {
   char* p[MAXW];
@@ -48,7 +64,7 @@ __device__ __forceinline__ int* flags(char* base, int slot, int b, int r) {
 
 template <int W>
 __global__ __launch_bounds__(NT) void one_shot_ar_kernel(Peers peers, int rank, const bf16_t* x, bf16_t* out,
-                                                         long n, long slot_bytes) {
+                                                         long n, long slot_bytes, unsigned long long budget) {
   __shared__ int e_sh;
   const int b = blockIdx.x, tid = threadIdx.x;
   char* mine = peers.p[rank];
@@ -66,15 +82,8 @@ __global__ __launch_bounds__(NT) void one_shot_ar_kernel(Peers peers, int rank, 
   if (tid < W) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // system scope: data before flag, for every GPU
     __hip_atomic_store(flags(peers.p[tid], slot, b, rank), e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    int* f = flags(mine, slot, b, tid);
-    unsigned spins = 0;
-    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != e) {
-      if (++spins > SPIN_LIMIT) {
-        __hip_atomic_store(reinterpret_cast<int*>(mine + ERR_OFF), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
+    if (!wait_flag(flags(mine, slot, b, tid), e, budget))
+      __hip_atomic_store(reinterpret_cast<int*>(mine + ERR_OFF), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   }
   __syncthreads();
@@ -111,10 +120,10 @@ __global__ __launch_bounds__(NT) void one_shot_ar_kernel(Peers peers, int rank, 
 // life (parallel/custom_ar.py TwoShot) and issues its calls on ONE stream: then every in-flight
 // block of every rank is in call k or k+1, and parity slots never collide.
 namespace ts {
-constexpr int MAXW = 8, MAXB = 64, NT = 512;
+constexpr int MAXW = 8, MAXB = 128, NT = 512;
 constexpr long FLAGS1 = 0, FLAGS2 = 2L * MAXB * MAXW * 4, EPOCH_OFF = 2 * FLAGS2, ERR_OFF = EPOCH_OFF + MAXB * 4;
-constexpr long DATA_OFF = 16384;
-constexpr unsigned SPIN_LIMIT = 1u << 24;
+constexpr long DATA_OFF = 32768;
+static_assert(ERR_OFF + 4 <= DATA_OFF, "two-shot header");
 enum Mode { AR = 0, RS = 1, AG = 2 };
 
 __device__ __forceinline__ int* flag(char* base, long off, int slot, int b, int r) {
@@ -122,21 +131,15 @@ __device__ __forceinline__ int* flag(char* base, long off, int slot, int b, int 
 }
 // lanes 0..W-1: post e to every peer's flag (release first), then wait for every peer's flag
 template <int W>
-__device__ __forceinline__ void exchange(const car::Peers& P, int rank, long off, int slot, int b, int e, char* mine) {
+__device__ __forceinline__ void exchange(const car::Peers& P, int rank, long off, int slot, int b, int e, char* mine,
+                                         unsigned long long budget) {
   const int tid = threadIdx.x;
   __syncthreads();
   if (tid < W) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     __hip_atomic_store(flag(P.p[tid], off, slot, b, rank), e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    int* f = flag(mine, off, slot, b, tid);
-    unsigned spins = 0;
-    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != e) {
-      if (++spins > SPIN_LIMIT) {
-        __hip_atomic_store(reinterpret_cast<int*>(mine + ERR_OFF), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
+    if (!car::wait_flag(flag(mine, off, slot, b, tid), e, budget))
+      __hip_atomic_store(reinterpret_cast<int*>(mine + ERR_OFF), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   }
   __syncthreads();
@@ -144,7 +147,7 @@ __device__ __forceinline__ void exchange(const car::Peers& P, int rank, long off
 
 template <int W, int MODE>
 __global__ __launch_bounds__(NT) void two_shot_kernel(car::Peers P, int rank, const bf16_t* x, bf16_t* out,
-                                                      long n, long slot_bytes) {
+                                                      long n, long slot_bytes, unsigned long long budget) {
   __shared__ int e_sh;
   const int b = blockIdx.x, tid = threadIdx.x;
   char* mine = P.p[rank];
@@ -166,7 +169,7 @@ __global__ __launch_bounds__(NT) void two_shot_kernel(car::Peers P, int rank, co
     for (int c = 0; c < W; ++c)
       for (long v = v0 + tid; v < v1; v += NT) mine_in[c * cv + v] = xin[c * cv + v];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    exchange<W>(P, rank, FLAGS1, slot, b, e, mine);
+    exchange<W>(P, rank, FLAGS1, slot, b, e, mine, budget);
     // phase 1: reduce my chunk over every peer's input (rank order)
     u32x4* red = red_of(rank);
     for (long v = v0 + tid; v < v1; v += NT) {
@@ -195,7 +198,7 @@ __global__ __launch_bounds__(NT) void two_shot_kernel(car::Peers P, int rank, co
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   if (MODE != RS) {
-    exchange<W>(P, rank, FLAGS2, slot, b, e, mine);
+    exchange<W>(P, rank, FLAGS2, slot, b, e, mine, budget);
     // phase 2: every peer's reduced chunk
     for (long v = v0 + tid; v < v1; v += NT) {
       u32x4 src[W];
@@ -208,17 +211,17 @@ __global__ __launch_bounds__(NT) void two_shot_kernel(car::Peers P, int rank, co
   } else {
     // RS posts phase 2 too (without reading anything): the slot-reuse argument needs every
     // call's phase-2 flags
-    exchange<W>(P, rank, FLAGS2, slot, b, e, mine);
+    exchange<W>(P, rank, FLAGS2, slot, b, e, mine, budget);
   }
   if (tid == 0) __hip_atomic_store(epoch, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <int W>
 void launch_two_shot(int mode, int blocks, hipStream_t st, const car::Peers& P, int rank, const bf16_t* x, bf16_t* o,
-                     long n, long slot_bytes) {
-  if (mode == AR) hipLaunchKernelGGL((two_shot_kernel<W, AR>), dim3(blocks), dim3(NT), 0, st, P, rank, x, o, n, slot_bytes);
-  else if (mode == RS) hipLaunchKernelGGL((two_shot_kernel<W, RS>), dim3(blocks), dim3(NT), 0, st, P, rank, x, o, n, slot_bytes);
-  else hipLaunchKernelGGL((two_shot_kernel<W, AG>), dim3(blocks), dim3(NT), 0, st, P, rank, x, o, n, slot_bytes);
+                     long n, long slot_bytes, unsigned long long bt) {
+  if (mode == AR) hipLaunchKernelGGL((two_shot_kernel<W, AR>), dim3(blocks), dim3(NT), 0, st, P, rank, x, o, n, slot_bytes, bt);
+  else if (mode == RS) hipLaunchKernelGGL((two_shot_kernel<W, RS>), dim3(blocks), dim3(NT), 0, st, P, rank, x, o, n, slot_bytes, bt);
+  else hipLaunchKernelGGL((two_shot_kernel<W, AG>), dim3(blocks), dim3(NT), 0, st, P, rank, x, o, n, slot_bytes, bt);
 }
 }  // namespace ts
 
@@ -250,9 +253,10 @@ int kf_car_close(void* ptr) { return hipIpcCloseMemHandle(ptr) == hipSuccess ? 0
 int kf_car_free(void* ptr) { return hipFree(ptr) == hipSuccess ? 0 : 1; }
 
 // ptrs: world device pointers (own buffer at index rank); x/out: n bf16 (n % 8 == 0,
-// 2 * n <= slot_bytes; out == x allowed).  Returns non-zero on a bad shape (nothing launched).
+// 2 * n <= slot_bytes; out == x allowed); timeout_s: how long a block waits for a peer before
+// it sets the error word.  Returns non-zero on a bad shape (nothing launched).
 int kf_car_allreduce(void* const* ptrs, int world, int rank, const void* x, void* out, long n, long slot_bytes,
-                     int blocks, hipStream_t st) {
+                     int blocks, double timeout_s, hipStream_t st) {
   if (world < 1 || world > MAXW || rank < 0 || rank >= world || n % 8 || 2 * n > slot_bytes) return 1;
   if (((uintptr_t)x | (uintptr_t)out) & 15) return 2;
   blocks = std::max(1, std::min(blocks, MAXB));
@@ -260,11 +264,12 @@ int kf_car_allreduce(void* const* ptrs, int world, int rank, const void* x, void
   for (int i = 0; i < world; ++i) P.p[i] = static_cast<char*>(ptrs[i]);
   auto X = static_cast<const bf16_t*>(x);
   auto O = static_cast<bf16_t*>(out);
+  const unsigned long long bt = budget_ticks(timeout_s);
   switch (world) {
-    case 1: hipLaunchKernelGGL(one_shot_ar_kernel<1>, dim3(blocks), dim3(NT), 0, st, P, rank, X, O, n, slot_bytes); break;
-    case 2: hipLaunchKernelGGL(one_shot_ar_kernel<2>, dim3(blocks), dim3(NT), 0, st, P, rank, X, O, n, slot_bytes); break;
-    case 4: hipLaunchKernelGGL(one_shot_ar_kernel<4>, dim3(blocks), dim3(NT), 0, st, P, rank, X, O, n, slot_bytes); break;
-    case 8: hipLaunchKernelGGL(one_shot_ar_kernel<8>, dim3(blocks), dim3(NT), 0, st, P, rank, X, O, n, slot_bytes); break;
+    case 1: hipLaunchKernelGGL(one_shot_ar_kernel<1>, dim3(blocks), dim3(NT), 0, st, P, rank, X, O, n, slot_bytes, bt); break;
+    case 2: hipLaunchKernelGGL(one_shot_ar_kernel<2>, dim3(blocks), dim3(NT), 0, st, P, rank, X, O, n, slot_bytes, bt); break;
+    case 4: hipLaunchKernelGGL(one_shot_ar_kernel<4>, dim3(blocks), dim3(NT), 0, st, P, rank, X, O, n, slot_bytes, bt); break;
+    case 8: hipLaunchKernelGGL(one_shot_ar_kernel<8>, dim3(blocks), dim3(NT), 0, st, P, rank, X, O, n, slot_bytes, bt); break;
     default: return 3;
   }
   KF_CHECK_LAUNCH();
@@ -289,7 +294,7 @@ int kf_ts_alloc(long slot_bytes, int world, void** ptr, void* handle) {
 // mode 0 all-reduce (x[n] -> out[n]), 1 reduce-scatter (x[n] -> out[n/world]), 2 all-gather
 // (x[n/world] -> out[n]); n is the FULL element count; n % (8 world) == 0, 2n <= slot_bytes.
 int kf_ts_run(int mode, void* const* ptrs, int world, int rank, const void* x, void* out, long n, long slot_bytes,
-              int blocks, hipStream_t st) {
+              int blocks, double timeout_s, hipStream_t st) {
   if (world < 1 || world > ts::MAXW || rank < 0 || rank >= world || mode < 0 || mode > 2) return 1;
   if (n % (8L * world) || 2 * n > slot_bytes || slot_bytes % (16L * world)) return 1;
   if (((uintptr_t)x | (uintptr_t)out) & 15) return 2;
@@ -299,15 +304,25 @@ int kf_ts_run(int mode, void* const* ptrs, int world, int rank, const void* x, v
   for (int i = 0; i < world; ++i) P.p[i] = static_cast<char*>(ptrs[i]);
   auto X = static_cast<const bf16_t*>(x);
   auto O = static_cast<bf16_t*>(out);
+  const unsigned long long bt = budget_ticks(timeout_s);
   switch (world) {
-    case 1: ts::launch_two_shot<1>(mode, blocks, st, P, rank, X, O, n, slot_bytes); break;
-    case 2: ts::launch_two_shot<2>(mode, blocks, st, P, rank, X, O, n, slot_bytes); break;
-    case 4: ts::launch_two_shot<4>(mode, blocks, st, P, rank, X, O, n, slot_bytes); break;
-    case 8: ts::launch_two_shot<8>(mode, blocks, st, P, rank, X, O, n, slot_bytes); break;
+    case 1: ts::launch_two_shot<1>(mode, blocks, st, P, rank, X, O, n, slot_bytes, bt); break;
+    case 2: ts::launch_two_shot<2>(mode, blocks, st, P, rank, X, O, n, slot_bytes, bt); break;
+    case 4: ts::launch_two_shot<4>(mode, blocks, st, P, rank, X, O, n, slot_bytes, bt); break;
+    case 8: ts::launch_two_shot<8>(mode, blocks, st, P, rank, X, O, n, slot_bytes, bt); break;
     default: return 4;
   }
   KF_CHECK_LAUNCH();
   return 0;
+}
+
+// Asynchronous read of the error word: queued on `st` (after the calls it must cover) into
+// pinned host memory; the caller looks at it once an event after this copy has completed, so
+// checking costs no host synchronisation.  The word is not cleared: once set, the
+// communicator is out of step for good.
+int kf_ts_error_async(void* own, int* host_pinned, hipStream_t st) {
+  char* p = static_cast<char*>(own) + ts::ERR_OFF;
+  return hipMemcpyAsync(host_pinned, p, 4, hipMemcpyDeviceToHost, st) == hipSuccess ? 0 : 1;
 }
 
 int kf_ts_error(void* own, hipStream_t st) {

@@ -29,13 +29,15 @@ from ..ops import _ext
 class OneShotAllReduce:
     """Collective constructor over ``group`` (all ranks on GPUs of this node)."""
 
-    def __init__(self, group=None, max_bytes: int = 4 << 20, blocks: int = 32):
+    def __init__(self, group=None, max_bytes: int = 4 << 20, blocks: int = 32, timeout_s: float = 10.0):
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         assert self.world in (1, 2, 4, 8), "one-shot all-reduce supports 1, 2, 4 or 8 ranks"
         self.max_bytes = int(max_bytes)
         self.blocks = int(blocks)
+        # wall-clock budget a kernel block waits for a peer before it sets the error word
+        self.timeout_s = float(timeout_s)
         k = _ext.ops()
         self._own, handle = k.car_alloc(self.max_bytes)
         handles: List[Optional[torch.Tensor]] = [None] * self.world
@@ -61,11 +63,11 @@ class OneShotAllReduce:
         if not self.supports(x):
             dist.all_reduce(x, group=self.group)
             return x
-        _ext.ops().car_allreduce_(self.ptrs, self.rank, x, self.max_bytes, self.blocks)
+        _ext.ops().car_allreduce_(self.ptrs, self.rank, x, self.max_bytes, self.blocks, self.timeout_s)
         return x
 
     def error(self) -> int:
-        """1 when a peer failed to arrive within the kernel's spin budget since the last check."""
+        """1 when a peer failed to arrive within ``timeout_s`` since the last check."""
         return int(_ext.ops().car_error(self._own))
 
     def check(self):
@@ -129,13 +131,24 @@ class TwoShot:
         tp_reduce_scatter_rows(x, st)          # now runs the two-shot kernel
     """
 
-    def __init__(self, group=None, max_bytes: int = 288 << 20, blocks: int = 64):
+    MAX_BLOCKS = 128
+
+    # workgroups per call: measured on one MI355X at 16/64/268 MB for 32/64/128 blocks
+    # (tools/bench_two_shot.py, profiles/two_shot_blocks_r5.md): 128 is fastest at every size
+    # and mode (RS 268 MB: 0.44 ms vs 0.70 at 64 and 1.21 at 32) -- each block keeps only a few
+    # uncached loads in flight, so the kernel needs the blocks to reach bandwidth
+    def __init__(self, group=None, max_bytes: int = 288 << 20, blocks: int = 128, timeout_s: float = 300.0):
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         assert self.world in (1, 2, 4, 8), "two-shot collectives support 1, 2, 4 or 8 ranks"
         self.max_bytes = int(max_bytes) // (16 * self.world) * (16 * self.world)
-        self.blocks = max(1, min(int(blocks), 64))
+        self.blocks = max(1, min(int(blocks), self.MAX_BLOCKS))
+        # wall-clock budget (s_memrealtime) a kernel block waits for a peer: a late peer -- one
+        # rank's first-step GEMM heuristics, a checkpoint write -- is waited for; only one that
+        # stays away this long sets the error word.  The trainer passes its process-group
+        # timeout, so the kernel gives up no sooner than RCCL would.
+        self.timeout_s = float(timeout_s)
         k = _ext.ops()
         self._own, handle = k.ts_alloc(self.max_bytes, self.world)
         handles: List[Optional[torch.Tensor]] = [None] * self.world
@@ -149,6 +162,10 @@ class TwoShot:
                 self._opened.append(p)
                 self.ptrs.append(p)
         self.stream = torch.cuda.Stream()
+        # asynchronous error-word reads: copied into pinned memory on the comm stream, looked
+        # at once the copy's event has completed (no host synchronisation per step)
+        self._err_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        self._err_event = None
         dist.barrier(group=group)
         self.failed = False
         self.calls = 0
@@ -162,7 +179,7 @@ class TwoShot:
         x = x.contiguous()
         self.stream.wait_stream(cur)
         with torch.cuda.stream(self.stream):
-            _ext.ops().ts_run(mode, self.ptrs, self.rank, x, out, self.max_bytes, self.blocks)
+            _ext.ops().ts_run(mode, self.ptrs, self.rank, x, out, self.max_bytes, self.blocks, self.timeout_s)
         # both stay allocated until the comm stream has used them
         x.record_stream(self.stream)
         out.record_stream(self.stream)
@@ -199,13 +216,44 @@ class TwoShot:
         w = self._run(2, x, out, async_op)
         return w if async_op else None
 
-    def check(self):
-        """Raise if a call since the last check timed out waiting for a peer (the
-        communicator is then out of step for good, as the one-shot one)."""
-        if self.failed or int(_ext.ops().ts_error(self._own)):
-            self.failed = True
-            raise RuntimeError("two-shot TP collective: a peer did not arrive within the spin budget; "
-                               "results since the last check are invalid (restart the job)")
+    def _raise(self):
+        self.failed = True
+        raise RuntimeError(f"two-shot TP collective: a peer did not arrive within {self.timeout_s:.0f} s; "
+                           "results since the error are invalid and the communicator is out of step "
+                           "(restart the job)")
+
+    def check(self, sync: bool = False):
+        """Raise if a call timed out waiting for a peer (the communicator is then out of step
+        for good, as the one-shot one).
+
+        Default (every training step): no host synchronisation.  The error word of the calls
+        issued so far is copied on the communicator's stream into pinned memory; the check
+        reads the PREVIOUS copy once its event has completed and queues the next one, so an
+        error surfaces a step or two late (the step that produced it already counted as
+        garbage either way).  ``sync=True`` (checkpoint, end of run) waits for every call
+        issued so far and reads the word now."""
+        if self.failed:
+            self._raise()
+        k = _ext.ops()
+        if sync:
+            self.stream.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(self.stream):
+                k.ts_error_async(self._own, self._err_host)
+            self.stream.synchronize()
+            self._err_event = None
+            if int(self._err_host[0]):
+                self._raise()
+            return
+        if self._err_event is not None:
+            if not self._err_event.query():
+                return                      # the previous read is still in flight: look next time
+            self._err_event = None
+            if int(self._err_host[0]):
+                self._raise()
+        with torch.cuda.stream(self.stream):
+            k.ts_error_async(self._own, self._err_host)
+            self._err_event = torch.cuda.Event()
+            self._err_event.record(self.stream)
 
     def close(self):
         k = _ext.ops()
@@ -226,4 +274,4 @@ def make_tp_comm(kind: str, st):
         raise ValueError(f"tp_comm must be 'rccl' or 'twoshot', not {kind!r}")
     if kind == "rccl" or st.tp == 1 or st.device.type != "cuda":
         return None
-    return TwoShot(st.tp_group)
+    return TwoShot(st.tp_group, timeout_s=float(getattr(st, "timeout_s", 300.0)))

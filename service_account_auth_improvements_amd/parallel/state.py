@@ -39,6 +39,8 @@ class ParallelState:
     # TP collective backend: None = torch.distributed (RCCL / gloo); a parallel.custom_ar.TwoShot
     # takes the TP reduce-scatter / all-gather / all-reduce it supports (runtime.trainer tp_comm)
     tp_comm: Optional[object] = None
+    # the process-group timeout: the budget the two-shot TP kernels wait for a late peer
+    timeout_s: float = 1800.0
 
     @property
     def is_first_stage(self):
@@ -126,7 +128,7 @@ def init_distributed(tp: int = 1, pp: int = 1, backend: Optional[str] = None,
     assert world % (tp * pp) == 0, f"world {world} not divisible by tp*pp={tp * pp}"
     dp = world // (tp * pp)
     st = ParallelState(world_size=world, rank=rank, local_rank=local, tp=tp, pp=pp, dp=dp,
-                       device=dev, backend=backend)
+                       device=dev, backend=backend, timeout_s=float(timeout_s))
     if world > 1:
         if not dist.is_initialized():
             kw = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))

@@ -96,6 +96,8 @@ def save_checkpoint(path: str, trainer, extra: Optional[dict] = None, data=None)
     st = trainer.st
     if hasattr(trainer, "sync_params"):
         trainer.sync_params()        # land in-flight ZeRO-1 parameter gathers first
+    if getattr(st, "tp_comm", None) is not None:
+        st.tp_comm.check(sync=True)  # never persist state a timed-out TP collective produced
     os.makedirs(path, exist_ok=True)
     opt = trainer.opt
     writes_params = st.dp_rank == 0

@@ -1,13 +1,19 @@
-"""One-shot IPC all-reduce (ops/csrc/custom_ar.hip) vs a float64 sum, with two ranks that
-share the single GPU of the test box (gloo carries only the IPC-handle exchange; the data
-moves through the peer-mapped uncached buffers).  On an 8-GPU node the same code runs one
-rank per GPU over xGMI."""
+"""One-shot IPC all-reduce (ops/csrc/custom_ar.hip) with 2, 4 and 8 ranks that share the single
+GPU of the test box (gloo carries only the IPC-handle exchange; the data moves through the
+peer-mapped uncached buffers).  On an 8-GPU node the same code runs one rank per GPU over xGMI;
+the W = 4 / 8 instantiations (TP = 4 / 8 decode) run here first.  Expected: the kernel's defined
+result, the fp32 sum of the bf16 inputs in rank order rounded once to bf16 -- bitwise."""
 import pytest
 import torch
 
 from dist_util import run_ranks
 
 pytestmark = pytest.mark.gpu
+
+
+def _inp(n, it, r):
+    g = torch.Generator(device="cpu").manual_seed(1000 * n + 10 * it + r)
+    return torch.randn(n, generator=g).to(torch.bfloat16)
 
 
 def _body(rank, world, n_list, iters):
@@ -17,19 +23,17 @@ def _body(rank, world, n_list, iters):
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(0)
-    car = OneShotAllReduce(max_bytes=1 << 20, blocks=16)
-    errs = []
+    car = OneShotAllReduce(max_bytes=1 << 20, blocks=16, timeout_s=60.0)
+    bad = []
     for n in n_list:
         for it in range(iters):
-            g = torch.Generator(device="cpu").manual_seed(1000 * n + 10 * it + rank)
-            x = torch.randn(n, generator=g).to("cuda:0", torch.bfloat16)
-            y = car(x)
+            y = car(_inp(n, it, rank).to("cuda:0"))
             torch.cuda.synchronize()
-            ref = torch.zeros(n, dtype=torch.float64)
+            acc = torch.zeros(n, dtype=torch.float32)
             for r in range(world):
-                gr = torch.Generator(device="cpu").manual_seed(1000 * n + 10 * it + r)
-                ref += torch.randn(n, generator=gr).to(torch.bfloat16).double()
-            errs.append(float((y.double().cpu() - ref).abs().max()))
+                acc += _inp(n, it, r).float()
+            if not torch.equal(y.cpu(), acc.to(torch.bfloat16)):
+                bad.append((n, it))
     # the kernel inside a captured graph: the device-side epochs advance on every replay
     x = torch.full((4096,), float(rank + 1), device="cuda:0", dtype=torch.bfloat16)
     s = torch.cuda.Stream()
@@ -49,15 +53,16 @@ def _body(rank, world, n_list, iters):
     err_flag = car.error()
     dist.barrier()
     car.close()
-    return max(errs), graph_ok, err_flag
+    return bad, graph_ok, err_flag
 
 
-def test_one_shot_allreduce_two_ranks_one_gpu():
-    res = run_ranks(_body, world=2, args=([8, 4096, 65536, 262144], 3), timeout=240)
-    for max_err, graph_ok, err_flag in res:
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_one_shot_allreduce_multirank_one_gpu(world):
+    res = run_ranks(_body, world=world, args=([8, 4096, 65536, 262144], 3), timeout=300)
+    for bad, graph_ok, err_flag in res:
         assert err_flag == 0
         assert graph_ok
-        assert max_err < 0.05, max_err     # bf16 output rounding of a 2-term sum
+        assert bad == [], bad
 
 
 def _stall_body(rank, world):
@@ -69,7 +74,7 @@ def _stall_body(rank, world):
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(0)
-    car = OneShotAllReduce(max_bytes=1 << 20, blocks=4)
+    car = OneShotAllReduce(max_bytes=1 << 20, blocks=4, timeout_s=1.0)
     x = torch.ones(4096, device="cuda:0", dtype=torch.bfloat16)
     car(x.clone())                        # both ranks: a healthy all-reduce first
     torch.cuda.synchronize()

@@ -1,12 +1,15 @@
 """Two-shot reduce-scatter / all-gather / all-reduce (ops/csrc/custom_ar.hip namespace ts,
-parallel/custom_ar.py TwoShot) with two ranks sharing the test box's one GPU (gloo carries only
-the IPC-handle exchange; the data moves through the peer-mapped uncached buffers, as over xGMI
-on an 8-GPU node).
+parallel/custom_ar.py TwoShot) with 2, 4 and 8 ranks sharing the test box's one GPU (gloo carries
+only the IPC-handle exchange; the data moves through the peer-mapped uncached buffers, as over
+xGMI on an 8-GPU node).  These are the W = 4 and W = 8 template instantiations an 8-GPU node
+runs (TP = 4 / 8), executed here before a multi-GPU node ever does.
 
-Two ranks: RCCL's sum of two bf16 tensors is one bf16 rounding of their exact fp32 sum, so the
-expected results below are exactly RCCL's (RCCL itself refuses two ranks on one GPU, so it
-cannot be run side by side here)."""
+Expected results are the kernel's DEFINED result, computed on the CPU: the fp32 sum of the ranks'
+bf16 inputs in rank order, rounded once to bf16 (for two ranks that is exactly RCCL's result:
+one rounding of the exact sum; RCCL itself refuses several ranks on one GPU, so it cannot run
+side by side here).  Every comparison is bitwise."""
 import os
+import time
 
 import pytest
 import torch
@@ -21,19 +24,26 @@ def _x(n, rank, it):
     return torch.randn(n, generator=g).to(torch.bfloat16)
 
 
-def _body(rank, world, sizes):
+def _rank_order_sum(xs):
+    acc = torch.zeros(xs[0].numel(), dtype=torch.float32)
+    for x in xs:
+        acc += x.float()
+    return acc.to(torch.bfloat16)
+
+
+def _body(rank, world, sizes, blocks):
     import torch.distributed as dist
 
     from service_account_auth_improvements_amd.parallel.custom_ar import TwoShot
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(0)
-    comm = TwoShot(max_bytes=64 << 20, blocks=64)
+    comm = TwoShot(max_bytes=64 << 20, blocks=blocks, timeout_s=60.0)
     bad = []
     for n in sizes:
         for it in range(2):
             xs = [_x(n, r, it) for r in range(world)]
-            ref = (xs[0].float() + xs[1].float()).to(torch.bfloat16)
+            ref = _rank_order_sum(xs)
             x = xs[rank].to("cuda:0")
             # all-reduce, in place (blocking)
             y = x.clone()
@@ -41,34 +51,104 @@ def _body(rank, world, sizes):
             if not torch.equal(y.cpu(), ref):
                 bad.append(("ar", n, it))
             # reduce-scatter, async handle
-            out = torch.empty(n // world, dtype=torch.bfloat16, device="cuda:0")
+            c = n // world
+            out = torch.empty(c, dtype=torch.bfloat16, device="cuda:0")
             w = comm.reduce_scatter(out, x, async_op=True)
             w.wait()
-            if not torch.equal(out.cpu(), ref[rank * n // world:(rank + 1) * n // world]):
+            if not torch.equal(out.cpu(), ref[rank * c:(rank + 1) * c]):
                 bad.append(("rs", n, it))
-            # all-gather of every rank's full x
-            full = torch.empty(n * world, dtype=torch.bfloat16, device="cuda:0")
-            comm.all_gather(full, x)
-            if not torch.equal(full.cpu(), torch.cat(xs)):
+            # all-gather: rank r contributes the first 1/W of its x, the result is n elements
+            full = torch.empty(n, dtype=torch.bfloat16, device="cuda:0")
+            comm.all_gather(full, x[:c].contiguous())
+            if not torch.equal(full.cpu(), torch.cat([xr[:c] for xr in xs])):
                 bad.append(("ag", n, it))
     torch.cuda.synchronize()
     calls = comm.calls
-    comm.check()
+    comm.check(sync=True)
+    comm.check()                      # the asynchronous form: queues a read, no host sync
     # outside the buffer / not bf16 -> torch.distributed (gloo here)
     big = torch.ones(8, dtype=torch.float32)
     comm.all_reduce(big)
     dist.barrier()
+    torch.cuda.synchronize()
+    comm.check()                      # reads the queued word (clean) and queues the next
     comm.close()
     return bad, calls, float(big[0])
 
 
-def test_two_shot_rs_ag_ar_bit_identical_two_ranks_one_gpu():
-    sizes = [16, 4096 * 8, 1 << 20, 16 << 20]      # up to 32 MB in, 64 MB gathered
-    res = run_ranks(_body, world=2, args=(sizes,), timeout=300)
+@pytest.mark.parametrize("world,blocks", [(2, 64), (4, 64), (8, 64), (4, 128)],
+                         ids=["w2", "w4", "w8", "w4-128blocks"])
+def test_two_shot_rs_ag_ar_bit_identical_multirank_one_gpu(world, blocks):
+    sizes = [8 * world, 4096 * 8, 1 << 20, 16 << 20]      # 16 elements .. 32 MB per rank
+    res = run_ranks(_body, world=world, args=(sizes, blocks), timeout=600)
     for bad, calls, fallback in res:
         assert bad == [], bad
         assert calls == 3 * 2 * len(sizes)
-        assert fallback == 2.0
+        assert fallback == float(world)
+
+
+def _stall_body(rank, world, mode):
+    import torch.distributed as dist
+
+    from service_account_auth_improvements_amd.parallel.custom_ar import TwoShot
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    timeout = 1.0 if mode == "dead" else 30.0
+    comm = TwoShot(max_bytes=4 << 20, blocks=16, timeout_s=timeout)
+    x = torch.full((4096,), float(rank + 1), device="cuda:0", dtype=torch.bfloat16)
+    y = x.clone()
+    comm.all_reduce(y)                 # every rank: one healthy call first
+    comm.check(sync=True)
+    dist.barrier()
+    raised = sticky = False
+    ok = None
+    if mode == "dead":
+        if rank == 0:                  # the last rank never calls again: rank 0 gives up after 1 s
+            y = x.clone()
+            comm.all_reduce(y)
+            try:
+                comm.check(sync=True)
+            except RuntimeError:
+                raised = True
+            try:
+                comm.check()
+            except RuntimeError:
+                sticky = True          # poisoned for good
+    else:                              # "late": the last rank arrives 2 s late, inside the budget
+        if rank == world - 1:
+            time.sleep(2.0)
+        y = x.clone()
+        comm.all_reduce(y)
+        torch.cuda.synchronize()
+        ok = bool((y.float() == world * (world + 1) / 2).all())
+        comm.check(sync=True)          # must not raise
+    dist.barrier()
+    if mode == "late" or rank == 0:
+        comm.close()
+    return rank, raised, sticky, ok
+
+
+def test_two_shot_dead_peer_sets_the_error_and_poisons():
+    res = run_ranks(_stall_body, world=2, args=("dead",), timeout=240)
+    r0, raised, sticky, _ = res[0]
+    assert r0 == 0 and raised and sticky
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_two_shot_late_peer_is_waited_for(world):
+    """A peer late by 2 s (a slow first step, a checkpoint write) is inside the 30 s wall-clock
+    budget: the call completes with the right sum and nothing is poisoned."""
+    res = run_ranks(_stall_body, world=world, args=("late",), timeout=240)
+    for _, raised, _, ok in res:
+        assert ok and not raised
+
+
+def _tp_cfg(world):
+    from service_account_auth_improvements_amd.models.llama import LlamaConfig
+    # TP = 4 needs 4 KV heads; the 2-rank runs keep the tiny preset
+    cfg = LlamaConfig.preset("tiny")
+    return cfg if world <= 2 else cfg.with_(n_kv_heads=4)
 
 
 def _train_body(rank, world, kind, sp):
@@ -77,7 +157,7 @@ def _train_body(rank, world, kind, sp):
     from service_account_auth_improvements_amd.runtime.trainer import TrainConfig, Trainer
     st = init_distributed(tp=world, pp=1, device="cuda")
     tr = Trainer(TrainConfig(model="tiny", seq_len=128, micro_batch=2, n_layers=2, lr=1e-3, sequence_parallel=sp,
-                             tp_comm_chunks=2, tp_comm=kind), st, full_init=True)
+                             tp_comm_chunks=2, tp_comm=kind), st, mcfg=_tp_cfg(world), full_init=True)
     assert type(st.tp_comm).__name__ == "TwoShot"
     g = torch.Generator().manual_seed(11)
     v = tr.mcfg.vocab_size
@@ -86,28 +166,29 @@ def _train_body(rank, world, kind, sp):
         b = [(torch.randint(0, v, (2, 128), generator=g).cuda(), torch.randint(0, v, (2, 128), generator=g).cuda())]
         losses.append(float(tr.train_step(b)))
     torch.cuda.synchronize()
-    st.tp_comm.check()
+    st.tp_comm.check(sync=True)
     return losses, st.tp_comm.calls
 
 
-@pytest.mark.parametrize("sp", [False, True], ids=["tp2", "tp2+sp"])
-def test_two_shot_tp2_training_matches_one_rank(sp):
-    """A TP=2 training step whose every activation collective (row-parallel reduce-scatter /
+@pytest.mark.parametrize("world,sp", [(2, False), (2, True), (4, False)], ids=["tp2", "tp2+sp", "tp4"])
+def test_two_shot_tp_training_matches_one_rank(world, sp):
+    """A TP training step whose every activation collective (row-parallel reduce-scatter /
     all-reduce, SP all-gather, backward input-gradient reductions) runs on the two-shot kernel
-    follows the single-rank step's losses."""
+    follows the single-rank step's losses (TP = 2 and, through the W = 4 kernels, TP = 4)."""
     from service_account_auth_improvements_amd.parallel.state import ParallelState
     from service_account_auth_improvements_amd.runtime.trainer import TrainConfig, Trainer
-    res = run_ranks(_train_body, world=2, args=("twoshot", sp), timeout=300)
+    res = run_ranks(_train_body, world=world, args=("twoshot", sp), timeout=300)
     tr = Trainer(TrainConfig(model="tiny", seq_len=128, micro_batch=2, n_layers=2, lr=1e-3),
-                 ParallelState(device=torch.device("cuda", 0)), full_init=True)
+                 ParallelState(device=torch.device("cuda", 0)), mcfg=_tp_cfg(world), full_init=True)
     g = torch.Generator().manual_seed(11)
     v = tr.mcfg.vocab_size
     ref = []
     for _ in range(2):
         b = [(torch.randint(0, v, (2, 128), generator=g).cuda(), torch.randint(0, v, (2, 128), generator=g).cuda())]
         ref.append(float(tr.train_step(b)))
-    (l0, c0), (l1, c1) = res
-    assert l0 == l1                       # both ranks computed the same bits
-    assert c0 == c1 and c0 > 0
+    l0, c0 = res[0]
+    for lr_, cr in res[1:]:
+        assert lr_ == l0                  # every rank computed the same bits
+        assert cr == c0 and c0 > 0
     for a, b in zip(l0, ref):
         assert abs(a - b) <= 2e-2 * abs(b), (l0, ref)
