@@ -7,6 +7,6 @@ cd "$(dirname "$0")"
 mkdir -p bin
 src=${3:-fa_bench.hip}
 extra=""
-case "$src" in fa_*) extra="-mllvm -amdgpu-mfma-vgpr-form" ;; esac
+case "$src" in fa*) extra="-mllvm -amdgpu-mfma-vgpr-form" ;; esac
 /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=fast -munsafe-fp-atomics $extra \
   -I../../service_account_auth_improvements_amd/ops/csrc $2 "$src" -o bin/$1

@@ -297,6 +297,14 @@ constexpr int FP = KF_FA_FWD_FP;
 // (measured and removed: ping-pong wave roles -- waves 4-7 taking each tile's barrier after their
 // S chain, 5-deep ring -- 2.31-2.36 vs 2.23-2.25 ms, profiles/fa_fwd_pingpong_ab.txt)
 constexpr int NSTF = NST;   // forward K+V ring depth
+// KF_FA_PKMUL=1: the forward's per-score scale multiply issued as packed pairs
+#ifndef KF_FA_PKMUL
+#define KF_FA_PKMUL 0
+#endif
+// KF_FA_FWD_PS=1: Q pre-scaled by scale*log2(e) in registers (bf16), so p = exp2(S') costs no multiply
+#ifndef KF_FA_FWD_PS
+#define KF_FA_FWD_PS 0
+#endif
 template <bool CAUSAL>
 __global__ __launch_bounds__(512, 1) void flash_fwd_kernel(
     const bf16_t* __restrict__ qkv, long ld, bf16_t* __restrict__ out, long ldo,
@@ -356,10 +364,23 @@ __global__ __launch_bounds__(512, 1) void flash_fwd_kernel(
   // a first use inside the loop would make hipcc wait vmcnt(0) on every tile
 #pragma unroll
   for (int ks = 0; ks < 8; ++ks) asm volatile("" : "+v"(qf[ks]));
+#if KF_FA_FWD_PS
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) {
+    float f[8];
+    unpack8(__builtin_bit_cast(u32x4, qf[ks]), f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] *= scale_log2;
+    qf[ks] = as_bf16x8(pack8(f));
+  }
+  const float sl = 1.f;        // S' is already in log2 units
+#else
+  const float sl = scale_log2;
+#endif
   const bf16x8 ones = fold_ones(hh);
   bf16x8 mref = bf16x8{};    // folded -m (m bf16-exact: the hi part carries it, lo = 0)
   bool first = true;
-  const float thresh = FOLD_T / scale_log2;   // m and S' are in raw score units
+  const float thresh = FOLD_T / sl;   // m and S' are in raw score units (log2 units with PS)
   float m = 0.f, lsum = 0.f;
   f32x16 o[4];
 #pragma unroll
@@ -422,7 +443,7 @@ __global__ __launch_bounds__(512, 1) void flash_fwd_kernel(
         // move the reference: m' = bf16(m + max(mx, 0)); rescale O, l and this tile's S'
         const float mnew = first ? bf16_round(mx) : bf16_round(m + fmaxf(mx, 0.f));
         const float shift = first ? mnew : mnew - m;
-        const float alpha = first ? 0.f : __builtin_amdgcn_exp2f(-shift * scale_log2);
+        const float alpha = first ? 0.f : __builtin_amdgcn_exp2f(-shift * sl);
         lsum *= alpha;
 #pragma unroll
         for (int t = 0; t < 4; ++t)
@@ -437,14 +458,28 @@ __global__ __launch_bounds__(512, 1) void flash_fwd_kernel(
         mref = fold_const(m, hh);
       }
       float rs = 0.f;
+#if KF_FA_PKMUL
+      // the scale multiply in pairs: v_pk_mul_f32 (16 issues per tile instead of 32)
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+          const f32x2_t t = f32x2_t{sc[kt][r], sc[kt][r + 1]} * f32x2_t{sl, sl};
+          const float p0 = __builtin_amdgcn_exp2f(t[0]), p1 = __builtin_amdgcn_exp2f(t[1]);
+          sc[kt][r] = p0;
+          sc[kt][r + 1] = p1;
+          rs += p0 + p1;
+        }
+#else
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float p = __builtin_amdgcn_exp2f(sc[kt][r] * scale_log2);
+          const float p = __builtin_amdgcn_exp2f(sc[kt][r] * sl);
           sc[kt][r] = p;
           rs += p;
         }
+#endif
       lsum += xor32_sum(rs);
       bf16x8 pf[2][2];
 #pragma unroll
@@ -511,7 +546,7 @@ __global__ __launch_bounds__(512, 1) void flash_fwd_kernel(
       v[1] = pack2(o[t][4 * gq + 2] * inv, o[t][4 * gq + 3] * inv);
       *reinterpret_cast<u32x2*>(op + d) = v;
     }
-  if (hh == 0) lse_out[((long)b * Hq + h) * S + q] = (m * scale_log2 + log2f(lsum)) * LN2;
+  if (hh == 0) lse_out[((long)b * Hq + h) * S + q] = (m * sl + log2f(lsum)) * LN2;
 }
 
 // ====================================================================================
@@ -811,6 +846,9 @@ constexpr int SMEM = OFF_K + BKVW * 256;       // 66048 B (2 WG per CU) / 98816 
 #endif
 constexpr int PA = KF_FA_DKDV_PA, PT = KF_FA_DKDV_PT;
 // 1 = s_setprio 1 over the MFMA chains, 0 over the softmax VALU and the DMA issue
+#ifndef KF_FA_DKDV_PS
+#define KF_FA_DKDV_PS 0
+#endif
 #ifndef KF_FA_DKDV_PRIO
 #define KF_FA_DKDV_PRIO 1
 #endif
@@ -951,6 +989,22 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
   if (niter > 0) stage(0, 0);
 #endif
   wait_dma_barrier();
+#if KF_FA_DKDV_PS
+  {   // K' = c K in place (the fold then carries lse log2 e and p = exp2(S'))
+    u32x4* kimg = reinterpret_cast<u32x4*>(smem + OFF_K);
+    for (int i = tid; i < BKVW * 16; i += 64 * NWK) {
+      float f[8];
+      unpack8(kimg[i], f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] *= c;
+      kimg[i] = pack8(f);
+    }
+    __syncthreads();
+  }
+  const float fold_mul = LOG2E, pmul = 1.f;
+#else
+  const float fold_mul = inv_scale, pmul = c;
+#endif
   const bf16x8 ones = fold_ones(hh);
 #if KF_FA_DKDV_PIPE
   int nx_hq = 0, nx_qt = 0;   // (head, tile) of the NEXT iteration to stage
@@ -1007,7 +1061,7 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
       static_for<0, PA>([&](auto kc) { rdA(kc); });
       lgkm_tie_f2<3 * PA>(lse_v, dl_v);
       // row constants -lse/scale and -delta of query row lr folded into the chains
-      f32x16 s = mfma32(fold_const(lse_v * inv_scale, hh), ones, f32x16{});
+      f32x16 s = mfma32(fold_const(lse_v * fold_mul, hh), ones, f32x16{});
       f32x16 dp = mfma32(fold_const(dl_v, hh), ones, f32x16{});
       static_for<0, 8>([&](auto kc) {
         constexpr int ks = decltype(kc)::value, sl = ks % (PA + 1);
@@ -1035,12 +1089,12 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
       if (need_mask) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float p = __builtin_amdgcn_exp2f(s[r] * c);
+          const float p = __builtin_amdgcn_exp2f(s[r] * pmul);
           s[r] = key > q0 + (r & 3) + 8 * (r >> 2) + 4 * hh ? 0.f : p;
         }
       } else {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) s[r] = __builtin_amdgcn_exp2f(s[r] * c);
+        for (int r = 0; r < 16; ++r) s[r] = __builtin_amdgcn_exp2f(s[r] * pmul);
       }
       bf16x8 pf[2], sf[2];
 #pragma unroll
@@ -1103,12 +1157,12 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
       if (need_mask) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float p = __builtin_amdgcn_exp2f(s[r] * c);
+          const float p = __builtin_amdgcn_exp2f(s[r] * pmul);
           s[r] = key > q0 + (r & 3) + 8 * (r >> 2) + 4 * hh ? 0.f : p;
         }
       } else {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) s[r] = __builtin_amdgcn_exp2f(s[r] * c);
+        for (int r = 0; r < 16; ++r) s[r] = __builtin_amdgcn_exp2f(s[r] * pmul);
       }
       bf16x8 pf[2];
 #pragma unroll
