@@ -194,8 +194,8 @@ def main():
                          "for ZeRO-1 at any N), else 2")
     ap.add_argument("--grad-accum", type=int, default=1)
     ap.add_argument("--zero1", dest="zero1", action="store_true", default=None,
-                    help="ZeRO-1: reduce-scatter grads, 1/N-sharded AdamW, parameter all-gather hidden "
-                         "behind the next forward (default when N > 1)")
+                    help="ZeRO-1 DDP: reduce-scatter grads, 1/N-sharded AdamW, parameter all-gather hidden "
+                         "behind the next forward (the default at every N; one shard at N = 1)")
     ap.add_argument("--no-zero1", dest="zero1", action="store_false", help="classic all-reduce DDP")
     ap.add_argument("--bucket-mb", type=int, default=256)
     ap.add_argument("--grad-reduce", default="fp32", choices=["fp32", "bf16"],
@@ -295,7 +295,9 @@ def _run(a, rank: int, crd):
     progress.mark("model_init")
     world = st.world_size
     if a.zero1 is None:
-        a.zero1 = st.dp > 1 or a.force_collectives
+        # one optimizer plan along the whole 1 -> N curve: ZeRO-1 DDP at every N (at dp1 its one
+        # shard is the whole AdamW state -- the same step and memory as unsharded)
+        a.zero1 = True
     if a.micro_batch <= 0:
         big = (st.device.type == "cuda" and torch.cuda.get_device_properties(st.device).total_memory >= 280e9
                and a.model == "llama3-8b" and a.seq_len // (st.dp if a.cp else 1) <= 8192 and a.tp == 1
@@ -391,6 +393,7 @@ def _run(a, rank: int, crd):
                 "parallelism": "".join(f"{k}{v}" for k, v in (("cp" if a.cp else "dp", st.dp), ("tp", a.tp), ("pp", a.pp))
                                        if v > 1 or k in ("dp", "cp")),
                 "optimizer_sharding": "zero1" if a.zero1 else "none",
+                "optimizer_shards": st.dp if a.zero1 else 1,
                 "grad_reduce": a.grad_reduce,
                 "micro_batch": a.micro_batch,
                 "grad_accum": a.grad_accum,

@@ -25,19 +25,44 @@ namespace {
 constexpr int D = 128;
 constexpr int NT = 256;
 constexpr int MAXG = 8;
-constexpr int MAXCHUNK = 1024;
+constexpr int SUB = 1024;       // keys per sub-chunk (LDS score rows)
 constexpr float LOG2E = 1.4426950408889634f;
 
+// DPP lane moves within a 16-lane row: one VALU op each (ds_bpermute, which __shfl_xor becomes,
+// is an LDS round trip, and the per-key score reductions were a chain of them)
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+// acc + a.lo * b.lo + a.hi * b.hi for packed bf16 pairs (v_dot2c_f32_bf16)
+__device__ __forceinline__ float dot2_bf16(u32 a, u32 b, float acc) {
+  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, a), __builtin_bit_cast(bf16x2_t, b), acc, false);
+}
+// sum over the 16 lanes of a row, identical bits in every lane (each step pairs lanes
+// symmetrically): quad_perm [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror, row_mirror
+__device__ __forceinline__ float row16_sum(float a) {
+  a += dpp<0xB1>(a);
+  a += dpp<0x4E>(a);
+  a += dpp<0x141>(a);
+  a += dpp<0x140>(a);
+  return a;
+}
+
+// One workgroup per (split, kv head, row).  4 workgroups per CU at G = 4 (launch bounds:
+// <= 128 VGPRs): B * Hkv = 1024 workgroups at batch 128 run in one round.  (A grid capped at 2
+// workgroups per CU walking 2 items each, with 6 rows per stream in flight, measured the same
+// 93.5 us per layer at batch 128 and spilled SGPRs.)
 template <int G>
-__global__ __launch_bounds__(NT) void decode_split_kernel(
+__global__ __launch_bounds__(NT, G <= 4 ? 4 : 2) void decode_split_kernel(
     const bf16_t* __restrict__ q, long q_ld, int hq_total,
     const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
     const int* __restrict__ slots, const int* __restrict__ lengths,
     long slot_stride, long head_stride, int splits, float scale_log2,
-    float* __restrict__ part_o, float* __restrict__ part_ml) {
-  __shared__ float sc[G][MAXCHUNK];
+    float* __restrict__ part_o, float* __restrict__ part_ml, bf16_t* __restrict__ out, long out_ld) {
+  // score rows padded by one round of keys: the last round writes (never read) past the chunk
+  __shared__ float sc[G][SUB + 64];
   __shared__ float red[4][G][D];
-  __shared__ float hm[G], hl[G];
+  __shared__ float hm[G], hl[G], ha[G];
 
   const int s = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -48,8 +73,15 @@ __global__ __launch_bounds__(NT) void decode_split_kernel(
   const int start = s * chunk;
   const int end = min(len, start + chunk);
   const long obase = ((long)b * hq_total + (long)hk * G) * splits + s;   // index of (b, h0, s)
+  // one split (large batch: B * Hkv workgroups fill the chip on their own): normalise here and
+  // write the bf16 output, no combine launch
+  const bool direct = splits == 1;
 
   if (start >= end) {   // empty split: neutral element for the combine
+    if (direct) {
+      for (int e = tid; e < G * D; e += NT) out[(long)b * out_ld + (long)(hk * G) * D + e] = f2bf(0.f);
+      return;
+    }
     if (tid < G) {
       part_ml[(obase + (long)tid * splits) * 2 + 0] = -INFINITY;
       part_ml[(obase + (long)tid * splits) * 2 + 1] = 0.f;
@@ -60,105 +92,157 @@ __global__ __launch_bounds__(NT) void decode_split_kernel(
     return;
   }
   const int n = end - start;
+  for (int e = tid; e < 4 * G * D; e += NT) (&red[0][0][0])[e] = 0.f;   // ordered by phase 1's barrier
 
-  // Latency, not bandwidth, bounds a batch-1 split (32 keys at 1024 / 32 splits): every global
-  // load below is issued before the first one is needed -- q, the first round's K rows and the
-  // first two rounds' V rows together, each next K row one round ahead -- so a short split pays
-  // about one memory round trip instead of one per phase (8.3 us per layer before, gpurun_out/r4u)
+  // Memory-level parallelism is the whole game here: at large batch every CU runs 4 of these
+  // workgroups and the chip is HBM-bound only if each keeps enough bytes in flight.  Every
+  // 16-lane stream therefore loads R = 3 key rows per round and issues the NEXT round's rows
+  // before it computes on the current ones (6 rows = 96 B per lane in flight, 96 KB per CU);
+  // the first V round is issued before phase 1 ends.  (R = 4 at 3 workgroups per CU has the
+  // same bytes in flight but left B * Hkv = 1024 workgroups a 1.33-round tail: 102 vs 93.5 us
+  // per layer at batch 128.)  Row indices are clamped to the sub-chunk (always valid
+  // addresses, no load under a branch: hipcc waited for every load in flight at each branch);
+  // what lies past it is masked in the arithmetic.  One load in flight per stream measured
+  // 4.2-4.3 TB/s at batch 64-128 (profiles/serve_llama3_8b_r4_final.jsonl).
+  constexpr int R = 3;
   const long kvbase = (long)slots[b] * slot_stride + (long)hk * head_stride;
-  const bf16_t* kp = kc + kvbase + (long)start * D + sub * 8;
-  const bf16_t* vp = vc + kvbase + (long)start * D + sub * 8;
-  const u32x4 zero = u32x4{0u, 0u, 0u, 0u};
-  u32x4 kcur = grp < n ? ld16(kp + (long)grp * D) : zero;
-  const u32x4 v0 = grp < n ? ld16(vp + (long)grp * D) : zero;
-  const u32x4 v1 = grp + 16 < n ? ld16(vp + (long)(grp + 16) * D) : zero;
+  const bf16_t* kbase = kc + kvbase + (long)start * D + sub * 8;
+  const bf16_t* vbase = vc + kvbase + (long)start * D + sub * 8;
 
-  // q for the G heads of this kv head: 8 dims per lane, pre-scaled into the log2 domain
-  float qf[G][8];
-#pragma unroll
-  for (int h = 0; h < G; ++h) {
-    const u32x4 v = ld16(q + (long)b * q_ld + (long)(hk * G + h) * D + sub * 8);
-    unpack8(v, qf[h]);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) qf[h][i] *= scale_log2;
-  }
 
-  // ---- phase 1: scores
-  for (int j0 = 0; j0 < n; j0 += 16) {
-    const int j = j0 + grp;
-    const u32x4 knext = j + 16 < n ? ld16(kp + (long)(j + 16) * D) : zero;
-    float kf_[8];
-    unpack8(kcur, kf_);
-    kcur = knext;
+  // The chunk is walked in sub-chunks of at most SUB keys (the LDS score buffer), merged online
+  // (running max / sum per head, the accumulator rescaled between sub-chunks): the split count
+  // is chosen for parallelism alone, not bounded below by the slot length Lmax.
+  for (int c0 = 0; c0 < n; c0 += SUB) {
+    const int nc = min(SUB, n - c0);
+    const bf16_t* kp = kbase + (long)c0 * D;
+    const bf16_t* vp = vbase + (long)c0 * D;
+    auto row = [&](int j) { return (long)min(j, nc - 1) * D; };
+    u32x4 kb[R];
 #pragma unroll
-    for (int h = 0; h < G; ++h) {
-      float a = 0.f;
+    for (int u = 0; u < R; ++u) kb[u] = ld16(kp + row(grp + 16 * u));
+    // q for the G heads of this kv head: 8 dims per lane, packed bf16 (the dot products are
+    // v_dot2 on bf16 pairs, exact products summed in fp32; the log2-domain scale is applied to
+    // the reduced score).  Re-read per sub-chunk (an L2 hit) so it is not live in phase 3.
+    u32x4 qb[G];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) a = fmaf(qf[h][i], kf_[i], a);
-      a += __shfl_xor(a, 1, 64);
-      a += __shfl_xor(a, 2, 64);
-      a += __shfl_xor(a, 4, 64);
-      a += __shfl_xor(a, 8, 64);
-      if (sub == 0 && j < n) sc[h][j] = a;
-    }
-  }
-  __syncthreads();
+    for (int h = 0; h < G; ++h) qb[h] = ld16(q + (long)b * q_ld + (long)(hk * G + h) * D + sub * 8);
 
-  // ---- phase 2: softmax statistics per head (wave w handles heads w, w+4)
-  for (int h = wave; h < G; h += 4) {
-    float m = -INFINITY;
-    for (int j = lane; j < n; j += 64) m = fmaxf(m, sc[h][j]);
-    m = wave_max(m);
-    float l = 0.f;
-    for (int j = lane; j < n; j += 64) {
-      const float p = exp2f(sc[h][j] - m);
-      sc[h][j] = p;
-      l += p;
+    // ---- phase 1: scores, R keys per stream per round, the next round's rows in flight
+    for (int j0 = 0; j0 < nc; j0 += 16 * R) {
+      u32x4 kn[R];
+#pragma unroll
+      for (int u = 0; u < R; ++u) kn[u] = ld16(kp + row(j0 + 16 * R + grp + 16 * u));
+#pragma unroll
+      for (int u = 0; u < R; ++u) {
+        const int j = j0 + grp + 16 * u;
+        // 4 v_dot2 per head on the packed rows (no bf16 -> fp32 unpack of k; decode attention
+        // is close to VALU-bound at G = 4), then the 16-lane row sum by DPP
+        float a[G];
+#pragma unroll
+        for (int h = 0; h < G; ++h) {
+          float t = dot2_bf16(qb[h][0], kb[u][0], 0.f);
+          t = dot2_bf16(qb[h][1], kb[u][1], t);
+          t = dot2_bf16(qb[h][2], kb[u][2], t);
+          t = dot2_bf16(qb[h][3], kb[u][3], t);
+          a[h] = row16_sum(t);
+        }
+        // lane `sub` of the row stores head `sub`'s score (no per-head branch); j >= nc lands
+        // in the padding, which phase 2 overwrites with p = 0
+        float v = a[0];
+#pragma unroll
+        for (int h = 1; h < G; ++h) v = sub == h ? a[h] : v;
+        if (sub < G) sc[sub][j] = v * scale_log2;
+        kb[u] = kn[u];
+      }
     }
-    l = wave_sum(l);
-    if (lane == 0) { hm[h] = m; hl[h] = l; }
-  }
-  __syncthreads();
+    // the first V round goes out before the barrier
+    u32x4 vb[R];
+#pragma unroll
+    for (int u = 0; u < R; ++u) vb[u] = ld16(vp + row(grp + 16 * u));
+    __syncthreads();
 
-  // ---- phase 3: P.V with 16 key streams
-  float acc[G][8];
-#pragma unroll
-  for (int h = 0; h < G; ++h)
-#pragma unroll
-    for (int i = 0; i < 8; ++i) acc[h][i] = 0.f;
-  for (int j = grp; j < n; j += 16) {
-    float vf[8];
-    unpack8(j < 16 ? v0 : j < 32 ? v1 : ld16(vp + (long)j * D), vf);
-#pragma unroll
-    for (int h = 0; h < G; ++h) {
-      const float p = sc[h][j];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) acc[h][i] = fmaf(p, vf[i], acc[h][i]);
+    // ---- phase 2: softmax statistics per head (wave w handles heads w, w+4), merged with the
+    // previous sub-chunks'
+    for (int h = wave; h < G; h += 4) {
+      float m = -INFINITY;
+      for (int j = lane; j < nc; j += 64) m = fmaxf(m, sc[h][j]);
+      m = wave_max(m);
+      const float m_old = c0 == 0 ? -INFINITY : hm[h];
+      const float mn = fmaxf(m, m_old);
+      float l = 0.f;
+      // through the padding of the last 16R-key round: phase 3 reads p = 0 there, no masking
+      for (int j = lane; j < (nc + 16 * R - 1) / (16 * R) * (16 * R); j += 64) {
+        const float p = j < nc ? exp2f(sc[h][j] - mn) : 0.f;
+        sc[h][j] = p;
+        l += p;
+      }
+      l = wave_sum(l);
+      if (lane == 0) {
+        const float alpha = c0 == 0 ? 0.f : exp2f(m_old - mn);
+        hm[h] = mn;
+        hl[h] = c0 == 0 ? l : fmaf(hl[h], alpha, l);
+        ha[h] = alpha;
+      }
     }
-  }
-  // reduce the 4 streams of a wave (lanes l, l^16, l^32, l^48 share a column)
-#pragma unroll
-  for (int h = 0; h < G; ++h)
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      float a = acc[h][i];
-      a += __shfl_xor(a, 16, 64);
-      a += __shfl_xor(a, 32, 64);
-      acc[h][i] = a;
-    }
-  if (lane < 16) {
+    __syncthreads();
+
+    // ---- phase 3: P.V, R keys per stream per round, the next round's rows in flight.  The
+    // sub-chunk's sum is folded into the wave's row of `red` at the end (rescaled by alpha), so
+    // no accumulator stays live through phase 1.
+    float acc[G][8];
 #pragma unroll
     for (int h = 0; h < G; ++h)
 #pragma unroll
-      for (int i = 0; i < 8; ++i) red[wave][h][sub * 8 + i] = acc[h][i];
+      for (int i = 0; i < 8; ++i) acc[h][i] = 0.f;
+    for (int j0 = 0; j0 < nc; j0 += 16 * R) {
+      u32x4 vn[R];
+#pragma unroll
+      for (int u = 0; u < R; ++u) vn[u] = ld16(vp + row(j0 + 16 * R + grp + 16 * u));
+#pragma unroll
+      for (int u = 0; u < R; ++u) {
+        const int j = j0 + grp + 16 * u;       // < nc rounded up to 16R: zero past nc (phase 2)
+        float vf[8];
+        unpack8(vb[u], vf);
+#pragma unroll
+        for (int h = 0; h < G; ++h) {
+          const float p = sc[h][j];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) acc[h][i] = fmaf(p, vf[i], acc[h][i]);
+        }
+        vb[u] = vn[u];
+      }
+    }
+    // reduce the 4 streams of a wave (lanes l, l^16, l^32, l^48 share a column) into red[wave]
+#pragma unroll
+    for (int h = 0; h < G; ++h)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float a = acc[h][i];
+        a += __shfl_xor(a, 16, 64);
+        a += __shfl_xor(a, 32, 64);
+        acc[h][i] = a;
+      }
+    if (lane < 16) {
+#pragma unroll
+      for (int h = 0; h < G; ++h) {
+        const float al = ha[h];                 // 0 for the first sub-chunk (red starts at 0)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) red[wave][h][sub * 8 + i] = fmaf(red[wave][h][sub * 8 + i], al, acc[h][i]);
+      }
+    }
+    if (c0 + SUB < n) __syncthreads();     // the next sub-chunk's phase 1 rewrites sc
   }
   __syncthreads();
   for (int e = tid; e < G * D; e += NT) {
     const int h = e / D, d = e % D;
     const float o = red[0][h][d] + red[1][h][d] + red[2][h][d] + red[3][h][d];
-    part_o[(obase + (long)h * splits) * D + d] = o;
+    if (direct)
+      out[(long)b * out_ld + (long)(hk * G + h) * D + d] = f2bf(hl[h] > 0.f ? o / hl[h] : 0.f);
+    else
+      part_o[(obase + (long)h * splits) * D + d] = o;
   }
-  if (tid < G) {
+  if (tid < G && !direct) {
     part_ml[(obase + (long)tid * splits) * 2 + 0] = hm[tid];
     part_ml[(obase + (long)tid * splits) * 2 + 1] = hl[tid];
   }
@@ -436,20 +520,21 @@ void launch_fused(dim3 grid, hipStream_t st, const bf16_t* q, long q_ld, int hq,
 template <int G>
 void launch_split(dim3 grid, hipStream_t st, const bf16_t* q, long q_ld, int hq, const bf16_t* kc,
                   const bf16_t* vc, const int* slots, const int* lengths, long slot_stride,
-                  long head_stride, int splits, float sl2, float* po, float* pml) {
+                  long head_stride, int splits, float sl2, float* po, float* pml, bf16_t* out, long out_ld) {
   hipLaunchKernelGGL(decode_split_kernel<G>, grid, dim3(NT), 0, st, q, q_ld, hq, kc, vc, slots, lengths,
-                     slot_stride, head_stride, splits, sl2, po, pml);
+                     slot_stride, head_stride, splits, sl2, po, pml, out, out_ld);
 }
 
 }  // namespace
 
-// Number of key splits for a batch: enough workgroups to cover 256 CUs ~4x, chunks of at
-// most MAXCHUNK keys (LDS score buffer) and at least 64 keys.
+// Number of key splits for a batch: about two workgroups per CU (B * Hkv * splits >= 512) and
+// chunks of at least 64 keys.  Any chunk length works (sub-chunks of SUB keys).  Measured in a
+// 32-layer graph at context 1024 (tools/bench_decode_splits.py): batch 64 runs 42.5 us per layer
+// at 1 split (512 workgroups, no combine) against 53.4 at 2 and 49.7 at 3.
 extern "C" int kf_decode_splits(int B, int Hkv, int Lmax) {
-  int want = std::max(1, (1024 + B * Hkv - 1) / (B * Hkv));
-  int max_by_len = std::max(1, Lmax / 64);
-  int min_by_lds = (Lmax + MAXCHUNK - 17) / (MAXCHUNK - 16);
-  return std::max(min_by_lds, std::min(want, max_by_len));
+  const int want = std::max(1, (512 + B * Hkv - 1) / (B * Hkv));
+  const int max_by_len = std::max(1, Lmax / 64);
+  return std::min(want, max_by_len);
 }
 
 // Small-batch single-launch decode attention (B <= SMALL_B).  splits1: key splits per (row, kv
@@ -499,7 +584,6 @@ extern "C" int kf_decode_attn(const void* q, long q_ld, const void* kc, const vo
   if (Dh != D || Hkv <= 0 || Hq % Hkv != 0) return 1;
   const int G = Hq / Hkv;
   if (G > MAXG || splits <= 0 || splits > CB_MAXS) return 2;
-  if ((Lmax + splits - 1) / splits > MAXCHUNK - 16) return 3;
   if (B == 0) return 0;
   const long head_stride = (long)Lmax * D, slot_stride = (long)Hkv * head_stride;
   const float sl2 = scale * LOG2E;
@@ -508,14 +592,15 @@ extern "C" int kf_decode_attn(const void* q, long q_ld, const void* kc, const vo
   auto k16 = (const bf16_t*)kc;
   auto v16 = (const bf16_t*)vc;
   switch (G) {
-    case 1: launch_split<1>(grid, st, q16, q_ld, Hq, k16, v16, slots, lengths, slot_stride, head_stride, splits, sl2, part_o, part_ml); break;
-    case 2: launch_split<2>(grid, st, q16, q_ld, Hq, k16, v16, slots, lengths, slot_stride, head_stride, splits, sl2, part_o, part_ml); break;
-    case 4: launch_split<4>(grid, st, q16, q_ld, Hq, k16, v16, slots, lengths, slot_stride, head_stride, splits, sl2, part_o, part_ml); break;
-    case 8: launch_split<8>(grid, st, q16, q_ld, Hq, k16, v16, slots, lengths, slot_stride, head_stride, splits, sl2, part_o, part_ml); break;
+    case 1: launch_split<1>(grid, st, q16, q_ld, Hq, k16, v16, slots, lengths, slot_stride, head_stride, splits, sl2, part_o, part_ml, (bf16_t*)out, out_ld); break;
+    case 2: launch_split<2>(grid, st, q16, q_ld, Hq, k16, v16, slots, lengths, slot_stride, head_stride, splits, sl2, part_o, part_ml, (bf16_t*)out, out_ld); break;
+    case 4: launch_split<4>(grid, st, q16, q_ld, Hq, k16, v16, slots, lengths, slot_stride, head_stride, splits, sl2, part_o, part_ml, (bf16_t*)out, out_ld); break;
+    case 8: launch_split<8>(grid, st, q16, q_ld, Hq, k16, v16, slots, lengths, slot_stride, head_stride, splits, sl2, part_o, part_ml, (bf16_t*)out, out_ld); break;
     default: return 4;
   }
-  hipLaunchKernelGGL(decode_combine_kernel, dim3(B * Hq), dim3(CB_NT), 0, st, part_o, part_ml, splits,
-                     (bf16_t*)out, out_ld, Hq);
+  if (splits > 1)
+    hipLaunchKernelGGL(decode_combine_kernel, dim3(B * Hq), dim3(CB_NT), 0, st, part_o, part_ml, splits,
+                       (bf16_t*)out, out_ld, Hq);
   KF_CHECK_LAUNCH();
   return 0;
 }

@@ -133,17 +133,19 @@ class TwoShot:
 
     MAX_BLOCKS = 128
 
-    # workgroups per call: measured on one MI355X at 16/64/268 MB for 32/64/128 blocks
-    # (tools/bench_two_shot.py, profiles/two_shot_blocks_r5.md): 128 is fastest at every size
-    # and mode (RS 268 MB: 0.44 ms vs 0.70 at 64 and 1.21 at 32) -- each block keeps only a few
-    # uncached loads in flight, so the kernel needs the blocks to reach bandwidth
-    def __init__(self, group=None, max_bytes: int = 288 << 20, blocks: int = 128, timeout_s: float = 300.0):
+    # workgroups per call (blocks=None): measured on one MI355X at 16/64/268 MB for 32/64/128
+    # blocks (tools/bench_two_shot.py, profiles/two_shot_blocks_r5.md): 128 is fastest at every
+    # size and mode (RS 268 MB: 0.44 ms vs 0.70 at 64 and 1.21 at 32) -- each block keeps only a
+    # few uncached loads in flight, so the kernel needs the blocks to reach bandwidth
+    DEFAULT_BLOCKS = 128
+
+    def __init__(self, group=None, max_bytes: int = 288 << 20, blocks: Optional[int] = None,
+                 timeout_s: float = 300.0):
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         assert self.world in (1, 2, 4, 8), "two-shot collectives support 1, 2, 4 or 8 ranks"
         self.max_bytes = int(max_bytes) // (16 * self.world) * (16 * self.world)
-        self.blocks = max(1, min(int(blocks), self.MAX_BLOCKS))
         # wall-clock budget (s_memrealtime) a kernel block waits for a peer: a late peer -- one
         # rank's first-step GEMM heuristics, a checkpoint write -- is waited for; only one that
         # stays away this long sets the error word.  The trainer passes its process-group
@@ -151,8 +153,22 @@ class TwoShot:
         self.timeout_s = float(timeout_s)
         k = _ext.ops()
         self._own, handle = k.ts_alloc(self.max_bytes, self.world)
-        handles: List[Optional[torch.Tensor]] = [None] * self.world
-        dist.all_gather_object(handles, handle, group=group)
+        props = torch.cuda.get_device_properties(torch.cuda.current_device())
+        dev_key = (str(props.uuid), props.pci_domain_id, props.pci_bus_id, props.pci_device_id)
+        gathered: List[Optional[tuple]] = [None] * self.world
+        dist.all_gather_object(gathered, (handle, dev_key), group=group)
+        handles = [g[0] for g in gathered]
+        # Ranks that share one GPU (the one-GPU multi-process tests and rehearsals): a call's
+        # blocks spin on the card until every peer's call arrives, so with W ranks x 128 blocks
+        # they can fill every CU and starve a peer's preceding kernels (its attention needs a
+        # whole CU's LDS) until the wait budget runs out.  The automatic count is then capped
+        # to leave half the CUs free; one rank per GPU (production) keeps the measured 128.
+        sharing = sum(1 for g in gathered if g[1] == dev_key)
+        if blocks is None:
+            blocks = self.DEFAULT_BLOCKS
+            if sharing > 1:
+                blocks = min(blocks, max(1, props.multi_processor_count // (2 * sharing)))
+        self.blocks = max(1, min(int(blocks), self.MAX_BLOCKS))
         self.ptrs, self._opened = [], []
         for r, h in enumerate(handles):
             if r == self.rank:

@@ -41,6 +41,8 @@ def test_bench_single_process_json():
     recs = _json_lines(r.stdout)
     assert len(recs) == 1
     _check(recs[0], 1)
+    # one optimizer plan along the 1 -> N curve (ZeRO-1; one shard at N = 1)
+    assert recs[0]["config"]["optimizer_sharding"] == "zero1" and recs[0]["config"]["optimizer_shards"] == 1
 
 
 def test_bench_reports_crd_to_first_step():
@@ -72,7 +74,7 @@ def test_bench_two_ranks_torchrun_json():
     recs = _json_lines(r.stdout)
     assert len(recs) == 1, r.stdout          # rank 0 only
     _check(recs[0], 2)
-    assert recs[0]["config"]["optimizer_sharding"] == "zero1"
+    assert recs[0]["config"]["optimizer_sharding"] == "zero1" and recs[0]["config"]["optimizer_shards"] == 2
 
 
 def test_bench_self_launches_ranks_without_torchrun():

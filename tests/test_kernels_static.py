@@ -79,3 +79,4 @@ def test_noop_extension_load_does_not_import_cpp_extension():
             "print('cpp_extension' if 'torch.utils.cpp_extension' in sys.modules else 'clean', time.time() - t)")
     out = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, check=True)
     assert out.stdout.split()[0] == "clean", out.stdout + out.stderr
+

@@ -31,7 +31,11 @@ def _ref_decode(q2d, kc, vc, slots, lengths, Hq):
     (2, 16, 2, 8192, [8192, 5000]), (4, 4, 4, 128, [128, 3, 64, 100]),
     # one-pass streaming kernel (chunks >= 256 keys): ragged lengths, tails, an empty split
     (32, 32, 8, 4096, [4096, 1, 17, 255, 256, 257, 1000, 3071] * 4),
-    (8, 64, 8, 16384, [16384, 9000, 1, 300, 5000, 16383, 2048, 7]), (16, 16, 2, 2048, [2048, 1500] * 8)])
+    (8, 64, 8, 16384, [16384, 9000, 1, 300, 5000, 16383, 2048, 7]), (16, 16, 2, 2048, [2048, 1500] * 8),
+    # large batch: 2 splits (B * Hkv = 512) and 1 split (1024, normalised in the split kernel, no
+    # combine); chunks longer than one 1024-key sub-chunk are merged online inside the workgroup
+    (64, 32, 8, 4096, [4096, 1, 2048, 2049, 3071, 1025, 17, 4000] * 8),
+    (128, 32, 8, 3000, [3000, 1, 1024, 1025, 2049, 64, 2999, 700] * 16)])
 def test_decode_attn(B, Hq, Hkv, Lmax, lens):
     assert _ext.load()
     g = torch.Generator(device="cpu").manual_seed(B * 7 + Lmax)

@@ -159,6 +159,10 @@ def _train_body(rank, world, kind, sp):
     tr = Trainer(TrainConfig(model="tiny", seq_len=128, micro_batch=2, n_layers=2, lr=1e-3, sequence_parallel=sp,
                              tp_comm_chunks=2, tp_comm=kind), st, mcfg=_tp_cfg(world), full_init=True)
     assert type(st.tp_comm).__name__ == "TwoShot"
+    # all ranks share the one GPU: the automatic block count leaves half the CUs to the peers'
+    # other kernels (W x 128 spinning blocks would starve them)
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    assert st.tp_comm.blocks == min(128, cus // (2 * world)), st.tp_comm.blocks
     g = torch.Generator().manual_seed(11)
     v = tr.mcfg.vocab_size
     losses = []

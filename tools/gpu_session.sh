@@ -10,6 +10,8 @@
 #   bench[:STEPS[:WARMUP]]  python bench.py (+ $BENCH_ARGS)                     -> OUTDIR/bench*.log
 #   prof[:STEPS]            rocprofv3 --kernel-trace --stats of bench.py (STEPS + 2 warm-up steps traced), per-step summary
 #                                                                               -> OUTDIR/prof/summary.md
+#   proftool:SCRIPT[:A,..]  rocprofv3 --kernel-trace --stats of python3 tools/SCRIPT A ..
+#                                                                               -> OUTDIR/proftool_N/kernel_stats.csv
 #   kbench:BIN[:A,B,..]     tools/kbench/bin/BIN A B ..                         -> OUTDIR/kbench.txt
 #                           (exit 3 = the bench's numerics check failed: recorded, not fatal)
 #   pmc:BIN[:A,B,..]        two PMC passes over a kbench binary (tools/kbench/pmc.sh)
@@ -61,6 +63,12 @@ for step in "$@"; do
       f=$(find "$O/prof" -name "*kernel_stats.csv" | head -1)
       python tools/prof_summary.py "$f" "$(( ${a1:-3} + 2 ))" > "$O/prof/summary.md" && cp "$f" "$O/prof/kernel_stats.csv"
       head -18 "$O/prof/summary.md" ;;
+    proftool)
+      d=$O/proftool_$n
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$d" -o run -- \
+        python3 "tools/$a1" "${args[@]}" > "$d.log" 2>&1 || fail "$step" $? "$d.log"
+      f=$(find "$d" -name "*kernel_stats.csv" | head -1)
+      cp "$f" "$d/kernel_stats.csv" && head -25 "$d/kernel_stats.csv" | cut -c1-200 ;;
     kbench)
       log=$O/kbench.txt
       echo "=== $a1 ${args[*]}" >> "$log"
