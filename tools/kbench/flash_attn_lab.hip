@@ -297,6 +297,11 @@ constexpr int FP = KF_FA_FWD_FP;
 // (measured and removed: ping-pong wave roles -- waves 4-7 taking each tile's barrier after their
 // S chain, 5-deep ring -- 2.31-2.36 vs 2.23-2.25 ms, profiles/fa_fwd_pingpong_ab.txt)
 constexpr int NSTF = NST;   // forward K+V ring depth
+// KF_FA_XPIPE=1: cross-tile pipelining in the forward -- the next tile's S chain MFMAs are issued
+// in the current tile's softmax (same wave), so the matrix pipe works while the VALU does exp/max
+#ifndef KF_FA_XPIPE
+#define KF_FA_XPIPE 0
+#endif
 // KF_FA_PKMUL=1: the forward's per-score scale multiply issued as packed pairs
 #ifndef KF_FA_PKMUL
 #define KF_FA_PKMUL 0
@@ -519,7 +524,171 @@ __global__ __launch_bounds__(512, 1) void flash_fwd_kernel(
       }
       };
   auto live_tile = [&](int j) { return live && (!CAUSAL || j * BK <= qmax_w); };
-
+#if KF_FA_XPIPE
+  // softmax + PV of tile j (sc) with tile j+1's S chain (nx) interleaved into it
+  auto fused = [&](int j, f32x16 (&sc)[2], f32x16 (&nx)[2]) {
+    const int k0 = j * BK;
+    const char* Vs = smem + (j % NSTF) * STG + TILE;
+    const u32 ln = lane_id_opaque(), lr_ = ln & 31;
+    const u32 a_t = (lds_addr(smem) + (u32)(((j + 1) % NSTF) * STG)) + lr_ * 256 + 16 * ((ln >> 5) ^ swz_x(lr_));
+    bf16x8 fk[FP + 1];
+    auto rdK = [&](auto ic) {
+      constexpr int i = decltype(ic)::value, kt = i & 1, ks = i >> 1;
+      fk[i % (FP + 1)] = rd_b128<8192 * kt>(a_t ^ (32 * ks));
+    };
+    auto sstep = [&](auto ic) {
+      constexpr int i = decltype(ic)::value, kt = i & 1, ks = i >> 1;
+      if constexpr (i + FP < 16) rdK(std::integral_constant<int, i + FP>());
+      lgkm_tie1<(i + FP < 16 ? FP : 15 - i)>(fk[i % (FP + 1)]);
+      nx[kt] = mfma32(fk[i % (FP + 1)], qf[ks], nx[kt]);
+    };
+#if KF_FA_XPIPE == 2
+    // half overlap: the kt = 0 chain (8 MFMAs) inside the softmax, kt = 1 after the PV
+    auto rdK0 = [&](int ks) { return rd_b128<0>(a_t ^ (32 * ks)); };
+    bf16x8 f0[2];
+    f0[0] = rdK0(0);
+    nx[0] = mfma32(ones, mref, f32x16{});
+    auto hstep = [&](auto ic) {
+      constexpr int ks = decltype(ic)::value;
+      if constexpr (ks + 1 < 8) f0[(ks + 1) & 1] = rdK0(ks + 1);
+      lgkm_tie1<(ks + 1 < 8 ? 1 : 0)>(f0[ks & 1]);
+      nx[0] = mfma32(f0[ks & 1], qf[ks], nx[0]);
+    };
+    static_for<0, 2>(hstep);
+#else
+    static_for<0, FP>([&](auto ic) { rdK(ic); });
+    nx[0] = mfma32(ones, mref, f32x16{});
+    nx[1] = mfma32(ones, mref, f32x16{});
+    static_for<0, 4>(sstep);
+#endif
+    if (CAUSAL && k0 + BK - 1 > qmin_w) {
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = k0 + 32 * kt + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          sc[kt][r] = key > q ? -INFINITY : sc[kt][r];
+        }
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sc[kt][r]);
+#if KF_FA_XPIPE == 2
+    static_for<2, 4>(hstep);
+#else
+    static_for<4, 8>(sstep);
+#endif
+    mx = xor32_max(mx);
+    if (__ballot(first || mx > thresh)) {
+      const float mnew = first ? bf16_round(mx) : bf16_round(m + fmaxf(mx, 0.f));
+      const float shift = first ? mnew : mnew - m;
+      const float alpha = first ? 0.f : __builtin_amdgcn_exp2f(-shift * sl);
+      lsum *= alpha;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          sc[kt][r] -= shift;
+          if (KF_FA_XPIPE != 2 || kt == 0) nx[kt][r] -= shift;    // the next chain started from the old reference
+        }
+      m = mnew;
+      first = false;
+      mref = fold_const(m, hh);
+    }
+    float rs = 0.f;
+    static_for<0, 32>([&](auto ec) {
+      constexpr int e = decltype(ec)::value, kt = e / 16, r = e % 16;
+      const float p = __builtin_amdgcn_exp2f(sc[kt][r] * sl);
+      sc[kt][r] = p;
+      rs += p;
+#if KF_FA_XPIPE == 2
+      if constexpr (e % 8 == 7) hstep(std::integral_constant<int, 4 + e / 8>());
+#else
+      if constexpr (e % 4 == 3) sstep(std::integral_constant<int, 8 + e / 4>());
+#endif
+    });
+    lsum += xor32_sum(rs);
+    bf16x8 pf[2][2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        u32x4 u;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) u[i] = pack2(sc[kt][8 * ss + 2 * i], sc[kt][8 * ss + 2 * i + 1]);
+        pf[kt][ss] = as_bf16x8(u);
+      }
+    const u32 vbase = lds_addr(Vs);
+    bf16x8 vf[2][4];
+    auto v_read = [&](int t, bf16x8* f) {
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          const int row = 32 * kt + 16 * ss + vrow, col = 32 * t + vcol;
+          f[2 * kt + ss] = tr_pair_asm(vbase + swz8(row, col), vbase + swz8(row + 8, col));
+        }
+    };
+    v_read(0, vf[0]);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      if (t < 3) {
+        v_read(t + 1, vf[(t + 1) & 1]);
+        lgkm_wait_tie<8>(vf[t & 1]);
+      } else {
+        lgkm_wait_tie<0>(vf[t & 1]);
+      }
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) o[t] = mfma32(vf[t & 1][2 * kt + ss], pf[kt][ss], o[t]);
+    }
+#if KF_FA_XPIPE == 2
+    {   // the kt = 1 chain of the next tile (folded reference: the current one)
+      bf16x8 f1[2];
+      auto rdK1 = [&](int ks) { return rd_b128<8192>(a_t ^ (32 * ks)); };
+      f1[0] = rdK1(0);
+      nx[1] = mfma32(ones, mref, f32x16{});
+      static_for<0, 8>([&](auto ic) {
+        constexpr int ks = decltype(ic)::value;
+        if constexpr (ks + 1 < 8) f1[(ks + 1) & 1] = rdK1(ks + 1);
+        lgkm_tie1<(ks + 1 < 8 ? 1 : 0)>(f1[ks & 1]);
+        nx[1] = mfma32(f1[ks & 1], qf[ks], nx[1]);
+      });
+    }
+#endif
+  };
+  // tile j: publish tile j+1 (all waves are past tile j-1, so its ring slot takes tile j+AH),
+  // then tile j's softmax + PV with tile j+1's S chain inside it
+  auto xstep = [&](int j, f32x16 (&cur)[2], f32x16 (&nxt)[2]) {
+    const bool nx_ = j + 1 < ntiles;
+    if (nx_) {
+      wait_stage(j + 1, min(j + AH - 1, ntiles - 1));
+      barrier();
+      if (j + AH < ntiles) stage(j + AH);
+    }
+    const bool lv = live_tile(j), lvn = nx_ && live_tile(j + 1);
+    // live tiles form a prefix (causal: j * BK <= qmax_w), so lvn implies lv.  A wave's last
+    // live tile runs the same body: its "next" chain reads whatever ring slot follows (LDS only)
+    // and is never consumed -- one code path keeps the register allocation spill-free
+    (void)lvn;
+    if (lv) fused(j, cur, nxt);
+  };
+  wait_stage(0, min(AH - 1, ntiles - 1));
+  barrier();
+  f32x16 sA[2], sB[2];
+  if (live_tile(0)) s_chain(0, sA);
+  for (int j = 0; j < ntiles; j += 2) {
+    xstep(j, sA, sB);
+    if (j + 1 < ntiles) xstep(j + 1, sB, sA);
+  }
+#else
   wait_stage(0, min(AH - 1, ntiles - 1));
   barrier();
   f32x16 scp[2];
@@ -533,6 +702,7 @@ __global__ __launch_bounds__(512, 1) void flash_fwd_kernel(
       barrier();
     }
   }
+#endif
   if (!live) return;
   const float inv = 1.f / lsum;
   bf16_t* op = out + ((long)b * S + q) * ldo + (long)h * D;
