@@ -365,14 +365,11 @@ __global__ __launch_bounds__(NT) void decode_fused_kernel(
   const int chunk = ((len + splits - 1) / splits + 15) & ~15;     // 16-key granules
   const int start = s * chunk, end = min(len, start + chunk);
 
-  float qf[G][8];
+  // q packed bf16 (scores are v_dot2 on bf16 pairs, fp32 sums; the log2-domain scale is
+  // applied to the reduced score)
+  u32x4 qb[G];
 #pragma unroll
-  for (int h = 0; h < G; ++h) {
-    const u32x4 v = ld16(q + (long)b * q_ld + (long)(hk * G + h) * D + sub * 8);
-    unpack8(v, qf[h]);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) qf[h][i] *= scale_log2;
-  }
+  for (int h = 0; h < G; ++h) qb[h] = ld16(q + (long)b * q_ld + (long)(hk * G + h) * D + sub * 8);
   const long kvbase = (long)slots[b] * slot_stride + (long)hk * head_stride;
   const bf16_t* kp = kc + kvbase;
   const bf16_t* vp = vc + kvbase;
@@ -388,31 +385,23 @@ __global__ __launch_bounds__(NT) void decode_fused_kernel(
   for (int r0 = start; r0 < end; r0 += KR) {
     const int j0 = r0 + grp, j1 = r0 + 16 + grp;
     const bool ok0 = j0 < end, ok1 = j1 < end;
-    const u32x4 zero = u32x4{0u, 0u, 0u, 0u};
-    const u32x4 k0 = ok0 ? ld16(kp + (long)j0 * D + sub * 8) : zero;
-    const u32x4 k1 = ok1 ? ld16(kp + (long)j1 * D + sub * 8) : zero;
-    const u32x4 v0 = ok0 ? ld16(vp + (long)j0 * D + sub * 8) : zero;
-    const u32x4 v1 = ok1 ? ld16(vp + (long)j1 * D + sub * 8) : zero;
-    float kf0[8], kf1[8], vf0[8], vf1[8];
-    unpack8(k0, kf0);
-    unpack8(k1, kf1);
+    // rows clamped into the chunk: every load is unconditional (no load under a branch), what
+    // lies past the chunk is masked in the arithmetic
+    const long o0 = (long)min(j0, end - 1) * D + sub * 8, o1 = (long)min(j1, end - 1) * D + sub * 8;
+    const u32x4 k0 = ld16(kp + o0), k1 = ld16(kp + o1), v0 = ld16(vp + o0), v1 = ld16(vp + o1);
+    float vf0[8], vf1[8];
     unpack8(v0, vf0);
     unpack8(v1, vf1);
 #pragma unroll
     for (int h = 0; h < G; ++h) {
-      float a0 = 0.f, a1 = 0.f;
+      float a0 = dot2_bf16(qb[h][0], k0[0], 0.f), a1 = dot2_bf16(qb[h][0], k1[0], 0.f);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        a0 = fmaf(qf[h][i], kf0[i], a0);
-        a1 = fmaf(qf[h][i], kf1[i], a1);
+      for (int c = 1; c < 4; ++c) {
+        a0 = dot2_bf16(qb[h][c], k0[c], a0);
+        a1 = dot2_bf16(qb[h][c], k1[c], a1);
       }
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) {
-        a0 += __shfl_xor(a0, o, 64);
-        a1 += __shfl_xor(a1, o, 64);
-      }
-      a0 = ok0 ? a0 : -INFINITY;
-      a1 = ok1 ? a1 : -INFINITY;
+      a0 = ok0 ? row16_sum(a0) * scale_log2 : -INFINITY;
+      a1 = ok1 ? row16_sum(a1) * scale_log2 : -INFINITY;
       const float mn = fmaxf(m[h], fmaxf(a0, a1));
       if (mn == -INFINITY) continue;              // no valid key yet for this stream
       const float al = exp2f(m[h] - mn), p0 = exp2f(a0 - mn), p1 = exp2f(a1 - mn);

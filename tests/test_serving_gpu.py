@@ -35,7 +35,9 @@ def _ref_decode(q2d, kc, vc, slots, lengths, Hq):
     # large batch: 2 splits (B * Hkv = 512) and 1 split (1024, normalised in the split kernel, no
     # combine); chunks longer than one 1024-key sub-chunk are merged online inside the workgroup
     (64, 32, 8, 4096, [4096, 1, 2048, 2049, 3071, 1025, 17, 4000] * 8),
-    (128, 32, 8, 3000, [3000, 1, 1024, 1025, 2049, 64, 2999, 700] * 16)])
+    (128, 32, 8, 3000, [3000, 1, 1024, 1025, 2049, 64, 2999, 700] * 16),
+    # the direct (one-split) path at the other GQA widths: G = 8 and G = 1, with sub-chunks
+    (128, 64, 8, 1500, [1500, 1030, 1, 999] * 32), (64, 8, 8, 2100, [2100, 2, 1024, 1025] * 16)])
 def test_decode_attn(B, Hq, Hkv, Lmax, lens):
     assert _ext.load()
     g = torch.Generator(device="cpu").manual_seed(B * 7 + Lmax)
