@@ -9,13 +9,21 @@
 // Split-K ("flash decoding"): grid (splits, Hkv, B), 256 threads.  One workgroup owns one
 // (row, kv head, key chunk) and serves all G = Hq/Hkv query heads of the group, so every
 // K/V byte is read exactly once.  A 16-lane quarter-wave owns one key row (16 lanes x 16 B);
-// a wave covers 4 keys per load, the block 16.
-//   phase 1: s[h][j] = q_h . k_j (fp32, log2 domain) -> LDS
-//   phase 2: per head max / exp2 / sum over the chunk (one wave per head)
-//   phase 3: o[h] += p[h][j] v_j with 16 independent key streams, reduced via LDS
-// Partial (o, m, l) per split go to an fp32 workspace; decode_combine merges the splits.
-// Decode is HBM-bound (2 flops/byte), so VALU dot products are the right tool: MFMA would
-// pad the G<=8 query rows to 16/32 and buy nothing.
+// a wave covers 4 keys per load, the block 16.  The chunk is walked in sub-chunks of up to
+// SUB keys (the LDS score rows), merged online, so the split count follows the batch
+// (kf_decode_splits: ~2 workgroups per CU), never the slot length Lmax:
+//   phase 1: s[h][j] = q_h . k_j: v_dot2 on packed bf16 pairs, the 16-lane row sum by DPP
+//            (four VALU ops; __shfl_xor compiled to a chain of ds_bpermute LDS round trips),
+//            lane h of the row stores head h's score -> LDS
+//   phase 2: per head max / exp2 / sum over the sub-chunk (one wave per head), merged with
+//            the running (max, sum); the padding past the sub-chunk becomes p = 0
+//   phase 3: o[h] += p[h][j] v_j with 16 independent key streams (no masking), reduced
+//            into LDS with the previous sub-chunks' rescaled sum
+// Partial (o, m, l) per split go to an fp32 workspace and decode_combine merges the splits;
+// with one split the workgroup normalises and writes the bf16 output itself (no combine).
+// Measured (tools/bench_decode_splits.py, 32-layer graph, ctx 1024): 6.1 TB/s at batch 64,
+// 5.7 TB/s at batch 128 (round 4: 4.2-4.3).  Decode is HBM-bound (2 flops/byte), so VALU dot
+// products are the right tool: MFMA would pad the G<=8 query rows to 16/32 and buy nothing.
 #include "common.h"
 
 using namespace kf;
