@@ -32,24 +32,36 @@ def _heartbeat():
             os.utime(hb, None)
 
 
-def _warm_device(index: int):
+def _warm_blas(index: int):
     """A fresh GPU process pays ~0.6 s of first-use costs before its first step can run: HIP
     runtime / device init (~0.2 s), hipBLASLt's first GEMM (library and kernel catalog, ~0.17 s),
     the HIP extension's code objects on its first launch (~0.19 s) -- tools/probe_first_use.py.
-    Paid here on a side thread while the main thread runs the rendezvous and builds the trainer
-    (everything it shares is lock-protected: torch's lazy CUDA init, ops/_ext.load).  Errors are
-    left for the main thread to hit and report."""
+    Paid on two side threads (this one: hipBLASLt; `_warm_ext`: the extension), concurrently
+    with each other and with the main thread's rendezvous and trainer construction (everything
+    they share is lock-protected: torch's lazy CUDA init, ops/_ext.load).  Errors are left for
+    the main thread to hit and report."""
     try:
         import torch
         torch.cuda.set_device(index)
         a = torch.zeros(128, 128, device=f"cuda:{index}", dtype=torch.bfloat16)
         torch.mm(a, a)
+        torch.cuda.synchronize(index)
+    except Exception:       # noqa: BLE001 -- the main thread reports real failures
+        pass
+
+
+def _warm_ext(index: int):
+    """The in-tree HIP extension: load the library and launch one kernel (see _warm_blas)."""
+    try:
+        import torch
+        torch.cuda.set_device(index)
         from ..ops import _ext
         if _ext.load():
             from .. import ops
+            a = torch.zeros(128, 128, device=f"cuda:{index}", dtype=torch.bfloat16)
             ops.rmsnorm_fwd(a, torch.ones(128, device=a.device, dtype=a.dtype), 1e-5)
-        torch.cuda.synchronize(index)
-    except Exception:       # noqa: BLE001 -- the main thread reports real failures
+            torch.cuda.synchronize(index)
+    except Exception:       # noqa: BLE001
         pass
 
 
@@ -89,13 +101,16 @@ def main(argv=None):
         dev = "cuda"
     else:
         dev = "cpu"
-    warm = None
+    warm = []
     if dev == "cuda" and os.environ.get("KFAMD_WARM", "1") != "0":
         import threading
         # the device init_distributed will select (not the raw LOCAL_RANK, which differs in the
         # several-ranks-per-GPU gloo rehearsal)
-        warm = threading.Thread(target=_warm_device, args=(local_device_index(),), name="kfamd-warm", daemon=True)
-        warm.start()
+        idx = local_device_index()
+        warm = [threading.Thread(target=f, args=(idx,), name=f"kfamd-{f.__name__[1:]}", daemon=True)
+                for f in (_warm_blas, _warm_ext)]
+        for t in warm:
+            t.start()
     st = init_distributed(tp=a.tp, pp=a.pp, device=dev)
     _event("dist_ready", seconds=time.time() - t_start)
     if a.model == "mnist":     # BASELINE configs[0]: operator/launcher plumbing job
@@ -123,8 +138,8 @@ def main(argv=None):
         from .checkpoint import load_checkpoint
         meta = load_checkpoint(a.resume, tr, data=data)
         _event("resumed", path=a.resume, step=int(meta["step"]))
-    if warm is not None:
-        warm.join()
+    for t in warm:
+        t.join()
     return _loop(a, tr, data, st, t_start)
 
 
