@@ -5,7 +5,8 @@
 // and stream them at 1.2-2.5 TB/s (profiles/serve_large_batch.md).  This kernel is laid out
 // for the stream:
 //
-//  * one workgroup = 64 W rows (4 waves x 16: the A operand of v_mfma_f32_16x16x32_bf16) x all
+//  * one workgroup = 64 WT W rows (4 waves x 16 WT, WT = 1, or 2 above 128 rows: the A operand
+//    of v_mfma_f32_16x16x32_bf16, every X fragment shared by the wave's WT tiles) x all
 //    M (X is the B operand, MT = M/16 padded to 4, 8, 12, 16 column tiles) x one K slice.
 //    K is split S ways (S chosen so the grid fills the CUs in one round); S > 1 writes fp32
 //    partials [S][M][N] that bgemm_reduce_kernel sums (and rounds, or SwiGLUs) in a second launch.
@@ -36,11 +37,18 @@ constexpr int BG_KQ = 256;             // K granularity (the deepest stage)
 // per MT: KS = 32-k MFMA steps per stage (a W row streams 64 KS contiguous bytes per stage:
 // HBM wants long runs per row -- 128 B runs streamed at ~3.8 TB/s), WD = ring depth (stages),
 // OCC = workgroups per CU.  X stage = 16 MT rows x 64 KS B.
-template <int MT> struct BgCfg;
-template <> struct BgCfg<4> { static constexpr int KS = 8, WD = 4, OCC = 1; };
-template <> struct BgCfg<8> { static constexpr int KS = 4, WD = 4, OCC = 1; };
-template <> struct BgCfg<12> { static constexpr int KS = 2, WD = 6, OCC = 1; };
-template <> struct BgCfg<16> { static constexpr int KS = 2, WD = 5, OCC = 1; };
+// WT = 16-row W tiles per wave: 2 shares every X fragment read from LDS between two W tiles
+// (half the LDS read traffic per weight byte; at M = 128 a one-tile wave reads 8 KB of X per
+// KB of W), at twice the W and accumulator registers.
+template <int MT, int WT> struct BgCfg;
+template <> struct BgCfg<4, 1> { static constexpr int KS = 8, WD = 4, OCC = 1; };
+template <> struct BgCfg<8, 1> { static constexpr int KS = 4, WD = 4, OCC = 1; };
+template <> struct BgCfg<12, 1> { static constexpr int KS = 2, WD = 6, OCC = 1; };
+template <> struct BgCfg<16, 1> { static constexpr int KS = 2, WD = 5, OCC = 1; };
+template <> struct BgCfg<4, 2> { static constexpr int KS = 4, WD = 4, OCC = 1; };
+template <> struct BgCfg<8, 2> { static constexpr int KS = 4, WD = 3, OCC = 1; };
+template <> struct BgCfg<12, 2> { static constexpr int KS = 2, WD = 4, OCC = 1; };
+template <> struct BgCfg<16, 2> { static constexpr int KS = 2, WD = 4, OCC = 1; };
 
 __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
@@ -85,16 +93,16 @@ __device__ __forceinline__ int xcd_remap(int bid, int total) {
 template <int KS>
 __device__ __forceinline__ int bg_swz(int row) { return KS == 2 ? (row >> 1) & 7 : row & 15; }
 
-template <int MT, bool SWIGLU>
-__global__ __launch_bounds__(64 * BG_WAVES, BgCfg<MT>::OCC) void bgemm_kernel(
+template <int MT, int WT, bool SWIGLU>
+__global__ __launch_bounds__(64 * BG_WAVES, (BgCfg<MT, WT>::OCC)) void bgemm_kernel(
     const bf16_t* __restrict__ x, long ldx, int M, const bf16_t* __restrict__ w, long ldw, int kslice, int S,
     int NB, bf16_t* __restrict__ y, long ldy, float* __restrict__ part, int NP, int up_off) {
-  constexpr int WD = BgCfg<MT>::WD, KS = BgCfg<MT>::KS;
+  constexpr int WD = BgCfg<MT, WT>::WD, KS = BgCfg<MT, WT>::KS;
   constexpr int BK = 32 * KS, ROWB = 2 * BK;        // k and X row bytes per stage
   constexpr int XST = 16 * MT * ROWB;               // bytes per X stage
   constexpr int RPI = 1024 / ROWB, LPR = 64 / RPI;  // X rows per DMA wave-instruction, lanes per row
   constexpr int XPW = XST / 1024 / BG_WAVES;        // X DMA wave-instructions per wave per stage
-  constexpr int C = XPW + KS;                       // VMEM instructions per wave per stage
+  constexpr int C = XPW + KS * WT;                  // VMEM instructions per wave per stage
   static_assert((WD - 2) * C <= 63, "vmcnt range");
   __shared__ __attribute__((aligned(16))) char smem[WD * XST];
 
@@ -103,10 +111,10 @@ __global__ __launch_bounds__(64 * BG_WAVES, BgCfg<MT>::OCC) void bgemm_kernel(
   const int s = lid % S, nb = lid / S;
   const int kb = s * kslice, nst = kslice / BK;
 
-  // this wave's 16 W rows (SwiGLU: waves 0-1 gate rows, waves 2-3 the matching up rows)
-  const int wrow0 = SWIGLU ? (wave < 2 ? nb * 32 + 16 * wave : nb * 32 + 16 * (wave - 2) + up_off)
-                           : nb * BG_BN + 16 * wave;
-  const bf16_t* wp = w + (long)(wrow0 + (l & 15)) * ldw + kb + 8 * (l >> 4);
+  // this wave's 16 WT W rows (SwiGLU: waves 0-1 gate rows, waves 2-3 the matching up rows)
+  const int wrow0 = SWIGLU ? (wave < 2 ? nb * 32 * WT + 16 * WT * wave : nb * 32 * WT + 16 * WT * (wave - 2) + up_off)
+                           : nb * BG_BN * WT + 16 * WT * wave;
+  const bf16_t* wp = w + (long)(wrow0 + (l & 15)) * ldw + kb + 8 * (l >> 4);   // tile t: + 16 t rows
   // X DMA: wave-instruction i (= wave + 4 t) fills rows RPI i ..; lane l -> row RPI i + l / LPR,
   // physical chunk l % LPR, i.e. logical chunk (l % LPR) ^ swz(row); rows >= M read row M-1
   const bf16_t* xp[XPW];
@@ -117,7 +125,7 @@ __global__ __launch_bounds__(64 * BG_WAVES, BgCfg<MT>::OCC) void bgemm_kernel(
   }
   char* const xdst = smem + 1024 * wave;            // + slot * XST + 4096 t
 
-  u32x4 wv[WD][KS];
+  u32x4 wv[WD][KS][WT];
   // Stage j's X DMA then its W loads, into ring slot SL (a compile-time register index).  Every
   // step issues exactly C instructions -- stages past the slice re-read L2-resident X rows into
   // a dead slot -- so one constant vmcnt per step is exact.
@@ -127,14 +135,19 @@ __global__ __launch_bounds__(64 * BG_WAVES, BgCfg<MT>::OCC) void bgemm_kernel(
     const bool live = j < nst;
 #pragma unroll
     for (int t = 0; t < XPW; ++t) glds16(live ? xp[t] + BK * j : xp[t], xdst + SL * XST + 4096 * t);
-    const bf16_t* src = live ? wp + BK * j : wdummy;
 #pragma unroll
-    for (int q = 0; q < KS; ++q) wv[SL][q] = gload16_nt(src + 32 * q);
+    for (int t = 0; t < WT; ++t) {
+      const bf16_t* src = live ? wp + (long)16 * t * ldw + BK * j : wdummy;
+#pragma unroll
+      for (int q = 0; q < KS; ++q) wv[SL][q][t] = gload16_nt(src + 32 * q);
+    }
   };
 
-  f32x4 acc[MT];
+  f32x4 acc[WT][MT];
 #pragma unroll
-  for (int m = 0; m < MT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < WT; ++t)
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[t][m] = f32x4{0.f, 0.f, 0.f, 0.f};
   // lane's X fragment address in a stage: row 16 m + (l & 15), logical chunk 4 ks + (l >> 4)
   const int xr = l & 15;
   const u32 xrd = lds_u32(smem) + xr * ROWB;
@@ -167,7 +180,9 @@ __global__ __launch_bounds__(64 * BG_WAVES, BgCfg<MT>::OCC) void bgemm_kernel(
     // (a dead step) frees the register while the load is still in flight, and a value placed
     // there meanwhile is overwritten when the load lands.
 #pragma unroll
-    for (int q = 0; q < KS; ++q) asm volatile("" : "+v"(wv[U][q]));
+    for (int q = 0; q < KS; ++q)
+#pragma unroll
+      for (int t = 0; t < WT; ++t) asm volatile("" : "+v"(wv[U][q][t]));
     if (j >= nst) return;                           // a dead step of the last revolution
     const u32 base = xrd + U * XST;
     bf16x8 xf[2][4];
@@ -188,9 +203,12 @@ __global__ __launch_bounds__(64 * BG_WAVES, BgCfg<MT>::OCC) void bgemm_kernel(
         lgkm_wait4<0>(xf[g & 1]);
       }
       const int ks = g / (MT / 4), m0 = 4 * (g % (MT / 4));
-      const bf16x8 a = __builtin_bit_cast(bf16x8, wv[U][ks]);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) acc[m0 + i] = mfma16(a, xf[g & 1][i], acc[m0 + i]);
+      for (int t = 0; t < WT; ++t) {
+        const bf16x8 a = __builtin_bit_cast(bf16x8, wv[U][ks][t]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[t][m0 + i] = mfma16(a, xf[g & 1][i], acc[t][m0 + i]);
+      }
     }
   };
   // whole ring revolutions; the last one's steps past nst only keep the load count uniform
@@ -208,50 +226,61 @@ __global__ __launch_bounds__(64 * BG_WAVES, BgCfg<MT>::OCC) void bgemm_kernel(
 #pragma unroll
   for (int u = 0; u < WD; ++u)                      // ... and only then release their registers
 #pragma unroll
-    for (int q = 0; q < KS; ++q) asm volatile("" : "+v"(wv[u][q]));
+    for (int q = 0; q < KS; ++q)
+#pragma unroll
+      for (int t = 0; t < WT; ++t) asm volatile("" : "+v"(wv[u][q][t]));
 
-  // acc[m]: lane l, reg r -> W row (n) 4 (l >> 4) + r of this wave's 16, X row (m) 16 m + (l & 15)
+  // acc[t][m]: lane l, reg r -> W row (n) 16 t + 4 (l >> 4) + r of this wave's 16 WT, X row (m)
+  // 16 m + (l & 15)
   const int nr = 4 * (l >> 4);
   if constexpr (SWIGLU) {
     // waves 2-3 hand their up-row sums to waves 0-1 through LDS (the ring is idle now)
     __syncthreads();
-    float* up = reinterpret_cast<float*>(smem);     // [2 waves][MT][64 lanes][4]
+    float* up = reinterpret_cast<float*>(smem);     // [2 waves][WT][MT][64 lanes][4]
     if (wave >= 2) {
 #pragma unroll
-      for (int m = 0; m < MT; ++m)
-        *reinterpret_cast<f32x4*>(up + (((wave - 2) * MT + m) * 64 + l) * 4) = acc[m];
+      for (int t = 0; t < WT; ++t)
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+          *reinterpret_cast<f32x4*>(up + ((((wave - 2) * WT + t) * MT + m) * 64 + l) * 4) = acc[t][m];
     }
     __syncthreads();
     if (wave >= 2) return;
-    const int col0 = nb * 32 + 16 * wave + nr;      // output column of reg 0
 #pragma unroll
-    for (int m = 0; m < MT; ++m) {
-      const int row = 16 * m + (l & 15);
-      const f32x4 u = *reinterpret_cast<const f32x4*>(up + ((wave * MT + m) * 64 + l) * 4);
-      if (S == 1) {
-        if (row < M) {
-          float o[4];
+    for (int t = 0; t < WT; ++t) {
+      const int col0 = nb * 32 * WT + 16 * (WT * wave + t) + nr;   // output (gate) column of reg 0
 #pragma unroll
-          for (int r = 0; r < 4; ++r) o[r] = acc[m][r] * sigmoidf_(acc[m][r]) * u[r];
-          *reinterpret_cast<u32x2*>(y + (long)row * ldy + col0) = u32x2{pack2(o[0], o[1]), pack2(o[2], o[3])};
+      for (int m = 0; m < MT; ++m) {
+        const int row = 16 * m + (l & 15);
+        const f32x4 u = *reinterpret_cast<const f32x4*>(up + (((wave * WT + t) * MT + m) * 64 + l) * 4);
+        if (S == 1) {
+          if (row < M) {
+            float o[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = acc[t][m][r] * sigmoidf_(acc[t][m][r]) * u[r];
+            *reinterpret_cast<u32x2*>(y + (long)row * ldy + col0) = u32x2{pack2(o[0], o[1]), pack2(o[2], o[3])};
+          }
+        } else if (row < M) {   // partials in 64-wide [32 gate | 32 up] blocks (bgemm_reduce_kernel)
+          float* p = part + ((long)s * M + row) * NP + (col0 / 32) * 64 + col0 % 32;
+          *reinterpret_cast<f32x4*>(p) = acc[t][m];
+          *reinterpret_cast<f32x4*>(p + 32) = u;
         }
-      } else if (row < M) {   // partials: gate at block column c, up at c + 32 of a 64-wide block
-        float* p = part + ((long)s * M + row) * NP + nb * 64 + 16 * wave + nr;
-        *reinterpret_cast<f32x4*>(p) = acc[m];
-        *reinterpret_cast<f32x4*>(p + 32) = u;
       }
     }
   } else {
-    const int col0 = nb * BG_BN + 16 * wave + nr;
 #pragma unroll
-    for (int m = 0; m < MT; ++m) {
-      const int row = 16 * m + (l & 15);
-      if (row >= M) continue;
-      if (S == 1) {
-        *reinterpret_cast<u32x2*>(y + (long)row * ldy + col0) =
-            u32x2{pack2(acc[m][0], acc[m][1]), pack2(acc[m][2], acc[m][3])};
-      } else {
-        *reinterpret_cast<f32x4*>(part + ((long)s * M + row) * NP + col0) = acc[m];
+    for (int t = 0; t < WT; ++t) {
+      const int col0 = nb * BG_BN * WT + 16 * (WT * wave + t) + nr;
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const int row = 16 * m + (l & 15);
+        if (row >= M) continue;
+        if (S == 1) {
+          *reinterpret_cast<u32x2*>(y + (long)row * ldy + col0) =
+              u32x2{pack2(acc[t][m][0], acc[t][m][1]), pack2(acc[t][m][2], acc[t][m][3])};
+        } else {
+          *reinterpret_cast<f32x4*>(part + ((long)s * M + row) * NP + col0) = acc[t][m];
+        }
       }
     }
   }
@@ -285,30 +314,45 @@ __global__ __launch_bounds__(256) void bgemm_reduce_kernel(const float* __restri
   }
 }
 
-template <int MT, bool SWIGLU>
+template <int MT, int WT, bool SWIGLU>
 void bg_launch(int grid, hipStream_t st, const bf16_t* x, long ldx, int M, const bf16_t* w, long ldw, int kslice,
                int S, int NB, bf16_t* y, long ldy, float* part, int NP, int up_off) {
-  hipLaunchKernelGGL((bgemm_kernel<MT, SWIGLU>), dim3(grid), dim3(64 * BG_WAVES), 0, st, x, ldx, M, w, ldw, kslice,
-                     S, NB, y, ldy, part, NP, up_off);
+  hipLaunchKernelGGL((bgemm_kernel<MT, WT, SWIGLU>), dim3(grid), dim3(64 * BG_WAVES), 0, st, x, ldx, M, w, ldw,
+                     kslice, S, NB, y, ldy, part, NP, up_off);
 }
 
 int bg_mt(int M) { return M <= 64 ? 4 : M <= 128 ? 8 : M <= 192 ? 12 : 16; }
 
 }  // namespace
 
+// W tiles per wave for an (M, N, K) problem; N must split into 64 WT-row blocks.  Two tiles above
+// 128 rows, where the X reads dominate: wd 59.4 -> 53.1 us and wqkv 37.9 -> 33.7 us at 256 rows;
+// at 64-128 rows the doubled registers cost more than the halved LDS reads (wo at 128 rows
+// 19.8 -> 25.2 us; profiles/serve_bgemm_wt_r5.md).  KFAMD_BGEMM_WT = 1 / 2 overrides (A/Bs).
+extern "C" int kf_bgemm_wt(int M, int N, int K) {
+  static const int force = [] {
+    const char* e = std::getenv("KFAMD_BGEMM_WT");
+    return e ? std::atoi(e) : 0;
+  }();
+  const int wt = force == 1 || force == 2 ? force : (M > 128 ? 2 : 1);
+  return N % (BG_BN * wt) == 0 ? wt : 1;
+}
+
 // K split for an (M, N, K) problem: enough workgroups for one full round of the CUs, K slices a
 // whole number of 64-k stages.  KFAMD_BGEMM_SPLIT overrides (tools/bench_bgemm.py sweeps).
-// N = rows of W (SwiGLU: gate + up), so the grid has N / 64 column blocks either way.
+// N = rows of W (SwiGLU: gate + up), so the grid has N / (64 WT) column blocks either way.
 extern "C" int kf_bgemm_splits(int M, int N, int K) {
   static const int force = [] {
     const char* e = std::getenv("KFAMD_BGEMM_SPLIT");
     return e ? std::atoi(e) : 0;
   }();
-  const int NB = N / BG_BN;
+  const int wt = kf_bgemm_wt(M, N, K);
+  const int NB = N / (BG_BN * wt);
   const int stages = K / BG_KQ;
   if (force > 0) return (stages % force == 0) ? force : 1;
-  int S = 1;   // one workgroup per CU: fill the 256 CUs, slices of >= 4 256-k quanta
-  while (S < 8 && NB * S * 2 <= 256 && stages % (S * 2) == 0 && stages / (S * 2) >= 4) S *= 2;
+  int S = 1;   // one workgroup per CU: fill the 256 CUs, slices of >= 4 (WT 2: 2) 256-k quanta
+  const int min_q = wt == 2 ? 2 : 4;
+  while (S < 8 && NB * S * 2 <= 256 && stages % (S * 2) == 0 && stages / (S * 2) >= min_q) S *= 2;
   return S;
 }
 
@@ -319,18 +363,24 @@ extern "C" int kf_bgemm(const void* x, long ldx, int M, const void* w, int N, in
                         int up_off, int S, float* part, hipStream_t st) {
   if (M < 1 || M > 256 || K % BG_KQ || ldx % 8 || ldy % 4 || S < 1 || (K / BG_KQ) % S) return 1;
   if ((((uintptr_t)x) | ((uintptr_t)w)) & 15 || ((uintptr_t)y) & 7) return 1;
-  if (swiglu ? (up_off % 32 || N != 2 * up_off) : N % BG_BN) return 1;
+  const int wt = kf_bgemm_wt(M, N, K);
+  if (swiglu ? (up_off % (32 * wt) || N != 2 * up_off) : N % (BG_BN * wt)) return 1;
   if (S > 1 && !part) return 1;
-  const int NB = swiglu ? up_off / 32 : N / BG_BN, NP = swiglu ? 2 * up_off : N;
+  const int NB = swiglu ? up_off / (32 * wt) : N / (BG_BN * wt), NP = swiglu ? 2 * up_off : N;
   const int kslice = K / S, grid = NB * S;
   auto X = (const bf16_t*)x;
   auto W = (const bf16_t*)w;
   auto Y = (bf16_t*)y;
   const int mt = bg_mt(M);
-#define BG_CASE(MTV)                                                                                         \
-  case MTV:                                                                                                  \
-    if (swiglu) bg_launch<MTV, true>(grid, st, X, ldx, M, W, (long)K, kslice, S, NB, Y, ldy, part, NP, up_off); \
-    else bg_launch<MTV, false>(grid, st, X, ldx, M, W, (long)K, kslice, S, NB, Y, ldy, part, NP, 0);         \
+#define BG_CASE(MTV)                                                                                           \
+  case MTV:                                                                                                    \
+    if (wt == 2) {                                                                                             \
+      if (swiglu) bg_launch<MTV, 2, true>(grid, st, X, ldx, M, W, (long)K, kslice, S, NB, Y, ldy, part, NP, up_off); \
+      else bg_launch<MTV, 2, false>(grid, st, X, ldx, M, W, (long)K, kslice, S, NB, Y, ldy, part, NP, 0);       \
+    } else {                                                                                                   \
+      if (swiglu) bg_launch<MTV, 1, true>(grid, st, X, ldx, M, W, (long)K, kslice, S, NB, Y, ldy, part, NP, up_off); \
+      else bg_launch<MTV, 1, false>(grid, st, X, ldx, M, W, (long)K, kslice, S, NB, Y, ldy, part, NP, 0);       \
+    }                                                                                                          \
     break;
   switch (mt) {
     BG_CASE(4)

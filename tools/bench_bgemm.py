@@ -15,7 +15,7 @@ import torch  # noqa: E402
 
 from service_account_auth_improvements_amd import ops  # noqa: E402
 
-MS = [int(m) for m in (sys.argv[1] if len(sys.argv) > 1 else "32,64,128,256").split(",")]
+MS = [int(m) for a in (sys.argv[1:] or ["32,64,128,256"]) for m in a.split(",")]
 SHAPES = {"wqkv": (6144, 4096, False), "wo": (4096, 4096, False), "wd": (4096, 14336, False),
           "wgu": (28672, 4096, True), "lm_head": (128256, 4096, False)}
 
