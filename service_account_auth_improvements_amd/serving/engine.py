@@ -273,10 +273,13 @@ class Engine:
         return tp_all_reduce(x, self.m.st)
 
     def _use_bgemm(self, x, w) -> bool:
-        # measured at TP=1 (a TP shard's K of 512-1792 leaves too few K stages to split)
-        return (BGEMM and self.m.tp == 1 and max(SKINNY_MAX_ROWS + 1, BGEMM_MIN_ROWS) <= x.shape[0] <= BGEMM_MAX_ROWS
-                and w.shape[0] <= BGEMM_MAX_N
-                and ops.bgemm_ok(x, w))
+        # measured at TP=1 (a TP shard's K of 512-1792 leaves too few K stages to split); above
+        # BGEMM_MAX_ROWS only the deep narrow projection (wd, K = 14336) gains, with two W tiles
+        # per wave: 53 vs 62 us at 256 rows (wo loses: 28 vs 24; profiles/serve_bgemm_wt_r5.md)
+        rows = x.shape[0]
+        in_range = (max(SKINNY_MAX_ROWS + 1, BGEMM_MIN_ROWS) <= rows <= BGEMM_MAX_ROWS
+                    or (BGEMM_MAX_ROWS < rows <= 256 and w.shape[1] >= 8192))
+        return BGEMM and self.m.tp == 1 and in_range and w.shape[0] <= BGEMM_MAX_N and ops.bgemm_ok(x, w)
 
     def _mm(self, x, w):
         """Decode GEMM: the skinny weight-streaming kernels for small batches on the GPU, the
