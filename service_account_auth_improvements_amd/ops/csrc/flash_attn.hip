@@ -32,6 +32,12 @@
 //    sums are transposed through LDS and added row-contiguously in fp32.
 //  * The two kernels run concurrently: dQ on the caller's stream, the accumulator memset and
 //    dK/dV on a per-device side stream (event fork/join, see kf_flash_bwd).
+// Measured alternatives (round 5, profiles/fa_dkdv2_r5.md, profiles/dq_atomic_r5.md): a one-wave-
+// per-SIMD dK/dV with 64-row iterations and the next S/dP chain under the softmax (15 % slower),
+// a fused dK/dV + dQ (its fp32 dQ atomics alone take 6.7 ms per layer at B4 S8192, more than
+// this whole backward), the forward's next-tile S chain under the current softmax (2 % slower),
+// and one stream for both backward kernels (same step time).  The matrix pipe is 50-60 % busy
+// in all three kernels (PMC, same file).
 #include "common.h"
 
 #include <mutex>
