@@ -106,6 +106,17 @@ class _Done:
         return True
 
 
+def two_shot_blocks(requested: Optional[int], sharing: int, cus: int) -> int:
+    """Workgroups per two-shot call: ``requested`` as given (capped to TwoShot.MAX_BLOCKS), else
+    the measured default, capped when ``sharing`` ranks drive the same GPU so that their spinning
+    calls leave half of its ``cus`` compute units to the peers' other kernels."""
+    if requested is None:
+        requested = TwoShot.DEFAULT_BLOCKS
+        if sharing > 1:
+            requested = min(requested, max(1, cus // (2 * sharing)))
+    return max(1, min(int(requested), TwoShot.MAX_BLOCKS))
+
+
 class TwoShot:
     """Two-shot reduce-scatter / all-gather / all-reduce over xGMI (ops/csrc/custom_ar.hip, ts).
 
@@ -164,11 +175,7 @@ class TwoShot:
         # whole CU's LDS) until the wait budget runs out.  The automatic count is then capped
         # to leave half the CUs free; one rank per GPU (production) keeps the measured 128.
         sharing = sum(1 for g in gathered if g[1] == dev_key)
-        if blocks is None:
-            blocks = self.DEFAULT_BLOCKS
-            if sharing > 1:
-                blocks = min(blocks, max(1, props.multi_processor_count // (2 * sharing)))
-        self.blocks = max(1, min(int(blocks), self.MAX_BLOCKS))
+        self.blocks = two_shot_blocks(blocks, sharing, props.multi_processor_count)
         self.ptrs, self._opened = [], []
         for r, h in enumerate(handles):
             if r == self.rank:

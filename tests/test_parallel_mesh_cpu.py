@@ -298,3 +298,15 @@ def test_make_tp_comm_rejects_unknown_backends():
     with pytest.raises(ValueError):
         make_tp_comm("nvls", ParallelState(tp=2))
     assert make_tp_comm("twoshot", ParallelState(tp=1)) is None
+
+
+def test_two_shot_block_count():
+    """TwoShot's workgroup count: the measured 128 for one rank per GPU, an explicit request
+    as given (capped to MAX_BLOCKS), and for ranks sharing one GPU half the CUs split among them
+    (profiles/two_shot_blocks_r5.md; the shared-GPU TP tests rely on it)."""
+    from service_account_auth_improvements_amd.parallel.custom_ar import TwoShot, two_shot_blocks
+    assert two_shot_blocks(None, 1, 256) == TwoShot.DEFAULT_BLOCKS == 128
+    assert two_shot_blocks(None, 4, 256) == 32 and two_shot_blocks(None, 8, 256) == 16
+    assert two_shot_blocks(None, 2, 256) == 64
+    assert two_shot_blocks(64, 4, 256) == 64 and two_shot_blocks(1000, 1, 256) == TwoShot.MAX_BLOCKS
+    assert two_shot_blocks(None, 1024, 256) == 1
