@@ -26,6 +26,27 @@ sys.path.insert(0, ROOT)
 NS = "kf-conformance"
 
 
+def free_port_pair() -> int:
+    """A port p with p and p + 1 both free (the job's MASTER_PORT and the launcher's rendezvous
+    port): fixed ports collided with other jobs on a shared host, e.g. tests run in parallel."""
+    import socket
+    while True:
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        p = s.getsockname()[1]
+        s.close()
+        if p >= 65000:
+            continue
+        t = socket.socket()
+        try:
+            t.bind(("127.0.0.1", p + 1))
+            return p
+        except OSError:
+            continue
+        finally:
+            t.close()
+
+
 def wait(fn, timeout):
     from service_account_auth_improvements_amd.controlplane.apiserver import ApiError
     end = time.time() + timeout
@@ -88,13 +109,13 @@ def main(argv=None):
         cmd = [sys.executable, "-m", "service_account_auth_improvements_amd", "train", "--model", "mnist",
                "--micro-batch", "32", "--steps", "20", "--device", "cpu"]
         job = training.pytorchjob_manifest("mnist-conformance", NS, "kfamd/trainer-rocm:latest", cmd, n_nodes=2,
-                                           gpus_per_node=0, master_port=29811)
+                                           gpus_per_node=0, master_port=free_port_pair())
         job["spec"]["nprocPerNode"] = "1"
         c.create(job)
         res = wait(lambda: job_done(c, "mnist-conformance"), a.timeout)
         check("training: PyTorchJob 2-replica MNIST (gloo)", res == "Succeeded", f"result={res}")
         mj = training.mpijob_manifest("mnist-mpi-conformance", NS, "kfamd/trainer-rocm:latest", cmd, workers=2,
-                                      gpus_per_worker=0, master_port=29821)
+                                      gpus_per_worker=0, master_port=free_port_pair())
         c.create(mj)
         res = wait(lambda: job_done(c, "mnist-mpi-conformance", training.MPI_API, "MPIJob"), a.timeout)
         check("training: MPIJob mpirun -np 2 MNIST (gloo)", res == "Succeeded", f"result={res}")
@@ -102,7 +123,7 @@ def main(argv=None):
             cmd = [sys.executable, "-m", "service_account_auth_improvements_amd", "train", "--model", "llama3-8b",
                    "--seq-len", "2048", "--steps", "2", "--device", "cuda"]
             c.create(training.pytorchjob_manifest("llama-conformance", NS, "kfamd/trainer-rocm:latest", cmd,
-                                                  n_nodes=1, gpus_per_node=1, master_port=29831))
+                                                  n_nodes=1, gpus_per_node=1, master_port=free_port_pair()))
             res = wait(lambda: job_done(c, "llama-conformance"), a.timeout)
             check("training: PyTorchJob Llama-3-8B on MI355X", res == "Succeeded", f"result={res}")
         c.delete("kubeflow.org/v1", "Profile", NS)
