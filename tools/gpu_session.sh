@@ -12,6 +12,8 @@
 #                                                                               -> OUTDIR/prof/summary.md
 #   proftool:SCRIPT[:A,..]  rocprofv3 --kernel-trace --stats of python3 tools/SCRIPT A ..
 #                                                                               -> OUTDIR/proftool_N/kernel_stats.csv
+#   pmctool:SCRIPT[:A,..]   the two PMC passes of tools/kbench/pmc.sh over python3 tools/SCRIPT A ..
+#                                                                               -> OUTDIR/pmctool_N/
 #   kbench:BIN[:A,B,..]     tools/kbench/bin/BIN A B ..                         -> OUTDIR/kbench.txt
 #                           (exit 3 = the bench's numerics check failed: recorded, not fatal)
 #   pmc:BIN[:A,B,..]        two PMC passes over a kbench binary (tools/kbench/pmc.sh)
@@ -69,6 +71,17 @@ for step in "$@"; do
         python3 "tools/$a1" "${args[@]}" > "$d.log" 2>&1 || fail "$step" $? "$d.log"
       f=$(find "$d" -name "*kernel_stats.csv" | head -1)
       cp "$f" "$d/kernel_stats.csv" && head -25 "$d/kernel_stats.csv" | cut -c1-200 ;;
+    pmctool)
+      # the two counter passes of tools/kbench/pmc.sh over python3 tools/SCRIPT (no trace domains)
+      d=$O/pmctool_$n
+      mkdir -p "$d"
+      timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_LDS \
+        SQ_LDS_BANK_CONFLICT SQ_WAIT_ANY SQ_INSTS_SALU --output-format csv -d "$d" -o p1 -- \
+        python3 "tools/$a1" "${args[@]}" > "$d/p1.log" 2>&1 || fail "$step" $? "$d/p1.log"
+      timeout -s KILL 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_BF16 GRBM_GUI_ACTIVE \
+        SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_MISC SQ_WAIT_INST_ANY \
+        --output-format csv -d "$d" -o p2 -- python3 "tools/$a1" "${args[@]}" > "$d/p2.log" 2>&1 || fail "$step" $? "$d/p2.log"
+      find "$d" -name "*counter_collection.csv" ;;
     kbench)
       log=$O/kbench.txt
       echo "=== $a1 ${args[*]}" >> "$log"
