@@ -327,6 +327,48 @@ def test_bgemm_decode_shapes_and_strided_rows():
         assert err < 1e-2, (N, K, err)
 
 
+def test_bgemm_split_launches_are_bitwise_stable_and_replay_in_graphs():
+    """Split-K batched-decode GEMMs (fp32 partials + the reduce launch): interleaved launches of
+    different shapes and splits give bitwise the first result of each, and a captured graph
+    replays it."""
+    from service_account_auth_improvements_amd import ops
+    g = torch.Generator(device="cpu").manual_seed(11)
+    cases = [(128, 4096, 4096, False), (64, 2048, 8192, False), (128, 1024, 2048, True), (200, 4096, 14336, False)]
+    data = []
+    for M, N, K, sw in cases:
+        x = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+        w = (torch.randn(N, K, generator=g) * 0.02).to(DEV, torch.bfloat16)
+        ref = torch.mm(x.float(), w.float().t())
+        if sw:
+            ref = torch.nn.functional.silu(ref[:, :N // 2]) * ref[:, N // 2:]
+        data.append((x, w, sw, ref))
+    first = {}
+    for rnd in range(6):
+        for ci, (x, w, sw, ref) in enumerate(data):
+            for S in (0, 2, 4):
+                y = ops.bgemm(x, w, swiglu=sw, splits=S)
+                if rnd == 0:
+                    err = ((y.float() - ref).abs().max() / ref.abs().max()).item()
+                    assert err < 1e-2, (ci, S, err)
+                    first[ci, S] = y
+                else:
+                    assert torch.equal(y, first[ci, S]), (rnd, ci, S)
+    x, w, sw, _ = data[0]
+    s = torch.cuda.Stream(device=DEV)
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        ops.bgemm(x, w, splits=4)
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        out = ops.bgemm(x, w, splits=4)
+    for _ in range(5):
+        out.zero_()
+        graph.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, first[0, 4])
+
+
 def _llama8b_engine(n_layers, use_graphs, max_len=4096):
     from service_account_auth_improvements_amd.serving.engine import build_engine
     return build_engine("llama3-8b", device=DEV, n_slots=4, max_len=max_len, n_layers=n_layers, use_graphs=use_graphs,
