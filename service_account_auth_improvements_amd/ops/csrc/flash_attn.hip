@@ -20,7 +20,7 @@
 //    kv-head), so its K/V (fwd, dQ) or Q/dO (dK/dV) stay in that XCD's 4 MB L2; causal
 //    work is launched heaviest-first.
 //
-// Forward: 1 workgroup = 8 waves x 32 query rows, 64-key tiles in a 4-deep LDS-DMA ring,
+// Forward: 1 workgroup = 8 waves x 32 query rows, 128-key tiles in a 2-deep LDS-DMA ring,
 // online softmax (exp2) with the running max folded into the MFMA chain (see the kernel).
 // Backward, two kernels, no dQ atomics:
 //  * dQ kernel (forward-shaped, per 128 query rows): S^T, dP^T = V.dO^T, P^T, dS^T,
@@ -53,7 +53,7 @@ typedef __attribute__((ext_vector_type(4))) float f4;
 namespace fa {
 constexpr int D = 128;
 constexpr int BQ = 128;           // sequence-length granule the launchers require (S % BQ == 0)
-constexpr int BK = 64;            // keys per tile (forward / dQ)
+constexpr int BK = 64;            // keys per tile of the dQ kernel (the forward: BKF = 128)
 constexpr int TILE = BK * D * 2;  // 16 KB
 constexpr int BKV = 128;          // keys per dK/dV workgroup (4 waves x 32)
 constexpr int QT = 32;            // query rows per dK/dV iteration
@@ -241,21 +241,22 @@ __device__ __forceinline__ bf16x8 fold_const(float c, int hh) {
 // Forward
 // ====================================================================================
 // 1 workgroup = 8 waves x 32 query rows (256 rows), one workgroup per CU (2 waves per SIMD).
-//  * K/V 64-key tiles arrive by LDS-DMA in a 4-deep ring of K+V stages (128 KB): the DMA
-//    runs three tiles ahead and each tile is published by a COUNTED vmcnt + raw s_barrier
-//    (a __syncthreads() would drain every stage in flight).  Each staged tile feeds 8 waves.
+//  * K/V 128-key tiles arrive by LDS-DMA in a 2-deep ring of K+V stages (2 x 64 KB): the DMA
+//    runs one tile ahead, and each tile is published by a vmcnt + raw s_barrier.  Each staged
+//    tile feeds 8 waves.  128-key tiles measured 4.6 % faster than 64-key tiles in a 4-deep
+//    ring (2.14 vs 2.24 ms at B4 S8192, same numerics): one barrier, one max / sum exchange and
+//    one threshold ballot per 128 keys (profiles/fa_fwd128_r5.md).
 //  * The loop is VALU-issue bound (two waves share a SIMD's vector issue; an MFMA holds it
-//    for 8 of its 32 cycles), so the softmax is put on a diet: Q is pre-scaled by
-//    scale*log2(e) once, and the running row max m (bf16-exact) rides in the S^T MFMA
-//    chain as a folded row constant, so p = exp2(S') costs one v_exp and no FMA.  m only
-//    moves (rescaling O, l and the tile) when a row's tile max exceeds it by > 2^8, which
-//    after the first tiles is rare -- the per-tile rescale of the usual online softmax is
-//    gone.  (Measured: +10 % over the FMA form; an MFMA row sum instead of the 32 VALU adds
-//    and static younger-half priority were both slower or null.)
-//  * V^T fragments for output block t+1 are read while block t's MFMAs run.
-// K+V ring depth of the forward and dQ kernels: 4 = 128 KB (5, all 160 KB of LDS, measured the
-// same: profiles/gemm_dw_r3.md)
-constexpr int BQ8 = 256, NST = 4, STG = 2 * TILE;   // stage = K tile + V tile (32 KB)
+//    for 8 of its 32 cycles), so the softmax is put on a diet: the running row max m
+//    (bf16-exact) rides in the S^T MFMA chain as a folded row constant, so p = exp2(c S')
+//    needs no subtraction.  m only moves (rescaling O, l and the tile) when a row's tile max
+//    exceeds it by > 2^8, which after the first tiles is rare -- the per-tile rescale of the
+//    usual online softmax is gone.  (Measured: +10 % over the FMA form; an MFMA row sum
+//    instead of the VALU adds and static younger-half priority were both slower or null.)
+//  * V^T fragments for PV group g+1 are read while group g's MFMAs run.
+// The dQ kernel keeps 64-key tiles in a 4-deep ring (its S and dP chains hold twice the
+// accumulators).  Ring depth 5 (all 160 KB of LDS) measured the same: profiles/gemm_dw_r3.md.
+constexpr int BQ8 = 256, NST = 4, STG = 2 * TILE;   // dQ: stage = K tile + V tile (32 KB)
 static_assert(NST * STG <= 163840, "LDS");
 constexpr float FOLD_T = 8.f;                       // tolerated growth of p above 1 (log2)
 
@@ -276,16 +277,22 @@ __device__ __forceinline__ u32 lane_id_opaque() {
   return x;
 }
 // K row fragments are read by inline asm FP MFMA steps ahead; tiles staged by SGPR-base DMA
-// (the compiler-scheduled form waited lgkmcnt(0) before every MFMA: profiles/fa_fwd_pipe_ab.txt)
+// (the compiler-scheduled form waited lgkmcnt(0) before every MFMA: profiles/fa_fwd_pipe_ab.txt;
+// 2 / 4 / 5 steps ahead measured the same in the 128-key forward)
 constexpr int FP = 3;
 // (measured and removed: ping-pong wave roles -- waves 4-7 taking each tile's barrier after their
-// S chain, 5-deep ring -- 2.31-2.36 vs 2.23-2.25 ms, profiles/fa_fwd_pingpong_ab.txt)
-constexpr int NSTF = NST;   // forward K+V ring depth
+// S chain -- 2.31-2.36 vs 2.23-2.25 ms, profiles/fa_fwd_pingpong_ab.txt)
+constexpr int BKF = 128;                 // forward keys per tile
+constexpr int TILEF = BKF * D * 2;       // 32 KB
+constexpr int NSF = 2;                   // forward ring depth (stages of K + V)
+constexpr int STGF = 2 * TILEF;
+constexpr int NKT = BKF / 32;            // 32-key chunks per tile
+static_assert(NSF * STGF <= 163840, "LDS");
 template <bool CAUSAL>
 __global__ __launch_bounds__(512, 1) void flash_fwd_kernel(
     const bf16_t* __restrict__ qkv, long ld, bf16_t* __restrict__ out, long ldo,
     float* __restrict__ lse_out, int B, int S, int Hq, int Hkv, float scale_log2) {
-  __shared__ __attribute__((aligned(1024))) char smem[NSTF * STG];
+  __shared__ __attribute__((aligned(1024))) char smem[NSF * STGF];
   const int nqb = (S + BQ8 - 1) / BQ8, G = Hq / Hkv;
   // logical order [b][hkv][q-block][g]: an XCD's contiguous range shares one K/V panel
   int lid = xcd_remap(blockIdx.x, B * Hq * nqb);
@@ -316,17 +323,18 @@ __global__ __launch_bounds__(512, 1) void flash_fwd_kernel(
     dma_kv = (u32)((row * ld + ch * 8) * 2);
   }
   const u32 lds_w = lds_addr(smem) + 1024 * w;
+  // 8 DMA wave-instructions per wave per stage: the 32-row segments i of the K and V tiles
   auto stage = [&](int j) {
-    const u32 st = lds_w + (j % NSTF) * STG;
-    const char* kb_ = reinterpret_cast<const char*>(kp + (long)j * BK * ld);
-    const char* vb_ = reinterpret_cast<const char*>(vp + (long)j * BK * ld);
-    dma_sv(kb_, dma_kv, st);
-    dma_sv(kb_ + 64 * ld, dma_kv, st + 8192);
-    dma_sv(vb_, dma_kv, st + TILE);
-    dma_sv(vb_ + 64 * ld, dma_kv, st + TILE + 8192);
+    const u32 st = lds_w + (j % NSF) * STGF;
+    const char* kb_ = reinterpret_cast<const char*>(kp + (long)j * BKF * ld);
+    const char* vb_ = reinterpret_cast<const char*>(vp + (long)j * BKF * ld);
+#pragma unroll
+    for (int i = 0; i < NKT; ++i) dma_sv(kb_ + (long)64 * ld * i, dma_kv, st + 8192 * i);
+#pragma unroll
+    for (int i = 0; i < NKT; ++i) dma_sv(vb_ + (long)64 * ld * i, dma_kv, st + TILEF + 8192 * i);
   };
-  const int ntiles = CAUSAL ? min(S, qb * BQ8 + BQ8) / BK : S / BK;
-  for (int j = 0; j < NSTF - 1 && j < ntiles; ++j) stage(j);
+  const int ntiles = CAUSAL ? min(S, qb * BQ8 + BQ8) / BKF : S / BKF;
+  if (ntiles > 0) stage(0);
 
   // retire the Q loads HERE (the compiler's wait counts only them, the DMA stays in flight):
   // a first use inside the loop would make hipcc wait vmcnt(0) on every tile
@@ -343,125 +351,126 @@ __global__ __launch_bounds__(512, 1) void flash_fwd_kernel(
   const int vrow = 4 * hh + ((l & 15) >> 2);
   const int vcol = 16 * ((l >> 4) & 1) + 4 * (l & 3);
 
-  constexpr int AH = NSTF - 1;
-  // S'^T = K (c Q)^T - m of tile j: key on the accumulator rows, query on the lane
-  auto s_chain = [&](int j, f32x16 (&sc)[2]) {
-    const char* Ks = smem + (j % NSTF) * STG;   // (kept: its removal reorders two SALU ops)
-    (void)Ks;
-      // K row fragments by inline asm, FP steps ahead; the two 32-key chains alternate
-      const u32 ln = lane_id_opaque(), lr_ = ln & 31;
-      const u32 a_t = (lds_addr(smem) + (u32)((j % NSTF) * STG)) + lr_ * 256 + 16 * ((ln >> 5) ^ swz_x(lr_));
-      bf16x8 fk[FP + 1];
-      auto rdK = [&](auto ic) {
-        constexpr int i = decltype(ic)::value, kt = i & 1, ks = i >> 1;
-        fk[i % (FP + 1)] = rd_b128<8192 * kt>(a_t ^ (32 * ks));
-      };
-      static_for<0, FP>([&](auto ic) { rdK(ic); });
-      sc[0] = mfma32(ones, mref, f32x16{});
-      sc[1] = mfma32(ones, mref, f32x16{});
-      static_for<0, 16>([&](auto ic) {
-        constexpr int i = decltype(ic)::value, kt = i & 1, ks = i >> 1;
-        if constexpr (i + FP < 16) rdK(std::integral_constant<int, i + FP>());
-        lgkm_tie1<(i + FP < 16 ? FP : 15 - i)>(fk[i % (FP + 1)]);
-        sc[kt] = mfma32(fk[i % (FP + 1)], qf[ks], sc[kt]);
-      });
+  // S'^T = K Q^T - m of tile j: key on the accumulator rows, query on the lane; K row fragments
+  // by inline asm, FP steps ahead, the four 32-key chains alternating
+  auto s_chain = [&](int j, f32x16 (&sc)[NKT]) {
+    const u32 ln = lane_id_opaque(), lr_ = ln & 31;
+    const u32 a_t = (lds_addr(smem) + (u32)((j % NSF) * STGF)) + lr_ * 256 + 16 * ((ln >> 5) ^ swz_x(lr_));
+    bf16x8 fk[FP + 1];
+    auto rdK = [&](auto ic) {
+      constexpr int i = decltype(ic)::value, kt = i % NKT, ks = i / NKT;
+      fk[i % (FP + 1)] = rd_b128<8192 * kt>(a_t ^ (32 * ks));
+    };
+    static_for<0, FP>([&](auto ic) { rdK(ic); });
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) sc[kt] = mfma32(ones, mref, f32x16{});
+    static_for<0, 8 * NKT>([&](auto ic) {
+      constexpr int i = decltype(ic)::value, kt = i % NKT, ks = i / NKT, NI = 8 * NKT;
+      if constexpr (i + FP < NI) rdK(std::integral_constant<int, i + FP>());
+      lgkm_tie1<(i + FP < NI ? FP : NI - 1 - i)>(fk[i % (FP + 1)]);
+      sc[kt] = mfma32(fk[i % (FP + 1)], qf[ks], sc[kt]);
+    });
   };
   // causal mask, online softmax, O^T += V^T P^T of tile j
-  auto soft_pv = [&](int j, f32x16 (&sc)[2]) {
-    const int k0 = j * BK;
-    const char* Vs = smem + (j % NSTF) * STG + TILE;
-      if (CAUSAL && k0 + BK - 1 > qmin_w) {   // a wave's diagonal tiles only (uniform branch)
+  auto soft_pv = [&](int j, f32x16 (&sc)[NKT]) {
+    const int k0 = j * BKF;
+    const char* Vs = smem + (j % NSF) * STGF + TILEF;
+    if (CAUSAL && k0 + BKF - 1 > qmin_w) {   // a wave's diagonal tiles only (uniform branch)
 #pragma unroll
-        for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int key = k0 + 32 * kt + (r & 3) + 8 * (r >> 2) + 4 * hh;
-            sc[kt][r] = key > q ? -INFINITY : sc[kt][r];
-          }
-      }
-      float mx = -INFINITY;
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sc[kt][r]);
-      mx = xor32_max(mx);
-      if (__ballot(first || mx > thresh)) {
-        // move the reference: m' = bf16(m + max(mx, 0)); rescale O, l and this tile's S'
-        const float mnew = first ? bf16_round(mx) : bf16_round(m + fmaxf(mx, 0.f));
-        const float shift = first ? mnew : mnew - m;
-        const float alpha = first ? 0.f : __builtin_amdgcn_exp2f(-shift * scale_log2);
-        lsum *= alpha;
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) sc[kt][r] -= shift;
-        m = mnew;
-        first = false;
-        mref = fold_const(m, hh);
-      }
-      float rs = 0.f;
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
+      for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float p = __builtin_amdgcn_exp2f(sc[kt][r] * scale_log2);
-          sc[kt][r] = p;
-          rs += p;
+          const int key = k0 + 32 * kt + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          sc[kt][r] = key > q ? -INFINITY : sc[kt][r];
         }
-      lsum += xor32_sum(rs);
-      bf16x8 pf[2][2];
+    }
+    float mx = -INFINITY;
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sc[kt][r]);
+    mx = xor32_max(mx);
+    if (__ballot(first || mx > thresh)) {
+      // move the reference: m' = bf16(m + max(mx, 0)); rescale O, l and this tile's S'
+      const float mnew = first ? bf16_round(mx) : bf16_round(m + fmaxf(mx, 0.f));
+      const float shift = first ? mnew : mnew - m;
+      const float alpha = first ? 0.f : __builtin_amdgcn_exp2f(-shift * scale_log2);
+      lsum *= alpha;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sc[kt][r] -= shift;
+      m = mnew;
+      first = false;
+      mref = fold_const(m, hh);
+    }
+    float rs = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = __builtin_amdgcn_exp2f(sc[kt][r] * scale_log2);
+        sc[kt][r] = p;
+        rs += p;
+      }
+    lsum += xor32_sum(rs);
+    bf16x8 pf[NKT][2];
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        u32x4 u;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) u[i] = pack2(sc[kt][8 * ss + 2 * i], sc[kt][8 * ss + 2 * i + 1]);
+        pf[kt][ss] = as_bf16x8(u);
+      }
+    // O^T += V^T P^T in 8 groups (output block t, key half hf); group g+1's V^T fragments are
+    // read while group g's MFMAs run
+    const u32 vbase = lds_addr(Vs);
+    bf16x8 vf[2][4];
+    auto v_read = [&](int gi, bf16x8* f) {
+      const int t = gi >> 1, hf = gi & 1;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
         for (int ss = 0; ss < 2; ++ss) {
-          u32x4 u;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) u[i] = pack2(sc[kt][8 * ss + 2 * i], sc[kt][8 * ss + 2 * i + 1]);
-          pf[kt][ss] = as_bf16x8(u);
+          const int row = 32 * (2 * hf + kk) + 16 * ss + vrow, col = 32 * t + vcol;
+          f[2 * kk + ss] = tr_pair_asm(vbase + swz8(row, col), vbase + swz8(row + 8, col));
         }
-      // O^T += V^T P^T; the V^T fragments of block t+1 are read while block t's MFMAs run
-      const u32 vbase = lds_addr(Vs);
-      bf16x8 vf[2][4];
-      auto v_read = [&](int t, bf16x8* f) {
+    };
+    v_read(0, vf[0]);
 #pragma unroll
-        for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-          for (int ss = 0; ss < 2; ++ss) {
-            const int row = 32 * kt + 16 * ss + vrow, col = 32 * t + vcol;
-            f[2 * kt + ss] = tr_pair_asm(vbase + swz8(row, col), vbase + swz8(row + 8, col));
-          }
-      };
-      v_read(0, vf[0]);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        if (t < 3) {
-          v_read(t + 1, vf[(t + 1) & 1]);
-          lgkm_wait_tie<8>(vf[t & 1]);
-        } else {
-          lgkm_wait_tie<0>(vf[t & 1]);
-        }
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-          for (int ss = 0; ss < 2; ++ss) o[t] = mfma32(vf[t & 1][2 * kt + ss], pf[kt][ss], o[t]);
+    for (int gi = 0; gi < 8; ++gi) {
+      if (gi < 7) {
+        v_read(gi + 1, vf[(gi + 1) & 1]);
+        lgkm_wait_tie<8>(vf[gi & 1]);
+      } else {
+        lgkm_wait_tie<0>(vf[gi & 1]);
       }
-      };
-  auto live_tile = [&](int j) { return live && (!CAUSAL || j * BK <= qmax_w); };
+      const int t = gi >> 1, hf = gi & 1;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) o[t] = mfma32(vf[gi & 1][2 * kk + ss], pf[2 * hf + kk][ss], o[t]);
+    }
+  };
+  auto live_tile = [&](int j) { return live && (!CAUSAL || j * BKF <= qmax_w); };
 
-  wait_stage(0, min(AH - 1, ntiles - 1));
+  vm_wait<0>();
   barrier();
-  f32x16 scp[2];
+  f32x16 scp[NKT];
   for (int j = 0; j < ntiles; ++j) {
-    if (j + AH < ntiles) stage(j + AH);
-    const bool lv = live_tile(j);
-    if (lv) s_chain(j, scp);
-    if (lv) soft_pv(j, scp);
+    if (j + 1 < ntiles) stage(j + 1);   // into the buffer every wave finished with (tile j-1)
+    if (live_tile(j)) {
+      s_chain(j, scp);
+      soft_pv(j, scp);
+    }
     if (j + 1 < ntiles) {
-      wait_stage(j + 1, min(j + AH, ntiles - 1));
+      vm_wait<0>();
       barrier();
     }
   }

@@ -3,6 +3,7 @@
 // sampled rows of O, lse, dQ, dK and dV against a float64 CPU reference.  Build variants
 // with -D flags on flash_attn_lab.hip, a lab copy of ops/csrc/flash_attn.hip (tools/kbench/build.sh); run: fa_bench [B S Hq Hkv iters].
 #include "flash_attn_lab.hip"   // the production kernels plus the measured-and-rejected knobs and stamps
+#include "fa_fwd128_lab.hip"    // KFAMD_FA_FWD=128: the 128-key-tile forward
 
 #include <cmath>
 #include <cstdio>
@@ -111,7 +112,12 @@ int main(int argc, char** argv) {
     const long chunks = (long)T * Hkv * 32;
     flash_bwd_post_kernel<<<(int)std::min<long>((chunks + 255) / 256, 16384), 256>>>(dk, dv, dqkv, ldq, T, Hq, Hkv);
   };
-  timeit("fwd", 2 * mm, [&] { flash_fwd_kernel<true><<<g_f, 512>>>(qkv, ldq, o, ldo, lse, B, S, Hq, Hkv, sl2); });
+  const char* fwd_env = getenv("KFAMD_FA_FWD");
+  const bool fwd128 = fwd_env && atoi(fwd_env) == 128;
+  timeit(fwd128 ? "fwd128" : "fwd", 2 * mm, [&] {
+    if (fwd128) flash_fwd128_kernel<true><<<g_f, 512>>>(qkv, ldq, o, ldo, lse, B, S, Hq, Hkv, sl2);
+    else flash_fwd_kernel<true><<<g_f, 512>>>(qkv, ldq, o, ldo, lse, B, S, Hq, Hkv, sl2);
+  });
   CK(hipGetLastError());
   double bwd = 0;
   bwd += timeit("pre", 0, [&] { flash_bwd_pre_kernel<<<(T * Hq + 15) / 16, 256>>>(o, ldo, dout, ldo, delta, B, S, Hq); });
