@@ -53,8 +53,7 @@ typedef __attribute__((ext_vector_type(4))) float f4;
 namespace fa {
 constexpr int D = 128;
 constexpr int BQ = 128;           // sequence-length granule the launchers require (S % BQ == 0)
-constexpr int BK = 64;            // keys per tile of the dQ kernel (the forward: BKF = 128)
-constexpr int TILE = BK * D * 2;  // 16 KB
+constexpr int BK = 64;            // keys per dQ half-stage (stages hold BKF = 128)
 constexpr int BKV = 128;          // keys per dK/dV workgroup (4 waves x 32)
 constexpr int QT = 32;            // query rows per dK/dV iteration
 constexpr int QCH = 1024;         // query rows per dK/dV work item (512 / 2048: 6 % / 4 % slower)
@@ -254,21 +253,11 @@ __device__ __forceinline__ bf16x8 fold_const(float c, int hh) {
 //    usual online softmax is gone.  (Measured: +10 % over the FMA form; an MFMA row sum
 //    instead of the VALU adds and static younger-half priority were both slower or null.)
 //  * V^T fragments for PV group g+1 are read while group g's MFMAs run.
-// The dQ kernel keeps 64-key tiles in a 4-deep ring (its S and dP chains hold twice the
-// accumulators).  Ring depth 5 (all 160 KB of LDS) measured the same: profiles/gemm_dw_r3.md.
-constexpr int BQ8 = 256, NST = 4, STG = 2 * TILE;   // dQ: stage = K tile + V tile (32 KB)
-static_assert(NST * STG <= 163840, "LDS");
+// The dQ kernel stages K/V the same way but computes each 128-key stage as two 64-key halves
+// (its S and dP chains hold twice the forward's accumulators): 2.81 vs 2.86 ms, the same
+// numerics (profiles/fa_fwd128_r5.md).
+constexpr int BQ8 = 256;                            // query rows per forward / dQ workgroup
 constexpr float FOLD_T = 8.f;                       // tolerated growth of p above 1 (log2)
-
-// wait until stage `next` landed, given that stages up to `last` were issued (4 DMA
-// instructions per wave per stage, retired in order)
-__device__ __forceinline__ void wait_stage(int next, int last) {
-  const int ahead = last - next;
-  if (ahead >= 3) vm_wait<12>();
-  else if (ahead >= 2) vm_wait<8>();
-  else if (ahead == 1) vm_wait<4>();
-  else vm_wait<0>();
-}
 
 // lane id from v_mbcnt in asm volatile: recomputed where used, never kept live in a VGPR
 __device__ __forceinline__ u32 lane_id_opaque() {
@@ -282,9 +271,9 @@ __device__ __forceinline__ u32 lane_id_opaque() {
 constexpr int FP = 3;
 // (measured and removed: ping-pong wave roles -- waves 4-7 taking each tile's barrier after their
 // S chain -- 2.31-2.36 vs 2.23-2.25 ms, profiles/fa_fwd_pingpong_ab.txt)
-constexpr int BKF = 128;                 // forward keys per tile
+constexpr int BKF = 128;                 // keys per K/V stage (forward and dQ)
 constexpr int TILEF = BKF * D * 2;       // 32 KB
-constexpr int NSF = 2;                   // forward ring depth (stages of K + V)
+constexpr int NSF = 2;                   // ring depth (stages of K + V)
 constexpr int STGF = 2 * TILEF;
 constexpr int NKT = BKF / 32;            // 32-key chunks per tile
 static_assert(NSF * STGF <= 163840, "LDS");
@@ -539,7 +528,7 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dq_kernel(
     const bf16_t* __restrict__ qkv, long ld, const bf16_t* __restrict__ dout, long lddo,
     const float* __restrict__ lse, const float* __restrict__ delta, bf16_t* __restrict__ dqkv,
     long lddq, int B, int S, int Hq, int Hkv, float scale_log2, float scale) {
-  __shared__ __attribute__((aligned(1024))) char smem[NST * STG];
+  __shared__ __attribute__((aligned(1024))) char smem[NSF * STGF];
   const int nqb = (S + BQ8 - 1) / BQ8, G = Hq / Hkv;
   int lid = xcd_remap(blockIdx.x, B * Hq * nqb);
   const int g = lid % G;
@@ -577,17 +566,19 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dq_kernel(
     dma_kv = (u32)((row * ld + ch * 8) * 2);
   }
   const u32 lds_w = lds_addr(smem) + 1024 * w;
+  // a stage is 128 keys of K and V (the forward's staging: 8 DMA wave-instructions per wave,
+  // 2-deep ring), computed as two 64-key halves under one barrier
   auto stage = [&](int j) {
-    const u32 st = lds_w + (j % NST) * STG;
-    const char* kb_ = reinterpret_cast<const char*>(kp + (long)j * BK * ld);
-    const char* vb_ = reinterpret_cast<const char*>(vp + (long)j * BK * ld);
-    dma_sv(kb_, dma_kv, st);
-    dma_sv(kb_ + 64 * ld, dma_kv, st + 8192);
-    dma_sv(vb_, dma_kv, st + TILE);
-    dma_sv(vb_ + 64 * ld, dma_kv, st + TILE + 8192);
+    const u32 st = lds_w + (j % NSF) * STGF;
+    const char* kb_ = reinterpret_cast<const char*>(kp + (long)j * BKF * ld);
+    const char* vb_ = reinterpret_cast<const char*>(vp + (long)j * BKF * ld);
+#pragma unroll
+    for (int i = 0; i < NKT; ++i) dma_sv(kb_ + (long)64 * ld * i, dma_kv, st + 8192 * i);
+#pragma unroll
+    for (int i = 0; i < NKT; ++i) dma_sv(vb_ + (long)64 * ld * i, dma_kv, st + TILEF + 8192 * i);
   };
-  const int ntiles = CAUSAL ? min(S, qb * BQ8 + BQ8) / BK : S / BK;
-  for (int j = 0; j < NST - 1 && j < ntiles; ++j) stage(j);
+  const int ntiles = CAUSAL ? min(S, qb * BQ8 + BQ8) / BKF : S / BKF;
+  if (ntiles > 0) stage(0);
   // retire the register loads before the loop (see the forward)
 #pragma unroll
   for (int ks = 0; ks < 8; ++ks) asm volatile("" : "+v"(qf[ks]), "+v"(df[ks]));
@@ -600,13 +591,16 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dq_kernel(
   const int vrow = 4 * hh + ((l & 15) >> 2);
   const int vcol = 16 * ((l >> 4) & 1) + 4 * (l & 3);
 
-  wait_stage(0, min(NST - 2, ntiles - 1));
+  vm_wait<0>();
   barrier();
   for (int j = 0; j < ntiles; ++j) {
-    if (j + NST - 1 < ntiles) stage(j + NST - 1);
-    const int k0 = j * BK;
+    if (j + 1 < ntiles) stage(j + 1);   // into the buffer every wave finished with (stage j-1)
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+    const int k0 = j * BKF + BK * hf;
     if (live && (!CAUSAL || k0 <= qmax_w)) {
-      const char* Ks = smem + (j % NST) * STG;
+      const u32 hoff = (u32)((j % NSF) * STGF + BK * 256 * hf);   // this half's K rows (V: + TILEF)
+      const char* Ks = smem + hoff;
       // non-causal: an opaque false keeps the causal loop's shape (folded away, hipcc spilled)
       int nm = CAUSAL ? (k0 + BK - 1 > qmin_w) : 0;
       if (!CAUSAL) asm volatile("" : "+v"(nm));
@@ -618,12 +612,12 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dq_kernel(
       // rematerialised from the lane id per tile (a long-lived copy spilled, and its reload
       // waited vmcnt(0) -- i.e. for every DMA stage in flight)
       const u32 ln = lane_id_opaque(), lr_ = ln & 31;
-      const u32 a_t = (lds_addr(smem) + (u32)((j % NST) * STG)) + lr_ * 256 + 16 * ((ln >> 5) ^ swz_x(lr_));
+      const u32 a_t = (lds_addr(smem) + hoff) + lr_ * 256 + 16 * ((ln >> 5) ^ swz_x(lr_));
       bf16x8 fk[QP + 1], fv[QP + 1];
       auto rdS = [&](auto ic) {
         constexpr int i = decltype(ic)::value, kt = i >> 3, ks = i & 7, sl = i % (QP + 1);
         fk[sl] = rd_b128<8192 * kt>(a_t ^ (32 * ks));
-        fv[sl] = rd_b128<TILE + 8192 * kt>(a_t ^ (32 * ks));
+        fv[sl] = rd_b128<TILEF + 8192 * kt>(a_t ^ (32 * ks));
       };
       static_for<0, QP>([&](auto ic) { rdS(ic); });
       f32x16 s, dp;
@@ -685,8 +679,9 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dq_kernel(
           for (int ss = 0; ss < 2; ++ss) dq[t] = mfma32(kf[t & 1][2 * kt + ss], sf[kt][ss], dq[t]);
       }
     }
+    }
     if (j + 1 < ntiles) {
-      wait_stage(j + 1, min(j + NST - 1, ntiles - 1));
+      vm_wait<0>();
       barrier();
     }
   }

@@ -4,6 +4,7 @@
 // with -D flags on flash_attn_lab.hip, a lab copy of ops/csrc/flash_attn.hip (tools/kbench/build.sh); run: fa_bench [B S Hq Hkv iters].
 #include "flash_attn_lab.hip"   // the production kernels plus the measured-and-rejected knobs and stamps
 #include "fa_fwd128_lab.hip"    // KFAMD_FA_FWD=128: the 128-key-tile forward
+#include "fa_dq128_lab.hip"     // KFAMD_FA_DQ=128: dQ with 128-key stages
 
 #include <cmath>
 #include <cstdio>
@@ -122,14 +123,18 @@ int main(int argc, char** argv) {
   double bwd = 0;
   bwd += timeit("pre", 0, [&] { flash_bwd_pre_kernel<<<(T * Hq + 15) / 16, 256>>>(o, ldo, dout, ldo, delta, B, S, Hq); });
   bwd += timeit(use64 ? "dkdv64" : "dkdv", 4 * mm, dkdv_run);
-  bwd += timeit("dq", 3 * mm, [&] {
-    flash_bwd_dq_kernel<true><<<g_q, 512>>>(qkv, ldq, dout, ldo, lse, delta, dqkv, ldq, B, S, Hq, Hkv, sl2, scale);
-  });
+  const char* dq_env = getenv("KFAMD_FA_DQ");
+  const bool dq128 = dq_env && atoi(dq_env) == 128;
+  auto dq_run = [&] {
+    if (dq128) flash_bwd_dq128_kernel<true><<<g_q, 512>>>(qkv, ldq, dout, ldo, lse, delta, dqkv, ldq, B, S, Hq, Hkv, sl2, scale);
+    else flash_bwd_dq_kernel<true><<<g_q, 512>>>(qkv, ldq, dout, ldo, lse, delta, dqkv, ldq, B, S, Hq, Hkv, sl2, scale);
+  };
+  bwd += timeit(dq128 ? "dq128" : "dq", 3 * mm, dq_run);
   bwd += timeit("post", 0, post);
   // one clean pass for the checks (the timing loops accumulated dK/dV repeatedly)
   zero();
   dkdv_run();
-  flash_bwd_dq_kernel<true><<<g_q, 512>>>(qkv, ldq, dout, ldo, lse, delta, dqkv, ldq, B, S, Hq, Hkv, sl2, scale);
+  dq_run();
   post();
   CK(hipDeviceSynchronize());
   printf("bwd_total %8.1f us  %6.0f TF(5-product)\n", bwd * 1e3, 5 * mm / (bwd * 1e-3) / 1e12);
