@@ -998,11 +998,19 @@ static_assert(NWK == 4 || NWK == 8, "dK/dV waves");
 constexpr int BKVW = 32 * NWK;                 // keys per workgroup
 // the per-iteration buffers sit first so their ds_read immediates (buffer + tile offsets)
 // stay below the 16-bit offset field; K (read through a per-wave VGPR base) follows
-constexpr int OFF_Q = 0;                       // [2][32 x 256 B]
-constexpr int OFF_DO = OFF_Q + 16384;          // [2][32 x 256 B]
-constexpr int OFF_LD = OFF_DO + 16384;         // [2][lse 32 f32 | delta 32 f32]
-constexpr int OFF_K = OFF_LD + 512;            // [BKVW keys x 256 B] = 32 / 64 KB (256-B aligned)
-constexpr int SMEM = OFF_K + BKVW * 256;       // 66048 B (2 WG per CU) / 98816 B (1 WG per CU)
+// KF_FA_DKDV_Q2=1 (with NW=8): 64 query rows per barrier -- the Q/dO ring holds two pairs of
+// 32-row slots, the two tiles of a pair are computed back to back under one barrier, and the
+// next pair is staged at the start of a pair
+#ifndef KF_FA_DKDV_Q2
+#define KF_FA_DKDV_Q2 0
+#endif
+static_assert(!KF_FA_DKDV_Q2 || KF_FA_DKDV_NW == 8, "Q2 needs the 8-wave workgroup (LDS)");
+constexpr int NSLOT = KF_FA_DKDV_Q2 ? 4 : 2;   // 32-row Q/dO slots
+constexpr int OFF_Q = 0;                       // [NSLOT][32 x 256 B]
+constexpr int OFF_DO = OFF_Q + NSLOT * 8192;   // [NSLOT][32 x 256 B]
+constexpr int OFF_LD = OFF_DO + NSLOT * 8192;  // [NSLOT][lse 32 f32 | delta 32 f32]
+constexpr int OFF_K = OFF_LD + NSLOT * 256;    // [BKVW keys x 256 B] = 32 / 64 KB (256-B aligned)
+constexpr int SMEM = OFF_K + BKVW * 256;       // 66048 B (2 WG per CU) / 98816 B (1 WG per CU) / Q2 132096 B
 // 1 = software-pipelined iteration (inline-asm LDS reads, counted waits); 0 = compiler-scheduled
 #ifndef KF_FA_DKDV_PIPE
 #define KF_FA_DKDV_PIPE 1
@@ -1153,7 +1161,14 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
   const int vrow = 4 * hh + ((l & 15) >> 2);
   const int vcol = 16 * ((l >> 4) & 1) + 4 * (l & 3);
 
-#if KF_FA_DKDV_PIPE
+#if KF_FA_DKDV_PIPE && KF_FA_DKDV_Q2
+  int nx_hq = 0, nx_qt = 0, cu_qt = 0;   // next tile to stage; this iteration's query tile
+  auto adv = [&]() {
+    if (++nx_qt == ntq) { nx_qt = 0; ++nx_hq; }
+  };
+  if (niter > 0) { stage(0, 0, 0); adv(); }
+  if (niter > 1) { stage(nx_hq, nx_qt, 1); adv(); }
+#elif KF_FA_DKDV_PIPE
   if (niter > 0) stage(0, 0, 0);
 #else
   if (niter > 0) stage(0, 0);
@@ -1176,11 +1191,13 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
   const float fold_mul = inv_scale, pmul = c;
 #endif
   const bf16x8 ones = fold_ones(hh);
-#if KF_FA_DKDV_PIPE
+#if KF_FA_DKDV_PIPE && !KF_FA_DKDV_Q2
   int nx_hq = 0, nx_qt = 0;   // (head, tile) of the NEXT iteration to stage
   auto adv = [&]() {
     if (++nx_qt == ntq) { nx_qt = 0; ++nx_hq; }
   };
+#endif
+#if KF_FA_DKDV_PIPE
   // Software-pipelined iteration.  Every LDS read is inline asm with an immediate buffer
   // offset and a counted, register-tying wait: the compiler-scheduled form issued each
   // operand right before its MFMA behind an lgkmcnt(0) (one read latency exposed per MFMA)
@@ -1208,10 +1225,21 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
   auto iter = [&](auto curc, int it) {
     constexpr int CUR = decltype(curc)::value;
     constexpr int OQ = OFF_Q + CUR * 8192, OD = OFF_DO + CUR * 8192, OL = CUR * 256;
+#if KF_FA_DKDV_Q2
+    const int q0 = qs + cu_qt * QT;   // this iteration's tile; nx_* is the next tile to stage
+    if (++cu_qt == ntq) cu_qt = 0;
+    KF_STAMP(0);
+    if constexpr (CUR % 2 == 0) {   // first tile of a pair: stage the next pair into the other one
+      constexpr int NB = ((CUR / 2) ^ 1) * 2;
+      if (it + 2 < niter) { stage(nx_hq, nx_qt, NB); adv(); }
+      if (it + 3 < niter) { stage(nx_hq, nx_qt, NB + 1); adv(); }
+    }
+#else
     const int q0 = qs + nx_qt * QT;   // this iteration's tile (advanced below to the next)
     KF_STAMP(0);
     adv();
     if (it + 1 < niter) stage(nx_hq, nx_qt, CUR ^ 1);
+#endif
     KF_STAMP(1);
     // opaque per iteration: keeps the 32 XOR-ed per-read addresses from being hoisted out of
     // the loop as invariants (they would pin ~30 VGPRs and spill)
@@ -1290,9 +1318,27 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
       prio(0);
       KF_STAMP(4);
     }
+#if KF_FA_DKDV_Q2
+    if (CUR % 2 == 1 || it + 1 >= niter) wait_dma_barrier();   // one barrier per pair
+#else
     wait_dma_barrier();
+#endif
     KF_STAMP(5);
   };
+#if KF_FA_DKDV_Q2
+  {
+    int it = 0;
+    for (; it + 3 < niter; it += 4) {
+      iter(std::integral_constant<int, 0>(), it);
+      iter(std::integral_constant<int, 1>(), it + 1);
+      iter(std::integral_constant<int, 2>(), it + 2);
+      iter(std::integral_constant<int, 3>(), it + 3);
+    }
+    if (it < niter) iter(std::integral_constant<int, 0>(), it);
+    if (it + 1 < niter) iter(std::integral_constant<int, 1>(), it + 1);
+    if (it + 2 < niter) iter(std::integral_constant<int, 2>(), it + 2);
+  }
+#else
   {
     int it = 0;
     for (; it + 1 < niter; it += 2) {
@@ -1301,6 +1347,7 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
     }
     if (it < niter) iter(std::integral_constant<int, 0>(), it);
   }
+#endif
 #if KF_FA_STAMPS
   const unsigned long long st_loop1 = __builtin_amdgcn_s_memtime();
 #endif
