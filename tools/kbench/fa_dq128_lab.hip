@@ -4,6 +4,9 @@
 #ifndef KF_DQ128_UNROLL
 #define KF_DQ128_UNROLL 0
 #endif
+#ifndef KF_DQ128_OST
+#define KF_DQ128_OST 0
+#endif
 namespace d128 {
 constexpr int BK2 = 128, TILE2 = BK2 * D * 2, NS2 = 2, STG2 = 2 * TILE2;
 static_assert(NS2 * STG2 <= 163840, "LDS");
@@ -175,6 +178,30 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dq128_kernel(
     }
   }
   if (!live) return;
+#if KF_DQ128_OST
+  {
+    // dQ staged through the ring buffer the last stage did not use, then whole-row stores
+    char* ob = smem + (ntiles % d128::NS2) * d128::STG2 + 8192 * w;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        u32x2 v;
+        v[0] = pack2(dq[t][4 * gq] * scale, dq[t][4 * gq + 1] * scale);
+        v[1] = pack2(dq[t][4 * gq + 2] * scale, dq[t][4 * gq + 3] * scale);
+        *reinterpret_cast<u32x2*>(ob + swz(lr, 4 * t + gq) + 8 * hh) = v;
+      }
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    bf16_t* orow = dqkv + ((long)b * S + qmin_w) * lddq + (long)h * D;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int row = 4 * i + (l >> 4), ch = l & 15;
+      st16(orow + (long)row * lddq + 8 * ch, *reinterpret_cast<const u32x4*>(ob + swz(row, ch)));
+    }
+  }
+#else
   bf16_t* op = dqkv + ((long)b * S + q) * lddq + (long)h * D;
 #pragma unroll
   for (int t = 0; t < 4; ++t)
@@ -186,5 +213,6 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dq128_kernel(
       v[1] = pack2(dq[t][4 * gq + 2] * scale, dq[t][4 * gq + 3] * scale);
       *reinterpret_cast<u32x2*>(op + d) = v;
     }
+#endif
 }
 

@@ -21,6 +21,10 @@ static_assert(NS * STGF <= 163840, "LDS");
 constexpr int FPK = KF_F128_FP;
 #ifndef KF_F128_LATE
 #define KF_F128_LATE 0
+#endif
+// 1 = O staged through LDS and stored as whole rows (16 B per lane) instead of 8-B pieces
+#ifndef KF_F128_OST
+#define KF_F128_OST 0
 #endif       // K row fragments read this many MFMA steps ahead
 }  // namespace f128
 
@@ -209,6 +213,31 @@ __global__ __launch_bounds__(512, 1) void flash_fwd128_kernel(
   }
   if (!live) return;
   const float inv = 1.f / lsum;
+#if KF_F128_OST
+  {
+    // O staged through the ring buffer the last tile did not use, [32 rows][256 B] per wave
+    // (swizzled 16-B chunks), then stored as whole rows: 16 B per lane, 4 rows per instruction
+    char* ob = smem + (ntiles % NS) * STGF + 8192 * w;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        u32x2 v;
+        v[0] = pack2(o[t][4 * gq] * inv, o[t][4 * gq + 1] * inv);
+        v[1] = pack2(o[t][4 * gq + 2] * inv, o[t][4 * gq + 3] * inv);
+        *reinterpret_cast<u32x2*>(ob + swz(lr, 4 * t + gq) + 8 * hh) = v;
+      }
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    bf16_t* orow = out + ((long)b * S + qmin_w) * ldo + (long)h * D;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int row = 4 * i + (l >> 4), ch = l & 15;
+      st16(orow + (long)row * ldo + 8 * ch, *reinterpret_cast<const u32x4*>(ob + swz(row, ch)));
+    }
+  }
+#else
   bf16_t* op = out + ((long)b * S + q) * ldo + (long)h * D;
 #pragma unroll
   for (int t = 0; t < 4; ++t)
@@ -220,5 +249,6 @@ __global__ __launch_bounds__(512, 1) void flash_fwd128_kernel(
       v[1] = pack2(o[t][4 * gq + 2] * inv, o[t][4 * gq + 3] * inv);
       *reinterpret_cast<u32x2*>(op + d) = v;
     }
+#endif
   if (hh == 0) lse_out[((long)b * Hq + h) * S + q] = (m * scale_log2 + log2f(lsum)) * LN2;
 }
