@@ -1004,6 +1004,9 @@ constexpr int BKVW = 32 * NWK;                 // keys per workgroup
 #ifndef KF_FA_DKDV_Q2
 #define KF_FA_DKDV_Q2 0
 #endif
+#ifndef KF_FA_DKDV_FLUSH
+#define KF_FA_DKDV_FLUSH 1
+#endif
 static_assert(!KF_FA_DKDV_Q2 || KF_FA_DKDV_NW == 8, "Q2 needs the 8-wave workgroup (LDS)");
 constexpr int NSLOT = KF_FA_DKDV_Q2 ? 4 : 2;   // 32-row Q/dO slots
 constexpr int OFF_Q = 0;                       // [NSLOT][32 x 256 B]
@@ -1436,7 +1439,10 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
       float* dst = dst_base + (rowB + kv0 + 128 * pass) * (long)(Hkv * D) + (long)hkv * D;
       for (int e = tid; e < 128 * 128; e += 64 * NWK) {
         const int key = e >> 7, d = e & 127;
-        atomicAdd(dst + (long)key * Hkv * D + d, T[key * 128 + (d ^ ((key & 31) << 2))]);
+        // KF_FA_DKDV_FLUSH: 1 = fp32 atomics (production); 0 = anatomy build without the partial
+        // sums (numerics broken); 2 = plain stores instead of atomics (numerics broken)
+        if (KF_FA_DKDV_FLUSH == 1) atomicAdd(dst + (long)key * Hkv * D + d, T[key * 128 + (d ^ ((key & 31) << 2))]);
+        else if (KF_FA_DKDV_FLUSH == 2) dst[(long)key * Hkv * D + d] = T[key * 128 + (d ^ ((key & 31) << 2))];
       }
       __syncthreads();
     }
