@@ -55,7 +55,7 @@ def _flags():
 
 # per-source extra flags: flash_attn.hip's kernels were tuned (and their code is pinned,
 # tests/test_kernels_static.py) with the MFMA accumulators in the VGPR form
-FILE_FLAGS = {"flash_attn.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+FILE_FLAGS = {"flash_attn.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form", "-fno-slp-vectorize"]}
 
 
 def _sources():
