@@ -54,7 +54,10 @@ def _flags():
 
 
 # per-source extra flags: flash_attn.hip's kernels were tuned (and their code is pinned,
-# tests/test_kernels_static.py) with the MFMA accumulators in the VGPR form
+# tests/test_kernels_static.py) with the MFMA accumulators in the VGPR form, and are built
+# without SLP vectorization: it packed the softmax's f32 adds / multiplies into v_pk_*_f32,
+# which cost more issue slots beside the MFMAs than the scalar ops (attention backward 7.50 ->
+# 7.26 ms at B4 S8192, profiles/fa_fwd128_r5.md)
 FILE_FLAGS = {"flash_attn.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form", "-fno-slp-vectorize"]}
 
 
