@@ -1007,6 +1007,12 @@ constexpr int BKVW = 32 * NWK;                 // keys per workgroup
 #ifndef KF_FA_DKDV_FLUSH
 #define KF_FA_DKDV_FLUSH 1
 #endif
+// flush transpose swizzle: 0 = d ^ ((key & 31) << 2) (4-way bank conflicts on the writes: the 64
+// lanes of a write hit 16 banks); 1 = key's 5 bits spread over d bits {0,1,3,4,5} (bit 2 is hh),
+// so every write instruction hits 64 distinct banks; rows stay permutations for the reads
+#ifndef KF_FA_DKDV_TSW
+#define KF_FA_DKDV_TSW 0
+#endif
 static_assert(!KF_FA_DKDV_Q2 || KF_FA_DKDV_NW == 8, "Q2 needs the 8-wave workgroup (LDS)");
 constexpr int NSLOT = KF_FA_DKDV_Q2 ? 4 : 2;   // 32-row Q/dO slots
 constexpr int OFF_Q = 0;                       // [NSLOT][32 x 256 B]
@@ -1052,6 +1058,9 @@ __device__ __forceinline__ void prio(int p) {
 __host__ __device__ inline int n_chunks(int kb, int S, bool causal) {
   const int q0 = causal ? kb * BKVW : 0;
   return (S - q0 + QCH - 1) / QCH;
+}
+__device__ __forceinline__ int tsw(int key) {
+  return KF_FA_DKDV_TSW ? ((key & 3) | ((key & 28) << 1)) : ((key & 31) << 2);
 }
 }  // namespace fb
 
@@ -1432,7 +1441,7 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
           for (int r = 0; r < 16; ++r) {
             const int d = 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hh;
             const int key = 32 * (w & 3) + lr;
-            T[key * 128 + (d ^ ((key & 31) << 2))] = acc[t][r] * mul;
+            T[key * 128 + (d ^ tsw(key))] = acc[t][r] * mul;
           }
       }
       __syncthreads();
@@ -1441,8 +1450,8 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
         const int key = e >> 7, d = e & 127;
         // KF_FA_DKDV_FLUSH: 1 = fp32 atomics (production); 0 = anatomy build without the partial
         // sums (numerics broken); 2 = plain stores instead of atomics (numerics broken)
-        if (KF_FA_DKDV_FLUSH == 1) atomicAdd(dst + (long)key * Hkv * D + d, T[key * 128 + (d ^ ((key & 31) << 2))]);
-        else if (KF_FA_DKDV_FLUSH == 2) dst[(long)key * Hkv * D + d] = T[key * 128 + (d ^ ((key & 31) << 2))];
+        if (KF_FA_DKDV_FLUSH == 1) atomicAdd(dst + (long)key * Hkv * D + d, T[key * 128 + (d ^ tsw(key))]);
+        else if (KF_FA_DKDV_FLUSH == 2) dst[(long)key * Hkv * D + d] = T[key * 128 + (d ^ tsw(key))];
       }
       __syncthreads();
     }
