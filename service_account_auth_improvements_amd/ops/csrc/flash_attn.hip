@@ -530,8 +530,9 @@ __global__ __launch_bounds__(256) void flash_bwd_pre_kernel(const bf16_t* __rest
 // ====================================================================================
 // Backward: dQ (forward-shaped)
 // ====================================================================================
-// Same skeleton as the forward (8 waves x 32 query rows, 4-deep K+V LDS-DMA ring, counted
-// vmcnt + raw barrier).  Per 64-key tile: S'^T = K Q^T - lse/scale and dP'^T = V dO^T - delta
+// Same skeleton as the forward (8 waves x 32 query rows, 128-key K+V stages in a 2-deep LDS-DMA
+// ring, one vmcnt + raw barrier per stage, each stage computed as two 64-key halves).  Per 64-key
+// half: S'^T = K Q^T - lse/scale and dP'^T = V dO^T - delta
 // come out of the MFMA chains with both row constants folded in (hi/lo bf16 split, no
 // accumulator-initialising moves), so dS^T = exp2(c S') * dP' per element; dQ^T += K^T dS^T
 // with the K^T fragments read (inline asm, counted waits) one output block ahead.
