@@ -56,7 +56,8 @@ constexpr int BQ = 128;           // sequence-length granule the launchers requi
 constexpr int BK = 64;            // keys per dQ half-stage (stages hold BKF = 128)
 constexpr int BKV = 128;          // keys per dK/dV workgroup (4 waves x 32)
 constexpr int QT = 32;            // query rows per dK/dV iteration
-constexpr int QCH = 1024;         // query rows per dK/dV work item (512 / 2048: 6 % / 4 % slower)
+constexpr int QCH = 1536;         // query rows per dK/dV work item: 1536 is 1.1 % faster than 1024 and 1280-2048
+                                  // (profiles/fa_fwd128_r5.md; 512: 6 % slower in round 3)
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float LN2 = 0.6931471805599453f;
 
