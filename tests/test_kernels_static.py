@@ -80,3 +80,23 @@ def test_noop_extension_load_does_not_import_cpp_extension():
     out = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, check=True)
     assert out.stdout.split()[0] == "clean", out.stdout + out.stderr
 
+
+
+@pytest.mark.skipif(HIPCC is None, reason="needs hipcc")
+def test_attention_kernels_carry_no_packed_f32_valu():
+    """flash_attn.hip is built without SLP vectorization (ops/_build.py FILE_FLAGS): packed f32
+    adds / multiplies beside the MFMAs cost more issue slots than the scalar ops (attention
+    backward 7.50 -> 7.26 ms, profiles/fa_fwd128_r5.md).  With the build's flags the kernels
+    contain none; with SLP on, hipcc emits ~370."""
+    from service_account_auth_improvements_amd.ops import _build
+    path = os.path.join(CSRC, "flash_attn.hip")
+    flags = ["-O3", "-std=c++17", f"--offload-arch={_build.ARCH}", "-ffp-contract=fast", "-munsafe-fp-atomics",
+             *_build.FILE_FLAGS.get("flash_attn.hip", [])]
+    assert "-fno-slp-vectorize" in flags
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "k.s")
+        subprocess.run([HIPCC, *flags, "--cuda-device-only", "-S", "-o", out, path], check=True,
+                       capture_output=True, text=True)
+        text = open(out).read()
+    packed = re.findall(r"^\s+v_pk_(?:add|mul|fma)_f32\b", text, re.M)
+    assert not packed, len(packed)
