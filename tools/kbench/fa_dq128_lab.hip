@@ -7,6 +7,10 @@
 #ifndef KF_DQ128_OST
 #define KF_DQ128_OST 0
 #endif
+// 1 = s_setprio 1 over the S/dP and dQ MFMA chains, 0 over the exp / pack VALU
+#ifndef KF_DQ128_PRIO
+#define KF_DQ128_PRIO 0
+#endif
 namespace d128 {
 constexpr int BK2 = 128, TILE2 = BK2 * D * 2, NS2 = 2, STG2 = 2 * TILE2;
 static_assert(NS2 * STG2 <= 163840, "LDS");
@@ -112,6 +116,7 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dq128_kernel(
         fv[sl] = rd_b128<d128::TILE2 + 8192 * kt>(a_t ^ (32 * ks));
       };
       static_for<0, QP>([&](auto ic) { rdS(ic); });
+      if (KF_DQ128_PRIO) __builtin_amdgcn_s_setprio(1);
       f32x16 s, dp;
       static_for<0, 16>([&](auto ic) {
         constexpr int i = decltype(ic)::value, kt = i >> 3, ks = i & 7, sl = i % (QP + 1);
@@ -126,6 +131,7 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dq128_kernel(
         s = mfma32(fk[sl], qf[ks], s);
         dp = mfma32(fv[sl], df[ks], dp);
         if constexpr (ks == 7) {
+          if (KF_DQ128_PRIO) __builtin_amdgcn_s_setprio(0);
           if (need_mask) {
             const int ln = (int)lane_id_opaque(), qq = qmin_w + (ln & 31), h4 = 4 * (ln >> 5);
 #pragma unroll
@@ -143,6 +149,7 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dq128_kernel(
             for (int e = 0; e < 4; ++e) u[e] = pack2(s[8 * ss + 2 * e], s[8 * ss + 2 * e + 1]);
             sf[kt][ss] = as_bf16x8(u);
           }
+          if (KF_DQ128_PRIO) __builtin_amdgcn_s_setprio(1);
         }
       });
       const u32 kbase = lds_addr(Ks);
@@ -170,6 +177,7 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dq128_kernel(
 #pragma unroll
           for (int ss = 0; ss < 2; ++ss) dq[t] = mfma32(kf[t & 1][2 * kt + ss], sf[kt][ss], dq[t]);
       }
+      if (KF_DQ128_PRIO) __builtin_amdgcn_s_setprio(0);
     }
     }
     if (j + 1 < ntiles) {
