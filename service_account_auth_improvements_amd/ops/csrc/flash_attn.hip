@@ -641,6 +641,10 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dq_kernel(
         fv[sl] = rd_b128<TILEF + 8192 * kt>(a_t ^ (32 * ks));
       };
       static_for<0, QP>([&](auto ic) { rdS(ic); });
+      // s_setprio 1 over the MFMA chains, 0 over the exp / pack VALU: the SIMD's other wave then
+      // keeps the matrix pipe fed through this wave's softmax (2.72 vs 2.76 ms,
+      // profiles/fa_fwd128_r5.md; the forward measured null)
+      __builtin_amdgcn_s_setprio(1);
       f32x16 s, dp;
       static_for<0, 16>([&](auto ic) {
         constexpr int i = decltype(ic)::value, kt = i >> 3, ks = i & 7, sl = i % (QP + 1);
@@ -655,6 +659,7 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dq_kernel(
         s = mfma32(fk[sl], qf[ks], s);
         dp = mfma32(fv[sl], df[ks], dp);
         if constexpr (ks == 7) {
+          __builtin_amdgcn_s_setprio(0);
           if (need_mask) {
             const int ln = (int)lane_id_opaque(), qq = qmin_w + (ln & 31), h4 = 4 * (ln >> 5);
 #pragma unroll
@@ -672,6 +677,7 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dq_kernel(
             for (int e = 0; e < 4; ++e) u[e] = pack2(s[8 * ss + 2 * e], s[8 * ss + 2 * e + 1]);
             sf[kt][ss] = as_bf16x8(u);
           }
+          __builtin_amdgcn_s_setprio(1);
         }
       });
       const u32 kbase = lds_addr(Ks);
@@ -699,6 +705,7 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dq_kernel(
 #pragma unroll
           for (int ss = 0; ss < 2; ++ss) dq[t] = mfma32(kf[t & 1][2 * kt + ss], sf[kt][ss], dq[t]);
       }
+      __builtin_amdgcn_s_setprio(0);
     }
     }
     if (j + 1 < ntiles) {
