@@ -26,7 +26,7 @@ constexpr int FPK = KF_F128_FP;
 #ifndef KF_F128_OST
 #define KF_F128_OST 0
 #endif
-// 1 = s_setprio 1 over the S chain and the PV MFMAs, 0 over the softmax
+// s_setprio 1 over the S chain (bit 0) and / or the PV MFMAs (bit 1), 0 over the softmax
 #ifndef KF_F128_PRIO
 #define KF_F128_PRIO 0
 #endif       // K row fragments read this many MFMA steps ahead
@@ -180,7 +180,7 @@ __global__ __launch_bounds__(512, 1) void flash_fwd128_kernel(
         }
     };
     v_read(0, vf[0]);
-    if (KF_F128_PRIO) __builtin_amdgcn_s_setprio(1);
+    if (KF_F128_PRIO & 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int gi = 0; gi < 8; ++gi) {
       if (gi < 7) {
@@ -195,7 +195,7 @@ __global__ __launch_bounds__(512, 1) void flash_fwd128_kernel(
 #pragma unroll
         for (int ss = 0; ss < 2; ++ss) o[t] = mfma32(vf[gi & 1][2 * kk + ss], pf[2 * hf + kk][ss], o[t]);
     }
-    if (KF_F128_PRIO) __builtin_amdgcn_s_setprio(0);
+    if (KF_F128_PRIO & 2) __builtin_amdgcn_s_setprio(0);
   };
   auto live_tile = [&](int j) { return live && (!CAUSAL || j * BKF <= qmax_w); };
 
@@ -206,9 +206,9 @@ __global__ __launch_bounds__(512, 1) void flash_fwd128_kernel(
     // into the buffer every wave finished with (tile j-1); KF_F128_LATE=1: after this tile's S chain
     if (!KF_F128_LATE && j + 1 < ntiles) stage(j + 1);
     if (live_tile(j)) {
-      if (KF_F128_PRIO) __builtin_amdgcn_s_setprio(1);
+      if (KF_F128_PRIO & 1) __builtin_amdgcn_s_setprio(1);
       s_chain(j, scp);
-      if (KF_F128_PRIO) __builtin_amdgcn_s_setprio(0);
+      if (KF_F128_PRIO & 1) __builtin_amdgcn_s_setprio(0);
       if (KF_F128_LATE && j + 1 < ntiles) stage(j + 1);
       soft_pv(j, scp);
     } else if (KF_F128_LATE && j + 1 < ntiles) {
