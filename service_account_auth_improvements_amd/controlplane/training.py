@@ -213,14 +213,15 @@ class _JobBase(Controller):
                 restart = rs.get("restartPolicy", "OnFailure")
                 spec["restartPolicy"] = "Never" if restart == "ExitCode" else (
                     "OnFailure" if restart == "OnFailure" else restart)
-                env_add = self._pod_env(job, rtype, i, specs, tpl)
+                env_add = self._pod_env(job, rtype, i, specs, tpl) + _worker_runtime_env(job)
                 for c in spec.get("containers") or []:
                     if c.get("name") in ("pytorch", "mpi", "launcher", "worker") or len(spec["containers"]) == 1:
                         names = {e["name"] for e in c.get("env") or []}
                         c["env"] = list(c.get("env") or []) + [e for e in env_add if e["name"] not in names]
+                ann = dict(tpl.get("metadata", {}).get("annotations") or {})
+                ann.update(_scrape_annotations(job))
                 pod = {"apiVersion": "v1", "kind": "Pod",
-                       "metadata": {"name": pn, "namespace": ns, "labels": labels,
-                                    "annotations": dict(tpl.get("metadata", {}).get("annotations") or {})},
+                       "metadata": {"name": pn, "namespace": ns, "labels": labels, "annotations": ann},
                        "spec": spec}
                 out.append(set_controller_reference(job, pod))
         return out
@@ -681,10 +682,40 @@ class MPIJobReconciler(_JobBase):
                 all(ph in ("Running", "Succeeded") for ph in phases.get("worker", [])))
 
 
+# job annotations the operator turns into worker-runtime settings (runtime/train_entry.py):
+#   kfamd.io/metrics-port    -> KFAMD_METRICS_PORT (rank 0 serves Prometheus /metrics there) and
+#                               the prometheus.io/{scrape,port,path} pod annotations
+#   kfamd.io/checkpoint-dir  -> KFAMD_CKPT_DIR (periodic checkpoints + auto-resume; a PVC path)
+#   kfamd.io/save-every      -> KFAMD_SAVE_EVERY (steps between checkpoints)
+ANN_METRICS_PORT = "kfamd.io/metrics-port"
+ANN_CKPT_DIR = "kfamd.io/checkpoint-dir"
+ANN_SAVE_EVERY = "kfamd.io/save-every"
+
+
+def _worker_runtime_env(job: dict) -> List[dict]:
+    ann = job.get("metadata", {}).get("annotations") or {}
+    env = []
+    for key, var in ((ANN_METRICS_PORT, "KFAMD_METRICS_PORT"), (ANN_CKPT_DIR, "KFAMD_CKPT_DIR"),
+                     (ANN_SAVE_EVERY, "KFAMD_SAVE_EVERY")):
+        if ann.get(key) not in (None, ""):
+            env.append({"name": var, "value": str(ann[key])})
+    return env
+
+
+def _scrape_annotations(job: dict) -> dict:
+    port = (job.get("metadata", {}).get("annotations") or {}).get(ANN_METRICS_PORT)
+    if port in (None, ""):
+        return {}
+    return {"prometheus.io/scrape": "true", "prometheus.io/port": str(port), "prometheus.io/path": "/metrics"}
+
+
 def pytorchjob_manifest(name: str, namespace: str, image: str, command: List[str], n_nodes: int = 1,
                         gpus_per_node: int = 8, master_port: Optional[int] = None,
-                        restart_policy: str = "OnFailure", backoff_limit: int = 3) -> dict:
-    """A PyTorchJob for the kfamd trainer: each replica runs kfamd-launch over its GPUs."""
+                        restart_policy: str = "OnFailure", backoff_limit: int = 3,
+                        metrics_port: Optional[int] = None, ckpt_dir: Optional[str] = None,
+                        save_every: Optional[int] = None) -> dict:
+    """A PyTorchJob for the kfamd trainer: each replica runs kfamd-launch over its GPUs.
+    ``metrics_port`` / ``ckpt_dir`` / ``save_every`` become the job annotations above."""
     def tpl():
         return {"metadata": {"annotations": {"sidecar.istio.io/inject": "false"}},
                 "spec": {"containers": [{"name": "pytorch", "image": image,
@@ -694,6 +725,9 @@ def pytorchjob_manifest(name: str, namespace: str, image: str, command: List[str
     if n_nodes > 1:
         specs["Worker"] = {"replicas": n_nodes - 1, "restartPolicy": restart_policy, "template": tpl()}
     ann = {"kfamd.io/master-port": str(master_port)} if master_port else {}
+    for key, v in ((ANN_METRICS_PORT, metrics_port), (ANN_CKPT_DIR, ckpt_dir), (ANN_SAVE_EVERY, save_every)):
+        if v is not None:
+            ann[key] = str(v)
     return {"apiVersion": PT_API, "kind": "PyTorchJob",
             "metadata": {"name": name, "namespace": namespace, "annotations": ann},
             "spec": {"nprocPerNode": str(gpus_per_node) if gpus_per_node else "1",

@@ -71,11 +71,11 @@ class MnistTrainer:
     def train_step(self, batches):
         """One optimizer step over a list of micro-batches (gradient accumulation)."""
         self.opt.zero_grad(set_to_none=True)
-        tot = 0.0
+        tot = None
         for x, y in batches:
             loss = F.cross_entropy(self.model(x), y) / len(batches)
             loss.backward()
-            tot += float(loss)
+            tot = loss.detach() if tot is None else tot + loss.detach()
         self.opt.step()
         self.step_idx += 1
-        return torch.tensor(tot)
+        return tot

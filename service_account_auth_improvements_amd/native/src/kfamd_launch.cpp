@@ -61,6 +61,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <set>
 #include <sstream>
 #include <string>
 #include <thread>
@@ -241,30 +242,40 @@ struct Assignment {
 // Runs in a background thread for the launcher's lifetime so restarts can re-join.
 struct RdzvServer {
   int fd = -1, nnodes = 1, min_nodes = 1;
-  double last_call = 5.0;
+  double last_call = 5.0, grace = 10.0;
   std::thread th;
-  void start(int port, int nn, int mn, double lc) {
+  void start(int port, int nn, int mn, double lc, double gr) {
     nnodes = nn;
     min_nodes = mn;
     last_call = lc;
+    grace = gr;
     fd = listen_on(port);
     if (fd < 0) return;
     th = std::thread([this] { loop(); });
     th.detach();
   }
   // a round is complete with all nnodes members, or (elastic) with >= min_nodes and no join
-  // for last_call seconds; never without node 0 (global rank 0 and its store live there)
-  bool complete(const std::map<int, std::pair<int, int>>& m, double last_join) const {
+  // for last_call seconds; never without node 0 (global rank 0 and its store live there).
+  // The early (elastic) close also waits for every member of the previous round, for up to
+  // grace + last_call after this round's first JOIN: on a membership change each running agent
+  // stops its workers (SIGTERM, up to --grace seconds) BEFORE it re-joins, so a node whose
+  // workers exit slowly must not be closed out of the round it is about to join.
+  bool complete(const std::map<int, std::pair<int, int>>& m, double last_join, double first_join,
+                const std::set<int>& prev) const {
     if (!m.count(0)) return false;
     if ((int)m.size() >= nnodes) return true;
-    return (int)m.size() >= min_nodes && min_nodes < nnodes && now_s() - last_join >= last_call;
+    if (!((int)m.size() >= min_nodes && min_nodes < nnodes && now_s() - last_join >= last_call)) return false;
+    for (int p : prev)
+      if (!m.count(p)) return first_join >= 0 && now_s() - first_join >= grace + last_call;
+    return true;
   }
   void loop() {
     int round = 0;
+    std::set<int> prev;                            // node ranks of the last closed round
     while (!g_stop) {
       std::map<int, std::pair<int, int>> members;  // node_rank -> (nproc, fd)
-      double last_join = now_s();
-      while (!complete(members, last_join) && !g_stop) {
+      double last_join = now_s(), first_join = -1;
+      while (!complete(members, last_join, first_join, prev) && !g_stop) {
         pollfd pfd{fd, POLLIN, 0};
         if (::poll(&pfd, 1, 100) <= 0) continue;
         int c = ::accept(fd, nullptr, nullptr);
@@ -286,9 +297,12 @@ struct RdzvServer {
         if (members.count(nr)) ::close(members[nr].second);   // a restarted agent re-joins
         members[nr] = {np, c};
         last_join = now_s();
+        if (first_join < 0) first_join = last_join;
       }
       if (g_stop) break;
       ++round;
+      prev.clear();
+      for (auto& m : members) prev.insert(m.first);
       int offset = 0, world = 0;
       for (auto& m : members) world += m.second.first;
       for (auto& m : members) {
@@ -501,7 +515,7 @@ int main(int argc, char** argv) {
   signal(SIGINT, on_signal);
   signal(SIGPIPE, SIG_IGN);
   RdzvServer server;
-  if (a.node_rank == 0) server.start(a.rdzv_port, a.nnodes, a.min_nodes, a.last_call);
+  if (a.node_rank == 0) server.start(a.rdzv_port, a.nnodes, a.min_nodes, a.last_call, a.grace);
   int rc = 1;
   for (int attempt = 0; attempt <= a.max_restarts;) {
     Assignment as;

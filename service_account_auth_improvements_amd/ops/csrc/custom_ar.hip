@@ -113,7 +113,7 @@ __global__ __launch_bounds__(NT) void one_shot_ar_kernel(Peers peers, int rank, 
 //   mode AR: input x[n] -> out[n] (sum)      mode RS: x[n] -> out[n/N] (own chunk of the sum)
 //   mode AG: x[n/N] (own chunk) -> out[n] (concatenation in rank order)
 // Buffer (uncached, IPC-exported, zeroed): [phase-1 flags | phase-2 flags: 2 slots x MAXB x MAXW
-// int32 each][epochs MAXB][err][pad to 16 KB][in: 2 slots x slot_bytes][red: 2 slots x slot_bytes/N]
+// int32 each][epochs MAXB][err][pad to 32 KB][in: 2 slots x slot_bytes][red: 2 slots x slot_bytes/N]
 // Same per-block epoch / two-slot argument as the one-shot kernel: to enter call e a block has
 // seen every peer's call-(e-1) phase-2 flag, so no peer still reads call e-2's slot.
 // Every block's epoch advances once per call, so the communicator keeps ONE grid size for its

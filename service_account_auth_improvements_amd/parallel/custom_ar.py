@@ -117,6 +117,19 @@ def two_shot_blocks(requested: Optional[int], sharing: int, cus: int) -> int:
     return max(1, min(int(requested), TwoShot.MAX_BLOCKS))
 
 
+def uniform_two_shot_blocks(requested: Optional[int], dev_keys: List[tuple], cus: List[int]) -> int:
+    """The ONE block count every rank of a communicator uses.  The kernel splits each chunk by
+    ``gridDim.x`` and pairs its peer flags by ``blockIdx``, so ranks that disagree read peer
+    ranges no peer block wrote (wrong sums) and leave blocks spinning until the wait budget
+    runs out.  Derived only from values every rank gathered -- the most ranks that share any one
+    GPU and the fewest CUs of any rank's GPU -- so an uneven spread (8 ranks on 3 GPUs: 3/3/2)
+    still yields one value."""
+    counts: dict = {}
+    for k in dev_keys:
+        counts[k] = counts.get(k, 0) + 1
+    return two_shot_blocks(requested, max(counts.values()), min(cus))
+
+
 class TwoShot:
     """Two-shot reduce-scatter / all-gather / all-reduce over xGMI (ops/csrc/custom_ar.hip, ts).
 
@@ -167,15 +180,15 @@ class TwoShot:
         props = torch.cuda.get_device_properties(torch.cuda.current_device())
         dev_key = (str(props.uuid), props.pci_domain_id, props.pci_bus_id, props.pci_device_id)
         gathered: List[Optional[tuple]] = [None] * self.world
-        dist.all_gather_object(gathered, (handle, dev_key), group=group)
+        dist.all_gather_object(gathered, (handle, dev_key, props.multi_processor_count), group=group)
         handles = [g[0] for g in gathered]
         # Ranks that share one GPU (the one-GPU multi-process tests and rehearsals): a call's
         # blocks spin on the card until every peer's call arrives, so with W ranks x 128 blocks
         # they can fill every CU and starve a peer's preceding kernels (its attention needs a
         # whole CU's LDS) until the wait budget runs out.  The automatic count is then capped
         # to leave half the CUs free; one rank per GPU (production) keeps the measured 128.
-        sharing = sum(1 for g in gathered if g[1] == dev_key)
-        self.blocks = two_shot_blocks(blocks, sharing, props.multi_processor_count)
+        # Every rank must launch the same count: computed from the gathered values only.
+        self.blocks = uniform_two_shot_blocks(blocks, [g[1] for g in gathered], [g[2] for g in gathered])
         self.ptrs, self._opened = [], []
         for r, h in enumerate(handles):
             if r == self.rank:

@@ -35,7 +35,8 @@ count; the whole 8B gradient is 16 GB -> ~64 buckets.
 """
 from __future__ import annotations
 
-from typing import List, Optional, Tuple
+import time
+from typing import Dict, List, Optional, Tuple
 
 import torch
 import torch.distributed as dist
@@ -43,6 +44,64 @@ import torch.distributed as dist
 from .. import ops
 from ..runtime import progress
 from ..runtime.flat import FlatGroup
+
+
+class CollectiveStats:
+    """Counts, bytes and seconds of the DP collectives, per op (``all_to_all``, ``all_reduce``,
+    ``reduce_scatter``, ``all_gather``) -- the training worker's ``/metrics`` series
+    (runtime/metrics.py).  Bytes are counted at launch on the host.  Seconds come from the
+    communicator's own start/end events (``Work._get_duration``; RCCL records them when
+    ``TORCH_NCCL_ENABLE_TIMING=1``, which the worker sets when metrics are on), or -- for a
+    backend whose ``wait()`` blocks the host (gloo) -- from launch to the return of ``wait()``.
+    Nothing here blocks: :meth:`harvest` folds in only collectives that already finished, so the
+    worker calls it once per step and reads the totals one step late."""
+
+    # bus-bandwidth factor per op at n ranks (the nccl-tests convention: bytes each link carries)
+    _BUS = {"all_reduce": lambda n: 2.0 * (n - 1) / n}
+
+    def __init__(self, world: int, host_timed: bool):
+        self.world = max(1, world)
+        self.host_timed = host_timed
+        self.totals: Dict[str, List[float]] = {}     # op -> [count, bytes, timed seconds, timed bytes]
+        self._open: Dict[int, list] = {}             # id(work) -> [op, bytes, work, t_launch, t_waited]
+
+    def launched(self, op: str, nbytes: int, work):
+        if work is not None:
+            self._open[id(work)] = [op, int(nbytes), work, time.perf_counter(), None]
+
+    def waited(self, work):
+        rec = self._open.get(id(work))
+        if rec is not None and rec[4] is None:
+            rec[4] = time.perf_counter()
+
+    def bus_factor(self, op: str) -> float:
+        n = self.world
+        return self._BUS.get(op, lambda n: (n - 1) / n)(n)
+
+    def harvest(self):
+        for key in list(self._open):
+            op, nb, w, t0, t1 = self._open[key]
+            try:
+                if not w.is_completed():
+                    continue
+            except RuntimeError:
+                continue
+            secs = None
+            try:
+                ms = w._get_duration()          # the communicator's own event pair
+                if ms is not None and ms >= 0:
+                    secs = ms / 1e3
+            except Exception:                   # noqa: BLE001 -- timing off / not supported
+                pass
+            if secs is None and self.host_timed and t1 is not None:
+                secs = t1 - t0
+            tot = self.totals.setdefault(op, [0, 0, 0.0, 0])
+            tot[0] += 1
+            tot[1] += nb
+            if secs is not None:
+                tot[2] += secs
+                tot[3] += nb
+            del self._open[key]
 
 
 class Bucket:
@@ -94,6 +153,7 @@ class GradReducer:
         self.off32: dict = {}
         self.a2a = self.fp32 and self.enabled and mode == "reduce_scatter"
         self._accumulated = False     # accumulate_micro ran in this step
+        self.stats: Optional[CollectiveStats] = None   # set by the worker when /metrics is on
         if self.fp32:
             for g in groups:
                 dev = g.grads.device
@@ -180,8 +240,11 @@ class GradReducer:
         if self.a2a:
             b.recv = torch.empty_like(x)
             b.work = dist.all_to_all_single(b.recv, x, group=self.dp_group, async_op=True)
+            self._note("all_to_all", x, b.work)
         elif self.mode == "allreduce":
-            b.work = dist.all_reduce(main[b.lo:b.hi] if self.fp32 else x, group=self.dp_group, async_op=True)
+            t = main[b.lo:b.hi] if self.fp32 else x
+            b.work = dist.all_reduce(t, group=self.dp_group, async_op=True)
+            self._note("all_reduce", t, b.work)
         else:
             n = (b.hi - b.lo) // self.dp
             r = dist.get_rank(self.dp_group) if self.dp_group is not None else dist.get_rank()
@@ -192,7 +255,16 @@ class GradReducer:
                 b.staged = (out, torch.empty_like(out))
                 out = b.staged[1]
             b.work = dist.reduce_scatter_tensor(out, x, group=self.dp_group, async_op=True)
+            self._note("reduce_scatter", x, b.work)
         self._pending.append(b)
+
+    def _note(self, op: str, t: torch.Tensor, work):
+        if self.stats is not None:
+            self.stats.launched(op, t.numel() * t.element_size(), work)
+
+    def _waited(self, work):
+        if self.stats is not None:
+            self.stats.waited(work)
 
     def grad_ready(self, group: FlatGroup, end_offset: int):
         """Model callback: every gradient of ``group`` below ``end_offset`` is final."""
@@ -207,6 +279,7 @@ class GradReducer:
     def _complete(self, b: Bucket):
         if b.work is not None:
             b.work.wait()
+            self._waited(b.work)
             b.work = None
         if b.staged is not None:
             b.staged[0].copy_(b.staged[1])
@@ -256,8 +329,10 @@ class GradReducer:
                 x = b.group.params[b.lo:b.hi]
                 n = (b.hi - b.lo) // self.dp
                 mine = x[r * n:(r + 1) * n]
-                self._gathers[(name, idx)] = dist.all_gather_into_tensor(
-                    x, mine if in_place else mine.clone(), group=self.dp_group, async_op=True)
+                w = dist.all_gather_into_tensor(x, mine if in_place else mine.clone(), group=self.dp_group,
+                                                async_op=True)
+                self._gathers[(name, idx)] = w
+                self._note("all_gather", x, w)
         if not overlap:
             self.wait_all_params()
 
@@ -270,10 +345,12 @@ class GradReducer:
                 w = self._gathers.pop((group.name, idx), None)
                 if w is not None:
                     w.wait()
+                    self._waited(w)
 
     def wait_all_params(self):
         for w in self._gathers.values():
             w.wait()
+            self._waited(w)
         self._gathers = {}
 
     def broadcast_params(self, src_global_rank: int = 0):

@@ -524,6 +524,7 @@ class PipelineTrainer:
             T //= st.tp                     # stages exchange this rank's block of token rows
         self.p2p = P2P(st, (T, mcfg.hidden), torch.bfloat16, st.device)
         self.step_idx = 0          # optimizer steps taken (restored by load_checkpoint)
+        self.pre_opt_waits: list = []   # asynchronous checkpoint snapshots (runtime/checkpoint.py)
 
     def _hook(self, on: bool, model=None):
         (model if model is not None else self.model).on_grad_ready = self.reducer.grad_ready if on else None
@@ -538,6 +539,8 @@ class PipelineTrainer:
             loss = one_f_one_b(self.model, self.p2p, micro_batches, 1.0 / ntok, self._hook, reducer=self.reducer)
         self.reducer.wait_all_params()     # a bucket the forward never read (padding) must land too
         self.reducer.finish()
+        from ..runtime.trainer import wait_pre_opt
+        wait_pre_opt(self)
         self.opt.step(grad_scale=1.0 / self.st.dp)
         self.reducer.all_gather_params(overlap=self.overlap_allgather)
         self.step_idx += 1

@@ -13,20 +13,94 @@ Layout of a checkpoint directory::
 Each file holds the flat bf16 parameter buffers of its stage/TP shard (``param/<group>``)
 and its optimizer shard(s) (``opt/<group>/<lo>-<hi>/{master,m,v}``).  Without ZeRO only
 dp rank 0 writes (replicas are identical); with ZeRO-1 every dp rank writes its slices.
-Tensors are written straight from device memory via safetensors (no pickling), and are
-loaded with the safe loader only.
+Files are written by a streaming writer (the safetensors format: an 8-byte header length, a
+JSON header, the raw tensor bytes -- straight from host memory, no serialisation copy, then
+fsync) and loaded with the safe loader only.
+
+Periodic checkpoint-restart (:class:`PeriodicCheckpointer`, worker flags ``--ckpt-dir`` /
+``--save-every``) -- the data-plane counterpart of the reference's level-triggered recovery,
+where controller state lives in the API object and survives restarts
+(/root/reference/components/notebook-controller/controllers/culling_controller.go:50-52):
+
+    <ckpt-dir>/step-00000040/...   one checkpoint directory per save (the layout above)
+    <ckpt-dir>/latest              name of the newest COMPLETE one, replaced atomically
+
+* the step's state is snapshotted into pinned host buffers on a side stream (the next step's
+  forward/backward runs meanwhile; only its optimizer update waits for the copy to finish),
+  and a writer thread streams the files out and fsyncs them;
+* every rank then drops a ``rank{r}.done`` marker carrying this world's save token; rank 0
+  publishes ``latest`` (tmp file, fsync, ``os.replace``) only once EVERY rank's marker is
+  there, so a world killed mid-save leaves the previous ``latest`` in place;
+* on (re)start every rank resumes from ``latest`` (an elastic restart or an OnFailure pod
+  restart loses at most ``--save-every`` steps), and a changed data-parallel world re-shards
+  the ZeRO-1 optimizer state by flat-range overlap (:func:`load_checkpoint`); a changed TP/PP
+  layout is refused with a clear error.
 """
 from __future__ import annotations
 
 import json
 import os
-from typing import Optional
+import re
+import struct
+import threading
+import time
+import uuid
+from typing import Dict, List, Optional, Tuple
 
 import torch
+
+LATEST = "latest"
+_STEP_DIR = re.compile(r"^step-(\d+)$")
+_OPT_KEY = re.compile(r"^opt/(.+)/(\d+)-(\d+)/(master|m|v)$")
+_ST_DTYPE = {torch.bfloat16: "BF16", torch.float32: "F32", torch.float16: "F16", torch.float64: "F64",
+             torch.int64: "I64", torch.int32: "I32", torch.int16: "I16", torch.int8: "I8",
+             torch.uint8: "U8", torch.bool: "BOOL"}
 
 
 def _fname(st) -> str:
     return f"tp{st.tp_rank}-pp{st.pp_rank}-dp{st.dp_rank}.safetensors"
+
+
+def _fsync_dir(path: str):
+    try:
+        fd = os.open(path, os.O_RDONLY)
+    except OSError:
+        return
+    try:
+        os.fsync(fd)
+    except OSError:
+        pass
+    finally:
+        os.close(fd)
+
+
+def write_safetensors(path: str, tensors: Dict[str, torch.Tensor], metadata: Optional[dict] = None):
+    """Stream CPU tensors into a safetensors file: header, then each tensor's bytes written
+    straight from its memory (no bytes copy of a 30 GB master shard), fsync, atomic rename."""
+    header, off, order = {}, 0, []
+    for k in sorted(tensors):
+        t = tensors[k]
+        if t.device.type != "cpu":
+            raise ValueError(f"{k}: write_safetensors takes host tensors")
+        n = t.numel() * t.element_size()
+        header[k] = {"dtype": _ST_DTYPE[t.dtype], "shape": list(t.shape), "data_offsets": [off, off + n]}
+        order.append(k)
+        off += n
+    if metadata:
+        header["__metadata__"] = {str(a): str(b) for a, b in metadata.items()}
+    hb = json.dumps(header, separators=(",", ":")).encode()
+    hb += b" " * (-len(hb) % 8)
+    tmp = path + ".tmp"
+    with open(tmp, "wb") as f:
+        f.write(struct.pack("<Q", len(hb)))
+        f.write(hb)
+        for k in order:
+            t = tensors[k].contiguous()
+            if t.numel():
+                f.write(memoryview(t.reshape(-1).view(torch.uint8).numpy()))
+        f.flush()
+        os.fsync(f.fileno())
+    os.replace(tmp, path)
 
 
 def _rank_state(data) -> dict:
@@ -57,22 +131,47 @@ def _rank() -> int:
     return dist.get_rank() if dist.is_initialized() else 0
 
 
+def _world() -> int:
+    import torch.distributed as dist
+    return dist.get_world_size() if dist.is_initialized() else 1
+
+
+def tp_check_all(st):
+    """Read the two-shot TP communicator's error word (a host sync) and fail EVERY rank of the
+    TP group together when any one of them timed out (a timed-out block sets only its
+    own rank's word, so without the MAX the healthy ranks would walk into the checkpoint's
+    collectives and hang until the process-group timeout)."""
+    comm = getattr(st, "tp_comm", None)
+    if comm is None:
+        return
+    import torch.distributed as dist
+    err = 0
+    try:
+        comm.check(sync=True)
+    except RuntimeError:
+        err = 1
+    if st.tp > 1 and dist.is_initialized():
+        t = torch.tensor([err], dtype=torch.int32, device=st.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=st.tp_group)
+        err = int(t.item())
+    if err:
+        comm._raise()
+
+
 def save_module_checkpoint(path: str, trainer, step: int, data=None, extra: Optional[dict] = None):
     """Checkpoint for plain nn.Module jobs (the MNIST plumbing job): module weights and the
     optimizer's per-parameter buffers, written by rank 0 (DDP replicas are identical)."""
-    from safetensors.torch import save_file
     import torch.distributed as dist
     os.makedirs(path, exist_ok=True)
     rank = _rank()
-    save_file({k: v.contiguous().cpu() for k, v in _rank_state(data).items()},
-              os.path.join(path, f"rank{rank}.state.safetensors"))
+    write_safetensors(os.path.join(path, f"rank{rank}.state.safetensors"),
+                      {k: v.contiguous().cpu() for k, v in _rank_state(data).items()})
     if rank == 0:
-        save_file({k: v.contiguous().cpu() for k, v in trainer.state_tensors().items()},
-                  os.path.join(path, "module.safetensors"))
+        write_safetensors(os.path.join(path, "module.safetensors"),
+                          {k: v.contiguous().cpu() for k, v in trainer.state_tensors().items()})
         meta = {"step": int(step), "format": "kfamd-module-v1"}
         meta.update(extra or {})
-        with open(os.path.join(path, "meta.json"), "w") as f:
-            json.dump(meta, f)
+        _write_json(os.path.join(path, "meta.json"), meta)
     if dist.is_initialized():
         dist.barrier()
 
@@ -86,51 +185,85 @@ def load_module_checkpoint(path: str, trainer, data=None) -> dict:
     return meta
 
 
+def _write_json(path: str, obj):
+    tmp = path + ".tmp"
+    with open(tmp, "w") as f:
+        json.dump(obj, f)
+        f.flush()
+        os.fsync(f.fileno())
+    os.replace(tmp, path)
+
+
+def _flat_state(trainer) -> Tuple[Dict[str, torch.Tensor], dict]:
+    """This rank's unique device state (the tensors of its shard file) and the meta record."""
+    st, opt = trainer.st, trainer.opt
+    tensors = {}
+    if st.dp_rank == 0:
+        for g in trainer.model.groups:
+            tensors[f"param/{g.name}"] = g.params.detach()
+    if opt.sharded or st.dp_rank == 0:
+        for sh in opt.shards:
+            k = f"opt/{sh.group.name}/{sh.lo}-{sh.hi}"
+            tensors[k + "/master"] = sh.master
+            tensors[k + "/m"] = sh.m
+            tensors[k + "/v"] = sh.v
+    meta = {"step": opt.step_count, "model": trainer.mcfg.__dict__,
+            "parallel": {"tp": st.tp, "pp": st.pp, "dp": st.dp, "zero1": opt.sharded},
+            "format": "kfamd-flat-v2"}
+    return tensors, meta
+
+
 def save_checkpoint(path: str, trainer, extra: Optional[dict] = None, data=None):
-    """Every rank calls this.  ``data`` (the rank's batch stream) has its generator state saved
-    so resume continues the stream instead of replaying it."""
-    from safetensors.torch import save_file
+    """Every rank calls this (synchronous; the periodic path is :class:`PeriodicCheckpointer`).
+    ``data`` (the rank's batch stream) has its generator state saved so resume continues the
+    stream instead of replaying it."""
     import torch.distributed as dist
     if not hasattr(trainer, "model") or not hasattr(trainer.model, "groups"):
         return save_module_checkpoint(path, trainer, getattr(trainer, "step_idx", 0), data, extra)
     st = trainer.st
     if hasattr(trainer, "sync_params"):
         trainer.sync_params()        # land in-flight ZeRO-1 parameter gathers first
-    if getattr(st, "tp_comm", None) is not None:
-        st.tp_comm.check(sync=True)  # never persist state a timed-out TP collective produced
+    tp_check_all(st)                 # never persist state a timed-out TP collective produced
     os.makedirs(path, exist_ok=True)
-    opt = trainer.opt
-    writes_params = st.dp_rank == 0
-    writes_opt = opt.sharded or st.dp_rank == 0
-    tensors = {}
-    if writes_params:
-        for g in trainer.model.groups:
-            tensors[f"param/{g.name}"] = g.params.detach().contiguous()
-    if writes_opt:
-        for sh in opt.shards:
-            k = f"opt/{sh.group.name}/{sh.lo}-{sh.hi}"
-            tensors[k + "/master"] = sh.master
-            tensors[k + "/m"] = sh.m
-            tensors[k + "/v"] = sh.v
+    tensors, meta = _flat_state(trainer)
     if tensors:
-        save_file({k: v.cpu() for k, v in tensors.items()}, os.path.join(path, _fname(st)))
-    save_file({k: v.contiguous().cpu() for k, v in _rank_state(data).items()},
-              os.path.join(path, f"rank{st.rank}.state.safetensors"))
+        write_safetensors(os.path.join(path, _fname(st)), {k: v.contiguous().cpu() for k, v in tensors.items()})
+    write_safetensors(os.path.join(path, f"rank{st.rank}.state.safetensors"),
+                      {k: v.contiguous().cpu() for k, v in _rank_state(data).items()})
     if dist.is_initialized():
         dist.barrier()
     if st.rank == 0:
-        meta = {"step": opt.step_count, "model": trainer.mcfg.__dict__,
-                "parallel": {"tp": st.tp, "pp": st.pp, "dp": st.dp, "zero1": opt.sharded},
-                "format": "kfamd-flat-v2"}
         meta.update(extra or {})
-        with open(os.path.join(path, "meta.json"), "w") as f:
-            json.dump(meta, f)
+        _write_json(os.path.join(path, "meta.json"), meta)
     if dist.is_initialized():
         dist.barrier()
 
 
+def _opt_sources(path: str, st) -> List[Tuple[str, str, int, int, str]]:
+    """Every optimizer range stored for this (tp, pp) shard by ANY dp rank of the saving world:
+    (file, group, lo, hi, key prefix)."""
+    from safetensors import safe_open
+    out = []
+    pre = f"tp{st.tp_rank}-pp{st.pp_rank}-dp"
+    for fn in sorted(os.listdir(path)):
+        if not (fn.startswith(pre) and fn.endswith(".safetensors")):
+            continue
+        f = os.path.join(path, fn)
+        with safe_open(f, framework="pt", device="cpu") as h:
+            for k in h.keys():
+                m = _OPT_KEY.match(k)
+                if m and m.group(4) == "master":
+                    out.append((f, m.group(1), int(m.group(2)), int(m.group(3)), k[:-len("/master")]))
+    return out
+
+
 def load_checkpoint(path: str, trainer, data=None) -> dict:
-    from safetensors.torch import load_file
+    """Restore params, optimizer state, step, RNG and data position.  The optimizer shards of
+    this rank are filled by flat-range overlap with whatever ranges the saving world stored, so
+    a checkpoint written at one data-parallel size (or with / without ZeRO-1) resumes at another:
+    ZeRO-1 state is re-sharded, elements past the saved (padded) length are zero.  A different
+    TP or PP layout cannot be re-sharded this way and is refused."""
+    from safetensors import safe_open
     if not hasattr(trainer, "model") or not hasattr(trainer.model, "groups"):
         return load_module_checkpoint(path, trainer, data)
     st = trainer.st
@@ -138,23 +271,40 @@ def load_checkpoint(path: str, trainer, data=None) -> dict:
         meta = json.load(f)
     p = meta["parallel"]
     if (p["tp"], p["pp"]) != (st.tp, st.pp):
-        raise ValueError(f"checkpoint layout tp{p['tp']}/pp{p['pp']} != current tp{st.tp}/pp{st.pp}")
+        raise ValueError(f"checkpoint {path}: layout tp{p['tp']}/pp{p['pp']} != current tp{st.tp}/pp{st.pp}; "
+                         "TP/PP re-sharding is not supported -- resume with the saving layout")
     dev = trainer.model.groups[0].params.device
     pfile = os.path.join(path, f"tp{st.tp_rank}-pp{st.pp_rank}-dp0.safetensors")
-    ptens = load_file(pfile, device="cpu")
-    for g in trainer.model.groups:
-        g.params.copy_(ptens[f"param/{g.name}"].to(dev))
-    opt = trainer.opt
-    ofile = os.path.join(path, _fname(st) if p.get("zero1") else os.path.basename(pfile))
-    otens = ptens if ofile == pfile else load_file(ofile, device="cpu")
-    for sh in opt.shards:
-        k = f"opt/{sh.group.name}/{sh.lo}-{sh.hi}"
-        if k + "/master" not in otens:
-            raise KeyError(f"optimizer shard {k} not in {ofile}")
-        sh.master.copy_(otens[k + "/master"].to(dev))
-        sh.m.copy_(otens[k + "/m"].to(dev))
-        sh.v.copy_(otens[k + "/v"].to(dev))
-    opt.step_count = int(meta["step"])
+    with safe_open(pfile, framework="pt", device="cpu") as h:
+        for g in trainer.model.groups:
+            src = h.get_slice(f"param/{g.name}")
+            n = min(src.get_shape()[0], g.numel)
+            g.params[:n].copy_(src[:n].to(dev))
+            if n < g.numel:
+                g.params[n:].zero_()
+    sources = _opt_sources(path, st)
+    handles = {}
+    try:
+        for sh in trainer.opt.shards:
+            filled = 0
+            for buf in (sh.master, sh.m, sh.v):
+                buf.zero_()
+            for f, gname, lo, hi, pre in sources:
+                if gname != sh.group.name or hi <= sh.lo or lo >= sh.hi:
+                    continue
+                a, b = max(lo, sh.lo), min(hi, sh.hi)
+                h = handles.get(f) or handles.setdefault(f, safe_open(f, framework="pt", device="cpu"))
+                for suf, buf in (("master", sh.master), ("m", sh.m), ("v", sh.v)):
+                    buf[a - sh.lo:b - sh.lo].copy_(h.get_slice(f"{pre}/{suf}")[a - lo:b - lo].to(dev))
+                filled += b - a
+            saved_len = max((hi for _, gname, _, hi, _ in sources if gname == sh.group.name), default=0)
+            need = min(sh.hi, saved_len) - min(sh.lo, saved_len)
+            if filled < need:
+                raise KeyError(f"optimizer range {sh.group.name}[{sh.lo}, {sh.hi}) is not covered by {path}")
+    finally:
+        for h in handles.values():
+            h.__exit__(None, None, None)
+    trainer.opt.step_count = int(meta["step"])
     if hasattr(trainer, "step_idx"):
         trainer.step_idx = int(meta["step"])
     _restore_rank_state(path, st.rank, data)
@@ -179,3 +329,175 @@ def load_params(model, path: str) -> dict:
                 raise ValueError(f"param/{g.name}: {t.numel()} elements, model expects {g.params.numel()}")
             g.params.copy_(t.to(g.params.device))
     return meta
+
+
+# ---------------------------------------------------------------- periodic checkpoint-restart
+
+def latest_checkpoint(root: str) -> Optional[str]:
+    """The newest COMPLETE checkpoint under ``root`` (the one ``latest`` names), or None."""
+    try:
+        with open(os.path.join(root, LATEST)) as f:
+            name = f.read().strip()
+    except OSError:
+        return None
+    path = os.path.join(root, name)
+    return path if name and os.path.exists(os.path.join(path, "meta.json")) else None
+
+
+def step_dir(root: str, step: int) -> str:
+    return os.path.join(root, f"step-{step:08d}")
+
+
+class PeriodicCheckpointer:
+    """Asynchronous periodic checkpoints with an atomically published ``latest`` (module doc).
+
+    ``save(step)`` returns once the snapshot is queued: on a GPU the device-to-host copies run
+    on a side stream into pinned buffers that are allocated once and reused, and the trainer's
+    NEXT optimizer update stream-waits for them (``trainer.pre_opt_waits``) -- the only point
+    where the step can be slowed.  A writer thread streams the files out; rank 0 publishes."""
+
+    def __init__(self, root: str, trainer, data=None, keep: int = 2, publish_timeout: float = 1800.0,
+                 on_published=None):
+        import torch.distributed as dist
+        self.root, self.trainer, self.data = root, trainer, data
+        self.keep = max(1, int(keep))
+        self.publish_timeout = publish_timeout
+        self.on_published = on_published
+        self.rank, self.world = _rank(), _world()
+        self.flat = hasattr(trainer, "model") and hasattr(trainer.model, "groups")
+        st = getattr(trainer, "st", None)
+        self.device = getattr(st, "device", torch.device("cpu")) if st is not None else torch.device("cpu")
+        # one token per world: a rank's done marker left by a killed earlier world for the same
+        # step number is never mistaken for this world's
+        tok = [uuid.uuid4().hex if self.rank == 0 else None]
+        if dist.is_initialized() and self.world > 1:
+            dist.broadcast_object_list(tok, src=0)
+        self.token = tok[0]
+        os.makedirs(root, exist_ok=True)
+        self._pinned: Dict[str, torch.Tensor] = {}
+        self._stream = torch.cuda.Stream(device=self.device) if self.device.type == "cuda" else None
+        self._thread: Optional[threading.Thread] = None
+        self._error: Optional[BaseException] = None
+        self.last_published: Optional[int] = None
+        self.last_seconds: Optional[float] = None
+        self.snapshot_seconds: Optional[float] = None
+
+    # -- snapshot (caller's thread)
+    def _host_copy(self, key: str, t: torch.Tensor) -> torch.Tensor:
+        if self._stream is None:
+            return t.detach().contiguous().clone()
+        buf = self._pinned.get(key)
+        if buf is None or buf.shape != t.shape or buf.dtype != t.dtype:
+            buf = self._pinned[key] = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+        buf.copy_(t.detach(), non_blocking=True)
+        return buf
+
+    def save(self, step: int):
+        """Snapshot the state after optimizer step ``step`` and write it in the background."""
+        self.wait()                       # the previous write owns the pinned buffers
+        tr = self.trainer
+        t0 = time.perf_counter()
+        path = step_dir(self.root, step)
+        if not self.flat:                 # plain nn.Module jobs (MNIST): small, synchronous
+            save_module_checkpoint(path, tr, step, self.data)
+            self._done_marker(path)
+            if self.rank == 0:
+                self._publish(path, step, t0)
+            return
+        if hasattr(tr, "sync_params"):
+            tr.sync_params()              # in-flight ZeRO-1 parameter gathers land first
+        tp_check_all(tr.st)
+        tensors, meta = _flat_state(tr)
+        rank_state = {k: v.contiguous().clone() for k, v in _rank_state(self.data).items()}
+        host = {}
+        ev = None
+        if self._stream is not None:
+            self._stream.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(self._stream):
+                for k, v in tensors.items():
+                    host[k] = self._host_copy(k, v)
+            ev = torch.cuda.Event()
+            ev.record(self._stream)
+            # the next optimizer update rewrites master / m / v / params: it waits for the copy
+            waits = getattr(tr, "pre_opt_waits", None)
+            if waits is not None:
+                waits.append(ev)
+            else:
+                ev.synchronize()
+        else:
+            host = {k: self._host_copy(k, v) for k, v in tensors.items()}
+        self.snapshot_seconds = time.perf_counter() - t0
+        fname = _fname(tr.st)
+        self._thread = threading.Thread(target=self._write, name="kfamd-ckpt-writer", daemon=True,
+                                        args=(path, step, fname, host, rank_state, meta, ev, t0))
+        self._thread.start()
+
+    # -- writer thread
+    def _write(self, path, step, fname, host, rank_state, meta, ev, t0):
+        try:
+            if ev is not None:
+                ev.synchronize()
+            os.makedirs(path, exist_ok=True)
+            if host:
+                write_safetensors(os.path.join(path, fname), host)
+            write_safetensors(os.path.join(path, f"rank{self.rank}.state.safetensors"), rank_state)
+            if self.rank == 0:
+                _write_json(os.path.join(path, "meta.json"), meta)
+            self._done_marker(path)
+            if self.rank == 0:
+                self._publish(path, step, t0)
+        except BaseException as e:        # noqa: BLE001 -- surfaced by wait() on the main thread
+            self._error = e
+
+    def _done_marker(self, path: str):
+        _fsync_dir(path)
+        _write_json(os.path.join(path, f"rank{self.rank}.done"), {"token": self.token})
+
+    def _all_done(self, path: str) -> bool:
+        for r in range(self.world):
+            try:
+                with open(os.path.join(path, f"rank{r}.done")) as f:
+                    if json.load(f).get("token") != self.token:
+                        return False
+            except (OSError, ValueError):
+                return False
+        return True
+
+    def _publish(self, path: str, step: int, t0: float):
+        deadline = time.time() + self.publish_timeout
+        while not self._all_done(path):
+            if time.time() > deadline:
+                raise TimeoutError(f"checkpoint {path}: not every rank finished within {self.publish_timeout:.0f} s")
+            time.sleep(0.05)
+        _fsync_dir(path)
+        tmp = os.path.join(self.root, LATEST + ".tmp")
+        with open(tmp, "w") as f:
+            f.write(os.path.basename(path) + "\n")
+            f.flush()
+            os.fsync(f.fileno())
+        os.replace(tmp, os.path.join(self.root, LATEST))
+        _fsync_dir(self.root)
+        self.last_published = step
+        self.last_seconds = time.perf_counter() - t0
+        self._prune(os.path.basename(path))
+        if self.on_published is not None:
+            self.on_published(step, self.last_seconds)
+
+    def _prune(self, newest: str):
+        import shutil
+        dirs = sorted(d for d in os.listdir(self.root) if _STEP_DIR.match(d))
+        done = [d for d in dirs if d <= newest]
+        for d in done[:-self.keep]:
+            shutil.rmtree(os.path.join(self.root, d), ignore_errors=True)
+
+    def wait(self):
+        """Block until the in-flight write (if any) has finished; re-raise its error."""
+        if self._thread is not None:
+            self._thread.join()
+            self._thread = None
+        if self._error is not None:
+            e, self._error = self._error, None
+            raise RuntimeError(f"checkpoint write failed: {e}") from e
+
+    def close(self):
+        self.wait()

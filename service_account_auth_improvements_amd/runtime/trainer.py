@@ -117,6 +117,9 @@ class Trainer:
         self._sync()
         self.init_times["optimizer_state_s"] = time.time() - t0
         self.step_idx = 0
+        # events the next optimizer update must stream-wait for: an asynchronous checkpoint's
+        # device-to-host snapshot of the state that update rewrites (runtime/checkpoint.py)
+        self.pre_opt_waits: list = []
         self._opt_stream = None
         self._segments = None
         if mode == "reduce_scatter" and tcfg.overlap_allgather:
@@ -189,6 +192,7 @@ class Trainer:
         self.model.on_grad_ready = None
         self.reducer.wait_all_params()     # a bucket the forward never read (padding) must land too
         self.reducer.finish()
+        wait_pre_opt(self, self._opt_stream)
         self.opt.step(grad_scale=1.0 / self.st.dp, segments=self._segments, stream=self._opt_stream)
         self.reducer.all_gather_params(overlap=self.tcfg.overlap_allgather)
         self.step_idx += 1
@@ -197,6 +201,18 @@ class Trainer:
             # (and the job) instead of training on it
             self.st.tp_comm.check()
         return total
+
+
+def wait_pre_opt(trainer, extra_stream=None):
+    """Stream-wait (never a host wait) for the events queued in ``trainer.pre_opt_waits``."""
+    if not trainer.pre_opt_waits:
+        return
+    cur = torch.cuda.current_stream()
+    for ev in trainer.pre_opt_waits:
+        cur.wait_event(ev)
+        if extra_stream is not None:
+            extra_stream.wait_event(ev)
+    trainer.pre_opt_waits = []
 
 
 class SyntheticData:

@@ -56,24 +56,26 @@ def _free_port_pair():
 
 
 class Agents:
-    def __init__(self, tmp_path, nnodes="1:3", iters=60, last_call=1.0, rdzv_timeout=60.0, step_s=0.1):
+    def __init__(self, tmp_path, nnodes="1:3", iters=60, last_call=1.0, rdzv_timeout=60.0, step_s=0.1,
+                 grace=3.0, worker=WORKER):
         self.exe = native.binary("kfamd_launch")
         self.out = tmp_path / "records.jsonl"
         self.script = tmp_path / "worker.py"
-        self.script.write_text(WORKER)
+        self.script.write_text(worker)
+        self.grace = grace
         self.port = _free_port_pair()
         self.nnodes, self.iters, self.last_call, self.rdzv_timeout = nnodes, iters, last_call, rdzv_timeout
         self.step_s = step_s
         self.logs = tmp_path
         self.procs = {}
 
-    def start(self, node: int, tag: str):
-        env = dict(os.environ, AGENT_TAG=tag, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
+    def start(self, node: int, tag: str, **extra_env):
+        env = dict(os.environ, AGENT_TAG=tag, PYTHONPATH=ROOT, OMP_NUM_THREADS="1", **extra_env)
         for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
             env.pop(k, None)
         cmd = [self.exe, "--nnodes", self.nnodes, "--node-rank", str(node), "--nproc-per-node", "1",
                "--master-addr", "127.0.0.1", "--master-port", str(self.port), "--max-restarts", "3",
-               "--rdzv-last-call", str(self.last_call), "--rdzv-timeout", str(self.rdzv_timeout), "--grace", "3",
+               "--rdzv-last-call", str(self.last_call), "--rdzv-timeout", str(self.rdzv_timeout), "--grace", str(self.grace),
                "--", sys.executable, str(self.script), str(self.out), str(self.iters), str(self.step_s)]
         log = open(self.logs / f"agent_{tag}.log", "w")
         self.procs[tag] = subprocess.Popen(cmd, env=env, stdout=log, stderr=subprocess.STDOUT)
@@ -193,5 +195,53 @@ def test_losing_node0_without_replacement_fails_after_the_rendezvous_timeout(tmp
         rcs = ag.wait_all(["n1", "n2"], timeout=90)
         assert rcs == {"n1": 3, "n2": 3}, (rcs, ag.log("n1"), ag.log("n2"))
         assert time.time() - t0 < 60
+    finally:
+        ag.stop()
+
+
+SLOW_EXIT_WORKER = r"""
+import datetime, json, os, signal, sys, time
+import torch, torch.distributed as dist
+node, rnd = int(os.environ["NODE_RANK"]), int(os.environ["KFAMD_RDZV_ROUND"])
+delay = float(os.environ.get("EXIT_DELAY", "0"))
+def on_term(*_):                 # a GPU worker tearing down (HBM release, RCCL abort) takes a while
+    time.sleep(delay)
+    os._exit(143)
+signal.signal(signal.SIGTERM, on_term)
+dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=60))
+r, w = dist.get_rank(), dist.get_world_size()
+with open(sys.argv[1], "a") as f:
+    f.write(json.dumps({"round": rnd, "rank": r, "world": w, "node": node, "agent": os.environ["AGENT_TAG"]}) + "\n")
+for i in range(int(sys.argv[2])):
+    if node == 2 and rnd == 1 and i == 5:
+        os._exit(1)              # node 2's worker crashes once
+    if i == 0 or i == int(sys.argv[2]) - 1:
+        t = torch.ones(1)        # collectives at the ends only: in between a long compute phase,
+        dist.all_reduce(t)       # so the peers learn of the crash from their agents' SIGTERM
+    time.sleep(float(sys.argv[3]))
+dist.destroy_process_group()
+"""
+
+
+@pytest.mark.slow
+def test_slowly_exiting_workers_do_not_miss_the_restart_round(tmp_path):
+    """on a membership change an agent stops its workers (SIGTERM, up to --grace)
+    before it re-joins.  Node 1's worker takes 3 s to exit, longer than the 1 s last-call period:
+    the server must wait for the previous round's members (up to grace + last call), so the
+    restart round is ONE world of all three -- not a world {0, 2} closed without node 1 and
+    then a second, free restart of everyone when node 1's late JOIN arrives."""
+    ag = Agents(tmp_path, nnodes="2:3", iters=40, last_call=1.0, grace=6.0, worker=SLOW_EXIT_WORKER)
+    try:
+        ag.start(0, "n0")
+        ag.start(1, "n1", EXIT_DELAY="3.0")
+        ag.start(2, "n2")
+        rcs = ag.wait_all(["n0", "n1", "n2"], timeout=150)
+        logs = {t: ag.log(t) for t in ("n0", "n1", "n2")}
+        assert rcs == {"n0": 0, "n1": 0, "n2": 0}, (rcs, logs)
+        rounds = {}
+        for x in ag.records():
+            rounds.setdefault(x["round"], set()).add((x["node"], x["world"]))
+        assert sorted(rounds) == [1, 2], (rounds, logs)            # exactly one restart round
+        assert rounds[2] == {(0, 3), (1, 3), (2, 3)}, (rounds, logs)
     finally:
         ag.stop()

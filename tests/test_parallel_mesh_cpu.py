@@ -310,3 +310,16 @@ def test_two_shot_block_count():
     assert two_shot_blocks(None, 2, 256) == 64
     assert two_shot_blocks(64, 4, 256) == 64 and two_shot_blocks(1000, 1, 256) == TwoShot.MAX_BLOCKS
     assert two_shot_blocks(None, 1024, 256) == 1
+
+
+def test_two_shot_block_count_is_uniform_over_uneven_gpu_sharing():
+    """every rank must launch the same block count.  8 ranks on 3 GPUs (3/3/2) and
+    mixed CU counts give ONE value on every rank, from the gathered keys only."""
+    from service_account_auth_improvements_amd.parallel.custom_ar import uniform_two_shot_blocks
+    keys = ["g0", "g0", "g0", "g1", "g1", "g1", "g2", "g2"]
+    cus = [256] * 8
+    per_rank = {uniform_two_shot_blocks(None, keys, cus) for _ in range(8)}
+    assert per_rank == {256 // (2 * 3)}
+    assert uniform_two_shot_blocks(None, ["a", "b"], [256, 240]) == 128      # one rank per GPU
+    assert uniform_two_shot_blocks(None, ["a", "a", "b", "b"], [256, 256, 240, 240]) == 240 // 4
+    assert uniform_two_shot_blocks(32, keys, cus) == 32

@@ -50,6 +50,24 @@ def test_pytorchjob_pods_env_and_status(cl):
     assert c.get("v1", "Pod", "llama-worker-0", "team")["status"]["phase"] == "Pending"
 
 
+def test_pytorchjob_metrics_and_checkpoint_annotations_reach_the_workers(cl):
+    """kfamd.io/metrics-port -> KFAMD_METRICS_PORT + prometheus.io scrape annotations on every
+    pod; kfamd.io/checkpoint-dir / save-every -> the worker's periodic checkpoint-restart env."""
+    srv, c, mgr, _ = cl
+    c.create(training.pytorchjob_manifest("obs", "team", "kfamd/trainer:rocm", ["python", "-c", "pass"],
+                                          n_nodes=1, gpus_per_node=1, metrics_port=9400,
+                                          ckpt_dir="/mnt/ckpt/obs", save_every=50))
+    mgr.run_until_idle()
+    p = c.get("v1", "Pod", "obs-master-0", "team")
+    env = {e["name"]: e["value"] for e in p["spec"]["containers"][0]["env"]}
+    assert env["KFAMD_METRICS_PORT"] == "9400"
+    assert env["KFAMD_CKPT_DIR"] == "/mnt/ckpt/obs" and env["KFAMD_SAVE_EVERY"] == "50"
+    ann = p["metadata"]["annotations"]
+    assert ann["prometheus.io/scrape"] == "true" and ann["prometheus.io/port"] == "9400"
+    assert ann["prometheus.io/path"] == "/metrics"
+    assert ann["sidecar.istio.io/inject"] == "false"          # the template's own annotation kept
+
+
 def test_pytorchjob_failure_restart_and_backoff(cl):
     srv, c, mgr, _ = cl
     c.create(training.pytorchjob_manifest("j", "team", "img", ["x"], n_nodes=1, gpus_per_node=1, backoff_limit=1))
