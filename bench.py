@@ -418,6 +418,8 @@ def _run(a, rank: int, crd):
         if crd is not None:
             out["crd_to_first_step_p50_s"] = crd.get("p50_s")
             out["crd_to_first_step_p90_s"] = crd.get("p90_s")
+            # the same box's bare `import torch` (median of 3, before the jobs): box speed vs pipeline
+            out["crd_to_first_step_p50_minus_import_control_s"] = crd.get("p50_minus_import_control_s")
             out["crd_to_first_step"] = crd
         if a.layers is not None:
             out["INVALID"] = "reduced layer count (debug run)"

@@ -79,12 +79,50 @@ def wait_device_release(base: dict, held: dict, n_devices: int = 1, timeout: flo
     return time.time() - t0
 
 
+def box_control(runs: int = 3, gpu: bool = False) -> dict:
+    """The same box's own cost of the part of a worker start this repo does not control, measured
+    right before the jobs: the median wall time of ``python -c 'import torch'`` (fresh
+    interpreters, page cache warm after the first), with ``os.cpu_count()``, the CPUs this
+    process may run on and the 1-minute load average.  ``gpu=True`` adds the same for
+    ``import torch`` + HIP runtime / device / context init (``torch.zeros(1, device='cuda')``)
+    in a child process.  ``p50 - import_torch_s`` then separates box speed from pipeline cost
+    (VERDICT r5 item 5)."""
+    import subprocess
+
+    def timed(code):
+        t = []
+        for _ in range(runs):
+            t0 = time.perf_counter()
+            subprocess.run([sys.executable, "-c", code], check=True, stdout=subprocess.DEVNULL,
+                           stderr=subprocess.DEVNULL)
+            t.append(time.perf_counter() - t0)
+        return t
+    imp = timed("import torch")
+    out = {"import_torch_s": round(statistics.median(imp), 3), "import_torch_runs_s": [round(x, 3) for x in imp],
+           "cpu_count": os.cpu_count(), "cpus_usable": len(os.sched_getaffinity(0)),
+           "loadavg_1m": round(os.getloadavg()[0], 2)}
+    if gpu:
+        hip = timed("import torch; torch.zeros(1, device='cuda'); torch.cuda.synchronize()")
+        out["import_torch_hip_init_s"] = round(statistics.median(hip), 3)
+        out["import_torch_hip_init_runs_s"] = [round(x, 3) for x in hip]
+    return out
+
+
 def measure(jobs: int = 3, model: str = "llama3-8b", gpus: int = 1, nodes: int = 1, seq_len: int = 8192,
             micro_batch: int = 1, layers: Optional[int] = None, device: str = "cuda", kind: str = "pytorchjob",
             processes: bool = True, gap: float = 0.0, release_wait: Optional[bool] = None,
-            timeout: float = 300.0, port_base: int = 29700,
+            timeout: float = 300.0, port_base: int = 29700, poll: Optional[float] = None,
+            control: bool = True,
             log: Callable[[str], None] = lambda s: print(s, file=sys.stderr, flush=True)) -> dict:
-    """Submit ``jobs`` jobs one after another; returns p50 / p90 / min and the breakdown."""
+    """Submit ``jobs`` jobs one after another; returns p50 / p90 / min and the breakdown.
+
+    ``poll`` is the measuring loop's period (default 0.05 s, ``KFAMD_CRD_POLL``).  The measured
+    time comes from the worker's own ``first_step`` timestamp, so the period adds nothing to
+    it; a short period only costs CPU that the worker's import competes for on a small box
+    (0.01 vs 0.1 s A/B: profiles/crd_to_first_step_r6.md)."""
+    if poll is None:
+        poll = float(os.environ.get("KFAMD_CRD_POLL", "0.05"))
+    ctl = box_control(gpu=device == "cuda") if control else None
     from .cluster import LocalCluster, ProcessCluster
     from .controlplane import training
     from .native import build_native
@@ -148,7 +186,7 @@ def measure(jobs: int = 3, model: str = "llama3-8b", gpus: int = 1, nodes: int =
                     first = fs[0]
                     held = _vram_used() if release_wait else {}
                     break
-                time.sleep(0.01)
+                time.sleep(poll)
             if first is None:
                 raise RuntimeError(f"{name}: no first_step within {timeout}s\n" + pod_log("bench", rank0_pod)[-3000:])
             r0 = [e for e in evs if e.get("rank") == 0]
@@ -176,7 +214,13 @@ def measure(jobs: int = 3, model: str = "llama3-8b", gpus: int = 1, nodes: int =
     finally:
         cl.stop()
     tot = sorted(r["total"] for r in rows)
-    return {"jobs": len(rows), "kind": kind, "model": model, "gpus_per_node": gpus, "nodes": nodes,
+    extra = {}
+    if ctl is not None:
+        p50 = statistics.median(tot)
+        extra = {"box_control": ctl, "p50_minus_import_control_s": round(p50 - ctl["import_torch_s"], 3)}
+        if "import_torch_hip_init_s" in ctl:
+            extra["p50_minus_import_hip_control_s"] = round(p50 - ctl["import_torch_hip_init_s"], 3)
+    return {**extra, "poll_s": poll, "jobs": len(rows), "kind": kind, "model": model, "gpus_per_node": gpus, "nodes": nodes,
             "control_plane": "processes over HTTP" if processes else "in-process",
             "p50_s": round(statistics.median(tot), 3),
             "p90_s": round(tot[min(len(tot) - 1, int(0.9 * len(tot)))], 3),

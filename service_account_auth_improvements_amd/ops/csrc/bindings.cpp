@@ -71,11 +71,6 @@ int kf_car_free(void*);
 int kf_car_allreduce(void* const*, int, int, const void*, void*, long, long, int, double, hipStream_t);
 int kf_car_error(void*, hipStream_t);
 long kf_ts_header_bytes();
-long kf_decode_step_ws_bytes();
-long kf_decode_step_err_offset();
-int kf_decode_step(const void*, int, int, int, int, int, int, int, int, const void*, const void*, const void*,
-                   const float*, const float*, const long*, const int*, const int*, int, float, float, void*, void*,
-                   hipStream_t);
 int kf_ts_alloc(long, int, void**, void*);
 int kf_ts_run(int, void* const*, int, int, const void*, void*, long, long, int, double, hipStream_t);
 int kf_ts_error(void*, hipStream_t);
@@ -386,45 +381,6 @@ at::Tensor decode_attn(const at::Tensor& q2d, const at::Tensor& kc, const at::Te
                           (float)scale, cur_stream()),
            "decode_attn");
   return out;
-}
-
-// Decode step for 1-4 rows as one persistent launch (ops/csrc/decode_step.hip).  tab: int64 [L, 8]
-// device pointers per layer (wqkv, wo, wgu, wd, norm1, norm2, k cache, v cache); token int64 [M],
-// slot / pos int32 [M]; ws: uint8 workspace of decode_step_ws_bytes(); logits: bf16 [M, V].
-// Returns the kernel's rc (0 = launched, else the model / device is not the shape it is built
-// for and nothing ran).
-int64_t decode_step_ws_bytes() { return kf_decode_step_ws_bytes(); }
-int64_t decode_step_err_offset() { return kf_decode_step_err_offset(); }
-
-int64_t decode_step(const at::Tensor& tab, int64_t hidden, int64_t ffn, int64_t hq, int64_t hkv, int64_t hd,
-                    const at::Tensor& embed, const at::Tensor& fnorm, const at::Tensor& lm, const at::Tensor& cos,
-                    const at::Tensor& sin, const at::Tensor& token, const at::Tensor& slot, const at::Tensor& pos,
-                    int64_t lmax, double eps, double scale, at::Tensor& ws, at::Tensor& logits) {
-  TORCH_CHECK(tab.is_cuda() && tab.scalar_type() == at::kLong && tab.dim() == 2 && tab.size(1) == 8 &&
-                  tab.is_contiguous(), "decode_step: tab must be int64 [L, 8] on the GPU");
-  check_bf16_cuda(embed, "embed");
-  check_bf16_cuda(fnorm, "final_norm");
-  check_bf16_cuda(lm, "lm_head");
-  check_bf16_cuda(logits, "logits");
-  TORCH_CHECK(embed.is_contiguous() && lm.is_contiguous() && fnorm.is_contiguous() && logits.is_contiguous(),
-              "decode_step: contiguous weights");
-  const int64_t M = token.numel();
-  TORCH_CHECK(lm.dim() == 2 && lm.size(1) == hidden && logits.numel() == M * lm.size(0), "decode_step: lm_head / logits");
-  TORCH_CHECK(cos.is_cuda() && cos.scalar_type() == at::kFloat && sin.is_cuda() && sin.scalar_type() == at::kFloat &&
-                  cos.is_contiguous() && sin.is_contiguous() && cos.size(-1) == 64 && cos.numel() >= lmax * 64,
-              "decode_step: fp32 RoPE tables [max_seq, 64] covering lmax");
-  TORCH_CHECK(token.is_cuda() && token.scalar_type() == at::kLong && token.is_contiguous() && M >= 1 && M <= 4,
-              "decode_step: token int64 [1..4]");
-  check_rows_i32(slot, M, "slot");
-  check_rows_i32(pos, M, "pos");
-  TORCH_CHECK(ws.is_cuda() && ws.scalar_type() == at::kByte && ws.numel() >= kf_decode_step_ws_bytes(),
-              "decode_step: workspace too small");
-  c10::hip::HIPGuardMasqueradingAsCUDA g(logits.device());
-  return kf_decode_step(tab.data_ptr(), (int)tab.size(0), (int)M, (int)hidden, (int)ffn, (int)hq, (int)hkv, (int)hd,
-                        (int)lm.size(0), embed.data_ptr(), fnorm.data_ptr(), lm.data_ptr(), cos.data_ptr<float>(),
-                        sin.data_ptr<float>(), (const long*)token.data_ptr<int64_t>(), slot.data_ptr<int>(),
-                        pos.data_ptr<int>(), (int)lmax, (float)eps, (float)scale, ws.data_ptr(), logits.data_ptr(),
-                        cur_stream());
 }
 
 // Append one token per row (K/V columns of fused qkv rows) at pos[b] of slot slots[b].
@@ -801,11 +757,6 @@ TORCH_LIBRARY(kfamd, m) {
   m.def("flash_fwd", &flash_fwd);
   m.def("flash_bwd", &flash_bwd);
   m.def("decode_attn", &decode_attn);
-  m.def("decode_step_ws_bytes", &decode_step_ws_bytes);
-  m.def("decode_step_err_offset", &decode_step_err_offset);
-  m.def("decode_step(Tensor tab, int hidden, int ffn, int hq, int hkv, int hd, Tensor embed, Tensor fnorm, "
-        "Tensor lm, Tensor cos, Tensor sin, Tensor token, Tensor slot, Tensor pos, int lmax, float eps, float scale, "
-        "Tensor(a!) ws, Tensor(b!) logits) -> int", &decode_step);
   m.def("skinny_gemm", &skinny_gemm);
   m.def("bgemm(Tensor x, Tensor w, bool swiglu, int splits) -> Tensor", &bgemm);
   m.def("skinny_gemm_norm", &skinny_gemm_norm);

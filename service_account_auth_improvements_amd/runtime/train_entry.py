@@ -91,6 +91,42 @@ def _heartbeat():
             os.utime(hb, None)
 
 
+def _hip_preinit(device_arg: str):
+    """Start HIP runtime + device initialisation on a side thread BEFORE ``import torch``, so the
+    ~0.2 s of runtime / device / context set-up runs under the ~1.4 s import instead of after it
+    (CRD-to-first-step; profiles/crd_to_first_step_r6.md).  It loads the very HIP runtime torch
+    will use (torch/lib/libamdhip64.so, found without importing torch: one runtime per process),
+    counts devices, selects this rank's (LOCAL_RANK modulo the count, as
+    parallel/state.local_device_index) and creates its context with ``hipFree(NULL)``.
+    ``KFAMD_HIP_PREINIT=0`` or ``--device cpu`` turns it off; any failure leaves the work to
+    torch's own lazy init."""
+    if device_arg == "cpu" or os.environ.get("KFAMD_HIP_PREINIT", "1") == "0":
+        return None
+    import ctypes
+    import importlib.util
+    import threading
+    spec = importlib.util.find_spec("torch")
+    if spec is None or spec.origin is None:
+        return None
+    lib = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so")
+    if not os.path.exists(lib) or not os.path.exists("/dev/kfd"):
+        return None
+
+    def run():
+        try:
+            h = ctypes.CDLL(lib, mode=ctypes.RTLD_GLOBAL)
+            n = ctypes.c_int(0)
+            if h.hipGetDeviceCount(ctypes.byref(n)) != 0 or n.value < 1:
+                return
+            if h.hipSetDevice(int(os.environ.get("LOCAL_RANK", "0")) % n.value) == 0:
+                h.hipFree(ctypes.c_void_p(0))
+        except Exception:   # noqa: BLE001 -- torch's lazy init does the same work later
+            pass
+    t = threading.Thread(target=run, name="kfamd-hip-preinit", daemon=True)
+    t.start()
+    return t
+
+
 def _warm_blas(index: int):
     """A fresh GPU process pays ~0.6 s of first-use costs before its first step can run: HIP
     runtime / device init (~0.2 s), hipBLASLt's first GEMM (library and kernel catalog, ~0.17 s),
@@ -158,13 +194,14 @@ def main(argv=None):
 
     t_start = time.time()
     _event("process_start")
+    pre = _hip_preinit(a.device)
     if os.environ.get("KFAMD_METRICS_PORT", "") != "":
         # the communicator records start/end events per collective: the /metrics bus bandwidth
         os.environ.setdefault("TORCH_NCCL_ENABLE_TIMING", "1")
     import torch
     from ..parallel.state import init_distributed, local_device_index
     from .trainer import SyntheticData, TrainConfig, Trainer
-    _event("imported", seconds=time.time() - t_start)
+    _event("imported", seconds=time.time() - t_start, hip_preinit=pre is not None)
 
     dev = None if a.device == "auto" else a.device
     if dev == "cuda" or (dev is None and torch.cuda.is_available()):

@@ -57,12 +57,10 @@ BGEMM_MIN_ROWS, BGEMM_MAX_ROWS = 33, 128   # at 32 rows its reduce launch costs 
 # prompts admitted in one scheduler iteration are prefilled together up to this many tokens
 PREFILL_MAX_TOKENS = int(os.environ.get("KFAMD_PREFILL_MAX_TOKENS", "16384"))
 PREFILL_PAD_RATIO = 1.25      # ... in length groups padded to at most 1.25x
-# batches 1-4: the whole decode step as ONE persistent kernel (ops/csrc/decode_step.hip) where
-# the model is its shape.  Opt-in (KFAMD_DECODE_PERSISTENT=1 or Engine(persistent=True)): on
-# MI355X it measures 3.54-3.65 ms/token at batch 1 against 3.15 for the kernel-per-op graph --
-# its 160 software grid barriers per token cost more than the launches they replace
-# (profiles/decode_step_ablation_r4p.txt, docs/ROUND4.md)
-PERSISTENT_DECODE = os.environ.get("KFAMD_DECODE_PERSISTENT", "0") == "1"
+# batches 1-4 run the same kernel-per-op graph as larger batches.  A whole-step persistent kernel
+# (one launch per token, grid barriers between the layer phases) measured 3.54-3.65 ms/token at
+# batch 1 against 3.15 for this graph and was moved out of the production library into
+# tools/kbench/decode_step_lab.hip (profiles/decode_step_ablation_r4p.txt, docs/ROUND6.md).
 # hipBLASLt/rocBLAS solutions for the decode GEMM shapes above SKINNY_MAX_ROWS where the library
 # heuristic picks a poor kernel (tools/tune_decode_gemm.py; only the shapes that measured >= 5 %
 # faster HBM-cold are kept, profiles/serve_large_batch.md).  Loaded into PyTorch TunableOp with
@@ -85,80 +83,8 @@ def _load_tuned_decode_gemms(dev, cfg, tp: int) -> bool:
     return True
 
 
-class PersistentDecode:
-    """Decode step for 1-4 rows as one persistent launch (ops/csrc/decode_step.hip): 256
-    workgroups, one per CU, stream every weight byte of the step once by LDS-DMA while grid
-    barriers order the layer's phases.  Built for Llama-3-8B at TP 1 on a 256-CU MI355X;
-    ``build`` returns None for anything else.  The kernel's grid barriers are bounded: a
-    timed-out step sets the error word (``failed()``), the engine disables this path and
-    recomputes the step kernel-per-op."""
-
-    MAX_ROWS = 4
-
-    def __init__(self, engine: "Engine"):
-        from ..ops import _ext
-        m, cfg = engine.m, engine.cfg
-        self.k = _ext.ops()
-        dev = engine.dev
-        rows = []
-        for li, i in enumerate(m.layers):
-            rows.append([m.P(f"l{i}.wqkv").data_ptr(), m.P(f"l{i}.wo").data_ptr(), m.P(f"l{i}.wgu").data_ptr(),
-                         m.P(f"l{i}.wd").data_ptr(), m.P(f"l{i}.norm1").data_ptr(), m.P(f"l{i}.norm2").data_ptr(),
-                         engine.kc[li].data_ptr(), engine.vc[li].data_ptr()])
-        self.tab = torch.tensor(rows, dtype=torch.int64, device=dev)
-        self.ws = torch.zeros(int(self.k.decode_step_ws_bytes()), dtype=torch.uint8, device=dev)
-        off = int(self.k.decode_step_err_offset())
-        self.err = self.ws[off:off + 4].view(torch.int32)
-        self.V = m.P("lm_head").shape[0]
-        self.logits = {}                # rows -> bf16 [rows, V] (graph-static per bucket)
-        self.cfg, self.m, self.lmax = cfg, m, engine.max_len
-        self.last_rc = 0                # the last launch's return code (0 = launched)
-        self.last_err = 0               # the error word read by the last failed() check
-
-    @staticmethod
-    def supported(engine: "Engine") -> bool:
-        m, cfg = engine.m, engine.cfg
-        return (engine.dev.type == "cuda" and m.tp == 1 and m.first and m.last
-                and (cfg.hidden, cfg.ffn, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim) == (4096, 14336, 32, 8, 128)
-                and len(m.layers) <= 32 and m.P("lm_head").shape[0] % 256 == 0)
-
-    @classmethod
-    def build(cls, engine: "Engine"):
-        return cls(engine) if cls.supported(engine) else None
-
-    def __call__(self, tokens, slots, pos):
-        """Launch one step for the M = len(tokens) <= 4 rows (token, slot, pos: device [M]
-        tensors); returns logits [M, V] or None when the kernel refused the shape / device
-        (nothing launched)."""
-        m, cfg = self.m, self.cfg
-        M = tokens.shape[0]
-        out = self.logits.get(M)
-        if out is None:
-            out = self.logits[M] = torch.empty((M, self.V), dtype=torch.bfloat16, device=self.ws.device)
-        rc = self.k.decode_step(self.tab, cfg.hidden, cfg.ffn, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim,
-                                m.P("embed"), m.P("final_norm"), m.P("lm_head"), m.cos, m.sin, tokens, slots, pos,
-                                self.lmax, float(cfg.norm_eps), 1.0 / math.sqrt(cfg.head_dim), self.ws, out)
-        self.last_rc = int(rc)
-        return out if rc == 0 else None
-
-    def sync_words(self) -> dict:
-        """The launch's barrier shard counters, attention tickets and error word (diagnostics)."""
-        off = int(self.k.decode_step_err_offset())
-        shard = 32
-        base = off - (8 + 4 * 8) * shard * 4
-        w = self.ws[base:off + shard * 4 + 4].view(torch.int32).cpu()
-        return {"barrier_shards": w[0:8 * shard:shard].tolist(),
-                "tickets": w[8 * shard:(8 + 32) * shard:shard].tolist(), "err": int(w[40 * shard]),
-                "exit": int(w[41 * shard])}
-
-    def failed(self) -> bool:
-        self.last_err = int(self.err.item())
-        return self.last_err != 0
-
-
 class Engine:
-    def __init__(self, model: Llama, n_slots: int = 64, max_len: int = 4096, use_graphs: Optional[bool] = None,
-                 persistent: Optional[bool] = None):
+    def __init__(self, model: Llama, n_slots: int = 64, max_len: int = 4096, use_graphs: Optional[bool] = None):
         self.m = model
         cfg = model.cfg
         self.cfg = cfg
@@ -179,10 +105,6 @@ class Engine:
         if model.tp > 1 and self.dev.type == "cuda":
             from ..parallel.custom_ar import OneShotAllReduce
             self.car = OneShotAllReduce(model.st.tp_group)
-        want = PERSISTENT_DECODE if persistent is None else bool(persistent)
-        self.persist = PersistentDecode.build(self) if want else None
-        # "active" / "off" / why the persistent path was dropped (reported by tools/bench_serve.py)
-        self.persist_status = "active" if self.persist is not None else "off"
         self._graphs: Dict[int, tuple] = {}
         self._staging: Dict[int, tuple] = {}   # bucket -> (pinned host [3, Bb], device [3, Bb], copy-done event)
 
@@ -316,12 +238,6 @@ class Engine:
 
     def _decode_body(self, tokens, slots, pos, lengths):
         m, cfg = self.m, self.cfg
-        if self.persist is not None and tokens.shape[0] <= PersistentDecode.MAX_ROWS:
-            out = self.persist(tokens, slots, pos)
-            if out is not None:
-                return out
-            # refused (device / shape): kernel-per-op from now on
-            self._drop_persist(f"refused rc={self.persist.last_rc}")
         r = self._embed(tokens)
         d = None
         for li, i in enumerate(m.layers):
@@ -376,9 +292,6 @@ class Engine:
             p = torch.tensor(pos, dtype=torch.int32, device=dev)
             out = self._decode_body(t, sl, p, p + 1)
             self._check_comm()
-            if B <= PersistentDecode.MAX_ROWS and self.persist is not None and self.persist.failed():
-                self._drop_persist(f"failed err={self.persist.last_err} {self.persist.sync_words()}")
-                return self.decode(tokens, slots, pos)
             return out
         Bb = next((b for b in BUCKETS if b >= B), None)
         if Bb is None:
@@ -407,21 +320,7 @@ class Engine:
         gl.copy_(dev_rows[2] + 1)
         graph.replay()
         self._check_comm()
-        if Bb <= PersistentDecode.MAX_ROWS and self.persist is not None and self.persist.failed():
-            # a grid barrier timed out (a CU never arrived): drop the persistent path, rebuild the
-            # bucket's graph kernel-per-op and recompute this step (it rewrites the step's K/V)
-            self._drop_persist(f"failed err={self.persist.last_err} {self.persist.sync_words()}")
-            for b in [b for b in self._graphs if b <= PersistentDecode.MAX_ROWS]:
-                self._graphs.pop(b)
-            return self.decode(tokens, slots, pos)
         return out[:B]
-
-    def _drop_persist(self, why: str):
-        import sys
-        self.persist = None
-        self.persist_status = why
-        print(f"serving: persistent decode kernel disabled ({why}); kernel-per-op decode from now on",
-              file=sys.stderr, flush=True)
 
     def _check_comm(self):
         """TP decode: fail the step (and the engine) when a one-shot all-reduce timed out on a
@@ -588,7 +487,7 @@ class Scheduler:
 def build_engine(model_name: str = "llama3-8b", device=None, n_slots: int = 64, max_len: int = 4096,
                  checkpoint: Optional[str] = None, n_layers: Optional[int] = None, seed: int = 1234,
                  st: Optional[ParallelState] = None, use_graphs: Optional[bool] = None,
-                 full_init: bool = False, persistent: Optional[bool] = None) -> Engine:
+                 full_init: bool = False) -> Engine:
     cfg = LlamaConfig.preset(model_name)
     if n_layers:
         cfg = cfg.with_(n_layers=n_layers)
@@ -599,4 +498,4 @@ def build_engine(model_name: str = "llama3-8b", device=None, n_slots: int = 64, 
     if checkpoint:
         from ..runtime.checkpoint import load_params
         load_params(model, checkpoint)
-    return Engine(model, n_slots=n_slots, max_len=max_len, use_graphs=use_graphs, persistent=persistent)
+    return Engine(model, n_slots=n_slots, max_len=max_len, use_graphs=use_graphs)

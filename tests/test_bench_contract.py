@@ -63,6 +63,11 @@ def test_bench_reports_crd_to_first_step():
     assert b["cr_to_running"] < b["import"] + b["init_to_first_step"] + 5
     assert abs(sum(b[k] for k in ("cr_to_running", "running_to_process", "import", "dist_init", "model_init",
                                    "init_to_first_step")) - crd["p50_s"]) < 1.0
+    # the same box's control: bare `import torch`, CPUs, load
+    ctl = crd["box_control"]
+    assert ctl["import_torch_s"] > 0 and len(ctl["import_torch_runs_s"]) == 3
+    assert ctl["cpu_count"] >= 1 and ctl["cpus_usable"] >= 1 and ctl["loadavg_1m"] >= 0
+    assert rec["crd_to_first_step_p50_minus_import_control_s"] == round(crd["p50_s"] - ctl["import_torch_s"], 3)
 
 
 def test_bench_two_ranks_torchrun_json():

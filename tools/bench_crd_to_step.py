@@ -39,11 +39,12 @@ def main():
                     help="mpijob: an upstream-style MPIJob (Launcher mpirun -np G, Worker with G GPUs)")
     ap.add_argument("--processes", action="store_true",
                     help="control plane and node agents as separate processes over HTTP (one kubelet per node)")
+    ap.add_argument("--poll", type=float, default=None, help="measuring loop period (s); default 0.05")
     a = ap.parse_args()
     from service_account_auth_improvements_amd.crdbench import measure
     out = measure(jobs=a.jobs, model=a.model, gpus=a.gpus, nodes=a.nodes, seq_len=a.seq_len,
                   micro_batch=a.micro_batch, layers=a.layers, device="cuda" if a.gpus else "cpu", kind=a.kind,
-                  processes=a.processes, gap=a.gap, timeout=a.timeout, log=lambda s: print(s, flush=True))
+                  processes=a.processes, gap=a.gap, timeout=a.timeout, poll=a.poll, log=lambda s: print(s, flush=True))
     print(json.dumps({"metric": "CRD-to-first-step", "gap_s": a.gap, **out}), flush=True)
 
 

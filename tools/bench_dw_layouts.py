@@ -26,6 +26,7 @@ from service_account_auth_improvements_amd import ops
 T = 32768
 SHAPES = {"wqkv": (6144, 4096), "wo": (4096, 4096), "wgu": (28672, 4096), "wd": (4096, 14336)}
 TUNABLE = "--tunable" in sys.argv
+ONLY = next((a.split("=", 1)[1].split(",") for a in sys.argv if a.startswith("--shapes=")), None)
 HEAD = ("lm_head", (128256, 4096), 4096)          # chunked head: 4096 tokens per product, 8 chunks
 
 
@@ -82,8 +83,12 @@ def run(name, N, K, tokens):
 
 
 def main():
-    res = {n: run(n, N, K, T) for n, (N, K) in SHAPES.items()}
+    res = {n: run(n, N, K, T) for n, (N, K) in SHAPES.items() if ONLY is None or n in ONLY}
+    if ONLY is not None and HEAD[0] not in ONLY:
+        return
     head = run(HEAD[0], *HEAD[1], HEAD[2])
+    if ONLY is not None:
+        return                      # a partial run: the step mix needs every shape
     mix = {}
     for k in ("hip_tn_ms", "blas_tn_ms", "blas_nn_ms", "blas_nn_pre_ms", "blas_nt_pre_ms",
               "tuned_tn_ms", "tuned_nn_pre_ms", "tuned_nt_pre_ms"):

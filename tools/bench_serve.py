@@ -27,13 +27,11 @@ def main():
     ap.add_argument("--steps", type=int, default=32)
     ap.add_argument("--max-len", type=int, default=2048)
     ap.add_argument("--prefill-batch", type=int, default=16, help="prompts per batched prefill pass")
-    ap.add_argument("--persistent", type=int, default=None, help="1: persistent decode kernel at batch <= 4")
     a = ap.parse_args()
     batches = [int(x) for b in a.batches for x in b.split(",") if x]
     nb = max(batches)
     t0 = time.time()
-    e = build_engine(a.model, device="cuda", n_slots=nb, max_len=a.max_len, n_layers=a.layers,
-                     persistent=None if a.persistent is None else bool(a.persistent))
+    e = build_engine(a.model, device="cuda", n_slots=nb, max_len=a.max_len, n_layers=a.layers)
     torch.cuda.synchronize()
     init_s = time.time() - t0
     prompt = [(i * 7919) % 1000 + 1 for i in range(a.ctx)]
@@ -72,10 +70,9 @@ def main():
             e.decode(toks, slots, [a.ctx + k] * B)
         torch.cuda.synchronize()
         dt = (time.time() - t0) / a.steps
-        path = "persistent" if (B <= 4 and getattr(e, "persist", None) is not None) else "kernel-per-op graph"
         print(json.dumps({"bench": "decode", "model": a.model, "batch": B, "context": a.ctx,
                           "ms_per_step": round(1e3 * dt, 3), "tokens_per_s": round(B / dt, 1),
-                          "decode_path": path, "persistent_status": getattr(e, "persist_status", "n/a")}),
+                          "decode_path": "kernel-per-op graph"}),
               flush=True)
     # decode-attention kernel alone: HBM bytes of K+V read per call
     from service_account_auth_improvements_amd.ops.attention import decode_attention
