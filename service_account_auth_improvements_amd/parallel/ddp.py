@@ -154,6 +154,9 @@ class GradReducer:
         self.a2a = self.fp32 and self.enabled and mode == "reduce_scatter"
         self._accumulated = False     # accumulate_micro ran in this step
         self.stats: Optional[CollectiveStats] = None   # set by the worker when /metrics is on
+        # one-GPU stand-in for the N > 1 collectives' CU / HBM footprint (tools/dp8_overlap_proxy.py):
+        # called at every bucket launch, at finish() and at the parameter gather
+        self.traffic_proxy = None
         if self.fp32:
             for g in groups:
                 dev = g.grads.device
@@ -233,6 +236,8 @@ class GradReducer:
                 ops.grad_accum_(m, x, ops.GRAD_FOLD if self.a2a else ops.GRAD_ADD)
             elif not self.a2a:
                 ops.grad_accum_(m, x, ops.GRAD_SET)       # fp32 all-reduce / optimizer operand
+        if self.traffic_proxy is not None:
+            self.traffic_proxy.on_bucket(x.numel() * x.element_size())
         if not self.enabled:
             return
         self._drain_completed()
@@ -301,6 +306,8 @@ class GradReducer:
         for bl in self.buckets.values():
             for b in bl:
                 self._launch(b)
+        if self.traffic_proxy is not None:
+            self.traffic_proxy.on_finish()
         progress.mark("dp collective wait", f"{len(self._pending)} buckets")
         for b in self._pending:
             self._complete(b)
@@ -314,6 +321,10 @@ class GradReducer:
         ``param_wait`` hook makes the compute stream wait on a bucket just before the next
         forward first reads it (:meth:`wait_params`), so the gather hides behind the
         previous layers' compute instead of sitting between optimizer and forward."""
+        if self.traffic_proxy is not None:
+            for bl in self.buckets.values():
+                for b in bl:
+                    self.traffic_proxy.on_gather((b.hi - b.lo) * b.group.params.element_size())
         if not self.enabled or self.mode != "reduce_scatter":
             return
         r = dist.get_rank(self.dp_group) if self.dp_group is not None else dist.get_rank()

@@ -157,3 +157,33 @@ def test_tensor_parallel_training_with_clipping_matches_tp1():
     # replicated norm weights: identical across TP ranks and close to TP=1
     assert torch.equal(res[0][1], res[1][1])
     assert _close(res[0][1], tr.model.norms.params.float(), 1e-2)
+
+
+def test_traffic_proxy_sees_every_bucket_the_finish_and_the_gather():
+    """GradReducer.traffic_proxy (tools/dp8_overlap_proxy.py): one step hands it every gradient
+    bucket's bytes as the bucket is launched, one finish() before the optimizer, and every
+    parameter bucket's bytes at the gather -- also at dp 1, where no collective runs."""
+    from service_account_auth_improvements_amd.parallel.state import ParallelState
+    from service_account_auth_improvements_amd.runtime.trainer import SyntheticData, TrainConfig, Trainer
+    tr = Trainer(TrainConfig(model="tiny", seq_len=32, micro_batch=2, zero1=True, bucket_mb=1),
+                 ParallelState(device=torch.device("cpu")))
+    seen = {"bucket": [], "finish": 0, "gather": []}
+
+    class Rec:
+        def on_bucket(self, n):
+            seen["bucket"].append(n)
+
+        def on_finish(self):
+            seen["finish"] += 1
+
+        def on_gather(self, n):
+            seen["gather"].append(n)
+
+    tr.reducer.traffic_proxy = Rec()
+    data = SyntheticData(tr.mcfg.vocab_size, 2, 32, "cpu", seed=0)
+    tr.train_step([data.next()])
+    total = sum(g.numel * g.grads.element_size() for g in tr.model.groups)
+    nb = sum(len(bl) for bl in tr.reducer.buckets.values())
+    assert len(seen["bucket"]) == nb > 1 and sum(seen["bucket"]) == total
+    assert seen["finish"] == 1
+    assert sum(seen["gather"]) == total
