@@ -81,28 +81,32 @@ def wait_device_release(base: dict, held: dict, n_devices: int = 1, timeout: flo
 
 def box_control(runs: int = 3, gpu: bool = False) -> dict:
     """The same box's own cost of the part of a worker start this repo does not control, measured
-    right before the jobs: the median wall time of ``python -c 'import torch'`` (fresh
-    interpreters, page cache warm after the first), with ``os.cpu_count()``, the CPUs this
-    process may run on and the 1-minute load average.  ``gpu=True`` adds the same for
-    ``import torch`` + HIP runtime / device / context init (``torch.zeros(1, device='cuda')``)
-    in a child process.  ``p50 - import_torch_s`` then separates box speed from pipeline cost
-    (VERDICT r5 item 5)."""
+    right before the jobs in fresh interpreters: ``import_torch_s`` is the median time of
+    ``import torch`` measured inside the child (the same span as a worker's ``import`` phase),
+    ``python_import_torch_wall_s`` the child's whole wall time (interpreter start and exit
+    included), with ``os.cpu_count()``, the CPUs this process may run on and the 1-minute load
+    average.  ``gpu=True`` adds ``import torch`` + HIP runtime / device / context init
+    (``torch.zeros(1, device='cuda')``), in-child.  ``p50 - import_torch_s`` then separates box
+    speed from pipeline cost."""
     import subprocess
 
     def timed(code):
-        t = []
+        inner, wall = [], []
         for _ in range(runs):
             t0 = time.perf_counter()
-            subprocess.run([sys.executable, "-c", code], check=True, stdout=subprocess.DEVNULL,
-                           stderr=subprocess.DEVNULL)
-            t.append(time.perf_counter() - t0)
-        return t
-    imp = timed("import torch")
+            r = subprocess.run([sys.executable, "-c", "import time; t0 = time.perf_counter(); " + code +
+                                "; print(time.perf_counter() - t0)"],
+                               check=True, capture_output=True, text=True)
+            wall.append(time.perf_counter() - t0)
+            inner.append(float(r.stdout.strip().splitlines()[-1]))
+        return inner, wall
+    imp, wall = timed("import torch")
     out = {"import_torch_s": round(statistics.median(imp), 3), "import_torch_runs_s": [round(x, 3) for x in imp],
+           "python_import_torch_wall_s": round(statistics.median(wall), 3),
            "cpu_count": os.cpu_count(), "cpus_usable": len(os.sched_getaffinity(0)),
            "loadavg_1m": round(os.getloadavg()[0], 2)}
     if gpu:
-        hip = timed("import torch; torch.zeros(1, device='cuda'); torch.cuda.synchronize()")
+        hip, _ = timed("import torch; torch.zeros(1, device='cuda'); torch.cuda.synchronize()")
         out["import_torch_hip_init_s"] = round(statistics.median(hip), 3)
         out["import_torch_hip_init_runs_s"] = [round(x, 3) for x in hip]
     return out
