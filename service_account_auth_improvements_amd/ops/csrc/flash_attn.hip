@@ -306,12 +306,26 @@ __device__ __forceinline__ void store_rows_via_lds(const f32x16 (&v)[4], float m
     st16(orow + (long)row * ldr + 8 * ch, *reinterpret_cast<const u32x4*>(ob + swz(row, ch)));
   }
 }
-template <bool CAUSAL>
-__global__ __launch_bounds__(512, 1) void flash_fwd_kernel(
+// NW waves per workgroup: 8 (256 query rows, 128-key K/V stages, one workgroup per CU) or 4 (128
+// rows, 64-key stages in 64 KB of LDS, two workgroups per CU with independent stage barriers)
+template <int NW> struct FwdCfg {
+  static constexpr int RW = 32 * NW;              // query rows per workgroup
+  static constexpr int BKS = NW == 8 ? 128 : 64;  // keys per K/V stage
+  static constexpr int KT = BKS / 32;             // 32-key chunks per stage
+  static constexpr int HF = BKS / 64;             // 64-key halves per stage (PV groups: 4 HF)
+  static constexpr int TILE = BKS * D * 2;
+  static constexpr int STG = 2 * TILE;
+  static constexpr int NDI = BKS / (4 * NW);      // DMA wave-instructions per wave per tile
+};
+template <bool CAUSAL, int NW>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void flash_fwd_kernel(
     const bf16_t* __restrict__ qkv, long ld, bf16_t* __restrict__ out, long ldo,
     float* __restrict__ lse_out, int B, int S, int Hq, int Hkv, float scale_log2) {
-  __shared__ __attribute__((aligned(1024))) char smem[NSF * STGF];
-  const int nqb = (S + BQ8 - 1) / BQ8, G = Hq / Hkv;
+  using C = FwdCfg<NW>;
+  constexpr int RW = C::RW, BKS = C::BKS, NKTL = C::KT, HF = C::HF, TILE = C::TILE, STG = C::STG;
+  static_assert(NSF * STG <= 163840 && C::NDI * 4 * NW == BKS, "forward stage layout");
+  __shared__ __attribute__((aligned(1024))) char smem[NSF * STG];
+  const int nqb = (S + RW - 1) / RW, G = Hq / Hkv;
   // logical order [b][hkv][q-block][g]: an XCD's contiguous range shares one K/V panel
   int lid = xcd_remap(blockIdx.x, B * Hq * nqb);
   const int g = lid % G;
@@ -323,8 +337,8 @@ __global__ __launch_bounds__(512, 1) void flash_fwd_kernel(
 
   const int tid = threadIdx.x, l = tid & 63, lr = l & 31, hh = l >> 5;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int q = qb * BQ8 + w * 32 + lr;
-  const int qmin_w = qb * BQ8 + w * 32, qmax_w = qmin_w + 31;
+  const int q = qb * RW + w * 32 + lr;
+  const int qmin_w = qb * RW + w * 32, qmax_w = qmin_w + 31;
   const bool live = qmin_w < S;   // the last block of S % 256 == 128 has 4 idle waves
 
   bf16x8 qf[8];  // B operand of S^T = K Q^T: Q[q][16ks + 8hh .. +8]
@@ -343,15 +357,15 @@ __global__ __launch_bounds__(512, 1) void flash_fwd_kernel(
   const u32 lds_w = lds_addr(smem) + 1024 * w;
   // 8 DMA wave-instructions per wave per stage: the 32-row segments i of the K and V tiles
   auto stage = [&](int j) {
-    const u32 st = lds_w + (j % NSF) * STGF;
-    const char* kb_ = reinterpret_cast<const char*>(kp + (long)j * BKF * ld);
-    const char* vb_ = reinterpret_cast<const char*>(vp + (long)j * BKF * ld);
+    const u32 st = lds_w + (j % NSF) * STG;
+    const char* kb_ = reinterpret_cast<const char*>(kp + (long)j * BKS * ld);
+    const char* vb_ = reinterpret_cast<const char*>(vp + (long)j * BKS * ld);
 #pragma unroll
-    for (int i = 0; i < NKT; ++i) dma_sv(kb_ + (long)64 * ld * i, dma_kv, st + 8192 * i);
+    for (int i = 0; i < C::NDI; ++i) dma_sv(kb_ + (long)8 * NW * ld * i, dma_kv, st + 1024 * NW * i);
 #pragma unroll
-    for (int i = 0; i < NKT; ++i) dma_sv(vb_ + (long)64 * ld * i, dma_kv, st + TILEF + 8192 * i);
+    for (int i = 0; i < C::NDI; ++i) dma_sv(vb_ + (long)8 * NW * ld * i, dma_kv, st + TILE + 1024 * NW * i);
   };
-  const int ntiles = CAUSAL ? min(S, qb * BQ8 + BQ8) / BKF : S / BKF;
+  const int ntiles = CAUSAL ? min(S, qb * RW + RW) / BKS : S / BKS;
   if (ntiles > 0) stage(0);
 
   // retire the Q loads HERE (the compiler's wait counts only them, the DMA stays in flight):
@@ -371,31 +385,31 @@ __global__ __launch_bounds__(512, 1) void flash_fwd_kernel(
 
   // S'^T = K Q^T - m of tile j: key on the accumulator rows, query on the lane; K row fragments
   // by inline asm, FP steps ahead, the four 32-key chains alternating
-  auto s_chain = [&](int j, f32x16 (&sc)[NKT]) {
+  auto s_chain = [&](int j, f32x16 (&sc)[NKTL]) {
     const u32 ln = lane_id_opaque(), lr_ = ln & 31;
-    const u32 a_t = (lds_addr(smem) + (u32)((j % NSF) * STGF)) + lr_ * 256 + 16 * ((ln >> 5) ^ swz_x(lr_));
+    const u32 a_t = (lds_addr(smem) + (u32)((j % NSF) * STG)) + lr_ * 256 + 16 * ((ln >> 5) ^ swz_x(lr_));
     bf16x8 fk[FP + 1];
     auto rdK = [&](auto ic) {
-      constexpr int i = decltype(ic)::value, kt = i % NKT, ks = i / NKT;
+      constexpr int i = decltype(ic)::value, kt = i % NKTL, ks = i / NKTL;
       fk[i % (FP + 1)] = rd_b128<8192 * kt>(a_t ^ (32 * ks));
     };
     static_for<0, FP>([&](auto ic) { rdK(ic); });
 #pragma unroll
-    for (int kt = 0; kt < NKT; ++kt) sc[kt] = mfma32(ones, mref, f32x16{});
-    static_for<0, 8 * NKT>([&](auto ic) {
-      constexpr int i = decltype(ic)::value, kt = i % NKT, ks = i / NKT, NI = 8 * NKT;
+    for (int kt = 0; kt < NKTL; ++kt) sc[kt] = mfma32(ones, mref, f32x16{});
+    static_for<0, 8 * NKTL>([&](auto ic) {
+      constexpr int i = decltype(ic)::value, kt = i % NKTL, ks = i / NKTL, NI = 8 * NKTL;
       if constexpr (i + FP < NI) rdK(std::integral_constant<int, i + FP>());
       lgkm_tie1<(i + FP < NI ? FP : NI - 1 - i)>(fk[i % (FP + 1)]);
       sc[kt] = mfma32(fk[i % (FP + 1)], qf[ks], sc[kt]);
     });
   };
   // causal mask, online softmax, O^T += V^T P^T of tile j
-  auto soft_pv = [&](int j, f32x16 (&sc)[NKT]) {
-    const int k0 = j * BKF;
-    const char* Vs = smem + (j % NSF) * STGF + TILEF;
-    if (CAUSAL && k0 + BKF - 1 > qmin_w) {   // a wave's diagonal tiles only (uniform branch)
+  auto soft_pv = [&](int j, f32x16 (&sc)[NKTL]) {
+    const int k0 = j * BKS;
+    const char* Vs = smem + (j % NSF) * STG + TILE;
+    if (CAUSAL && k0 + BKS - 1 > qmin_w) {   // a wave's diagonal tiles only (uniform branch)
 #pragma unroll
-      for (int kt = 0; kt < NKT; ++kt)
+      for (int kt = 0; kt < NKTL; ++kt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int key = k0 + 32 * kt + (r & 3) + 8 * (r >> 2) + 4 * hh;
@@ -404,7 +418,7 @@ __global__ __launch_bounds__(512, 1) void flash_fwd_kernel(
     }
     float mx = -INFINITY;
 #pragma unroll
-    for (int kt = 0; kt < NKT; ++kt)
+    for (int kt = 0; kt < NKTL; ++kt)
 #pragma unroll
       for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sc[kt][r]);
     mx = xor32_max(mx);
@@ -419,7 +433,7 @@ __global__ __launch_bounds__(512, 1) void flash_fwd_kernel(
 #pragma unroll
         for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
 #pragma unroll
-      for (int kt = 0; kt < NKT; ++kt)
+      for (int kt = 0; kt < NKTL; ++kt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) sc[kt][r] -= shift;
       m = mnew;
@@ -428,7 +442,7 @@ __global__ __launch_bounds__(512, 1) void flash_fwd_kernel(
     }
     float rs = 0.f;
 #pragma unroll
-    for (int kt = 0; kt < NKT; ++kt)
+    for (int kt = 0; kt < NKTL; ++kt)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const float p = __builtin_amdgcn_exp2f(sc[kt][r] * scale_log2);
@@ -436,9 +450,9 @@ __global__ __launch_bounds__(512, 1) void flash_fwd_kernel(
         rs += p;
       }
     lsum += xor32_sum(rs);
-    bf16x8 pf[NKT][2];
+    bf16x8 pf[NKTL][2];
 #pragma unroll
-    for (int kt = 0; kt < NKT; ++kt)
+    for (int kt = 0; kt < NKTL; ++kt)
 #pragma unroll
       for (int ss = 0; ss < 2; ++ss) {
         u32x4 u;
@@ -451,7 +465,7 @@ __global__ __launch_bounds__(512, 1) void flash_fwd_kernel(
     const u32 vbase = lds_addr(Vs);
     bf16x8 vf[2][4];
     auto v_read = [&](int gi, bf16x8* f) {
-      const int t = gi >> 1, hf = gi & 1;
+      const int t = gi / HF, hf = gi % HF;
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -462,25 +476,25 @@ __global__ __launch_bounds__(512, 1) void flash_fwd_kernel(
     };
     v_read(0, vf[0]);
 #pragma unroll
-    for (int gi = 0; gi < 8; ++gi) {
-      if (gi < 7) {
+    for (int gi = 0; gi < 4 * HF; ++gi) {
+      if (gi < 4 * HF - 1) {
         v_read(gi + 1, vf[(gi + 1) & 1]);
         lgkm_wait_tie<8>(vf[gi & 1]);
       } else {
         lgkm_wait_tie<0>(vf[gi & 1]);
       }
-      const int t = gi >> 1, hf = gi & 1;
+      const int t = gi / HF, hf = gi % HF;
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
         for (int ss = 0; ss < 2; ++ss) o[t] = mfma32(vf[gi & 1][2 * kk + ss], pf[2 * hf + kk][ss], o[t]);
     }
   };
-  auto live_tile = [&](int j) { return live && (!CAUSAL || j * BKF <= qmax_w); };
+  auto live_tile = [&](int j) { return live && (!CAUSAL || j * BKS <= qmax_w); };
 
   vm_wait<0>();
   barrier();
-  f32x16 scp[NKT];
+  f32x16 scp[NKTL];
   for (int j = 0; j < ntiles; ++j) {
     if (j + 1 < ntiles) stage(j + 1);   // into the buffer every wave finished with (tile j-1)
     if (live_tile(j)) {
@@ -494,7 +508,7 @@ __global__ __launch_bounds__(512, 1) void flash_fwd_kernel(
   }
   if (!live) return;
   const float inv = 1.f / lsum;
-  store_rows_via_lds(o, inv, smem + (ntiles % NSF) * STGF + 8192 * w, out + ((long)b * S + qmin_w) * ldo + (long)h * D,
+  store_rows_via_lds(o, inv, smem + (ntiles % NSF) * STG + 8192 * w, out + ((long)b * S + qmin_w) * ldo + (long)h * D,
                      ldo);
   if (hh == 0) lse_out[((long)b * Hq + h) * S + q] = (m * scale_log2 + log2f(lsum)) * LN2;
 }
@@ -544,13 +558,27 @@ template <int N>
 __device__ __forceinline__ void lgkm_tie2(bf16x8& a, bf16x8& b) {
   asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "i"(N) : "memory");
 }
-template <bool CAUSAL>
-__global__ __launch_bounds__(512, 1) void flash_bwd_dq_kernel(
+// NW waves per workgroup: 8 (256 query rows, 128-key stages computed as two 64-key halves, one
+// workgroup per CU) or 4 (128 rows, 64-key stages, 64 KB of LDS: two workgroups per CU whose
+// stage barriers are independent, so the two waves sharing a SIMD are not phase-locked)
+template <int NW> struct DqCfg {
+  static constexpr int RW = 32 * NW;              // query rows per workgroup
+  static constexpr int BKS = NW == 8 ? 128 : 64;  // keys per K/V stage
+  static constexpr int TILE = BKS * D * 2;        // one K (or V) tile
+  static constexpr int STG = 2 * TILE;
+  static constexpr int NH = BKS / BK;             // 64-key halves per stage
+  static constexpr int NI = BKS / (4 * NW);       // DMA wave-instructions per wave per tile
+};
+template <bool CAUSAL, int NW>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void flash_bwd_dq_kernel(
     const bf16_t* __restrict__ qkv, long ld, const bf16_t* __restrict__ dout, long lddo,
     const float* __restrict__ lse, const float* __restrict__ delta, bf16_t* __restrict__ dqkv,
     long lddq, int B, int S, int Hq, int Hkv, float scale_log2, float scale) {
-  __shared__ __attribute__((aligned(1024))) char smem[NSF * STGF];
-  const int nqb = (S + BQ8 - 1) / BQ8, G = Hq / Hkv;
+  using C = DqCfg<NW>;
+  constexpr int RW = C::RW, BKS = C::BKS, TILE = C::TILE, STG = C::STG;
+  static_assert(NSF * STG <= 163840 && C::NI * 4 * NW == BKS, "dQ stage layout");
+  __shared__ __attribute__((aligned(1024))) char smem[NSF * STG];
+  const int nqb = (S + RW - 1) / RW, G = Hq / Hkv;
   int lid = xcd_remap(blockIdx.x, B * Hq * nqb);
   const int g = lid % G;
   lid /= G;
@@ -561,8 +589,8 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dq_kernel(
 
   const int tid = threadIdx.x, l = tid & 63, lr = l & 31, hh = l >> 5;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int q = qb * BQ8 + w * 32 + lr, qc = min(q, S - 1);
-  const int qmin_w = qb * BQ8 + w * 32, qmax_w = qmin_w + 31;
+  const int q = qb * RW + w * 32 + lr, qc = min(q, S - 1);
+  const int qmin_w = qb * RW + w * 32, qmax_w = qmin_w + 31;
   const bool live = qmin_w < S;
 
   bf16x8 qf[8], df[8];
@@ -579,8 +607,8 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dq_kernel(
   float dl = delta[((long)b * Hq + h) * S + qc];
   const bf16_t* kp = qkv + (long)b * S * ld + (long)(Hq + hkv) * D;
   const bf16_t* vp = qkv + (long)b * S * ld + (long)(Hq + Hkv + hkv) * D;
-  // wave w fills rows 4w.. and 4w+32.. of the K and V images: SGPR panel base + one 32-bit lane
-  // offset shared by K and V (same row stride; rows 32 apart share the chunk swizzle)
+  // wave w fills rows 4w.., 4w+4NW.. of the K and V images: SGPR panel base + one 32-bit lane
+  // offset shared by K and V (same row stride; rows 16 apart share the chunk swizzle)
   u32 dma_kv;
   {
     const int row = 4 * w + (l >> 4), ch = (l & 15) ^ swz_x(row);
@@ -590,15 +618,15 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dq_kernel(
   // a stage is 128 keys of K and V (the forward's staging: 8 DMA wave-instructions per wave,
   // 2-deep ring), computed as two 64-key halves under one barrier
   auto stage = [&](int j) {
-    const u32 st = lds_w + (j % NSF) * STGF;
-    const char* kb_ = reinterpret_cast<const char*>(kp + (long)j * BKF * ld);
-    const char* vb_ = reinterpret_cast<const char*>(vp + (long)j * BKF * ld);
+    const u32 st = lds_w + (j % NSF) * STG;
+    const char* kb_ = reinterpret_cast<const char*>(kp + (long)j * BKS * ld);
+    const char* vb_ = reinterpret_cast<const char*>(vp + (long)j * BKS * ld);
 #pragma unroll
-    for (int i = 0; i < NKT; ++i) dma_sv(kb_ + (long)64 * ld * i, dma_kv, st + 8192 * i);
+    for (int i = 0; i < C::NI; ++i) dma_sv(kb_ + (long)8 * NW * ld * i, dma_kv, st + 1024 * NW * i);
 #pragma unroll
-    for (int i = 0; i < NKT; ++i) dma_sv(vb_ + (long)64 * ld * i, dma_kv, st + TILEF + 8192 * i);
+    for (int i = 0; i < C::NI; ++i) dma_sv(vb_ + (long)8 * NW * ld * i, dma_kv, st + TILE + 1024 * NW * i);
   };
-  const int ntiles = CAUSAL ? min(S, qb * BQ8 + BQ8) / BKF : S / BKF;
+  const int ntiles = CAUSAL ? min(S, qb * RW + RW) / BKS : S / BKS;
   if (ntiles > 0) stage(0);
   // retire the register loads before the loop (see the forward)
 #pragma unroll
@@ -617,10 +645,10 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dq_kernel(
   for (int j = 0; j < ntiles; ++j) {
     if (j + 1 < ntiles) stage(j + 1);   // into the buffer every wave finished with (stage j-1)
 #pragma unroll
-    for (int hf = 0; hf < 2; ++hf) {
-    const int k0 = j * BKF + BK * hf;
+    for (int hf = 0; hf < C::NH; ++hf) {
+    const int k0 = j * BKS + BK * hf;
     if (live && (!CAUSAL || k0 <= qmax_w)) {
-      const u32 hoff = (u32)((j % NSF) * STGF + BK * 256 * hf);   // this half's K rows (V: + TILEF)
+      const u32 hoff = (u32)((j % NSF) * STG + BK * 256 * hf);   // this half's K rows (V: + TILE)
       const char* Ks = smem + hoff;
       // non-causal: an opaque false keeps the causal loop's shape (folded away, hipcc spilled)
       int nm = CAUSAL ? (k0 + BK - 1 > qmin_w) : 0;
@@ -638,7 +666,7 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dq_kernel(
       auto rdS = [&](auto ic) {
         constexpr int i = decltype(ic)::value, kt = i >> 3, ks = i & 7, sl = i % (QP + 1);
         fk[sl] = rd_b128<8192 * kt>(a_t ^ (32 * ks));
-        fv[sl] = rd_b128<TILEF + 8192 * kt>(a_t ^ (32 * ks));
+        fv[sl] = rd_b128<TILE + 8192 * kt>(a_t ^ (32 * ks));
       };
       static_for<0, QP>([&](auto ic) { rdS(ic); });
       // s_setprio 1 over the MFMA chains, 0 over the exp / pack VALU: the SIMD's other wave then
@@ -714,7 +742,7 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dq_kernel(
     }
   }
   if (!live) return;
-  store_rows_via_lds(dq, scale, smem + (ntiles % NSF) * STGF + 8192 * w,
+  store_rows_via_lds(dq, scale, smem + (ntiles % NSF) * STG + 8192 * w,
                      dqkv + ((long)b * S + qmin_w) * lddq + (long)h * D, lddq);
 }
 
@@ -997,16 +1025,19 @@ __global__ __launch_bounds__(256) void flash_bwd_post_kernel(const float* __rest
 
 extern "C" {
 
+// waves per forward workgroup (FwdCfg)
+constexpr int FWD_NW = 8;
+
 int kf_flash_fwd(const void* qkv, long ld, void* out, long ldo, float* lse, int B, int S, int Hq,
                  int Hkv, int D_, float scale, int causal, hipStream_t st) {
   if (D_ != D || S % BQ != 0 || Hq % Hkv != 0 || ld % 8 || ldo % 8) return 1;
-  const int grid = B * Hq * ((S + BQ8 - 1) / BQ8);
+  const int grid = B * Hq * ((S + FwdCfg<FWD_NW>::RW - 1) / FwdCfg<FWD_NW>::RW);
   const float sl2 = scale * LOG2E;
   if (causal)
-    flash_fwd_kernel<true><<<grid, 512, 0, st>>>((const bf16_t*)qkv, ld, (bf16_t*)out, ldo, lse, B, S,
+    flash_fwd_kernel<true, FWD_NW><<<grid, 64 * FWD_NW, 0, st>>>((const bf16_t*)qkv, ld, (bf16_t*)out, ldo, lse, B, S,
                                                  Hq, Hkv, sl2);
   else
-    flash_fwd_kernel<false><<<grid, 512, 0, st>>>((const bf16_t*)qkv, ld, (bf16_t*)out, ldo, lse, B,
+    flash_fwd_kernel<false, FWD_NW><<<grid, 64 * FWD_NW, 0, st>>>((const bf16_t*)qkv, ld, (bf16_t*)out, ldo, lse, B,
                                                   S, Hq, Hkv, sl2);
   return 0;
 }
@@ -1052,6 +1083,8 @@ BwdFork* bwd_fork() {
 }
 }  // namespace
 
+// waves per dQ workgroup (DqCfg)
+constexpr int DQ_NW = 8;
 // dk_acc/dv_acc: fp32 [B*S, Hkv*128] scratch (zeroed here); delta: fp32 [B, Hq, S] scratch.
 int kf_flash_bwd(const void* qkv, long ld, const void* o, long ldo, const void* dout, long lddo,
                  const float* lse, float* delta, float* dk_acc, float* dv_acc, void* dqkv,
@@ -1083,17 +1116,17 @@ int kf_flash_bwd(const void* qkv, long ld, const void* o, long ldo, const void* 
     return fail(2);
   int items = 0;
   for (int kb = 0; kb < S / BKVW; ++kb) items += n_chunks(kb, S, causal);
-  const int g_kv = B * Hkv * items, g_q = B * Hq * ((S + BQ8 - 1) / BQ8);
+  const int g_kv = B * Hkv * items, g_q = B * Hq * ((S + DqCfg<DQ_NW>::RW - 1) / DqCfg<DQ_NW>::RW);
   const float sl2 = scale * LOG2E;
   if (causal) {
     flash_bwd_dkdv_kernel<true><<<g_kv, 64 * NWK, 0, skv>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo, lse,
                                                          delta, dk_acc, dv_acc, B, S, Hq, Hkv, scale, items);
-    flash_bwd_dq_kernel<true><<<g_q, 512, 0, st>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo, lse,
+    flash_bwd_dq_kernel<true, DQ_NW><<<g_q, 64 * DQ_NW, 0, st>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo, lse,
                                                    delta, (bf16_t*)dqkv, lddqkv, B, S, Hq, Hkv, sl2, scale);
   } else {
     flash_bwd_dkdv_kernel<false><<<g_kv, 64 * NWK, 0, skv>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo, lse,
                                                           delta, dk_acc, dv_acc, B, S, Hq, Hkv, scale, items);
-    flash_bwd_dq_kernel<false><<<g_q, 512, 0, st>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo, lse,
+    flash_bwd_dq_kernel<false, DQ_NW><<<g_q, 64 * DQ_NW, 0, st>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo, lse,
                                                     delta, (bf16_t*)dqkv, lddqkv, B, S, Hq, Hkv, sl2, scale);
   }
   if (skv != st &&

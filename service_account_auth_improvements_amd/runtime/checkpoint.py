@@ -376,11 +376,23 @@ class PeriodicCheckpointer:
         os.makedirs(root, exist_ok=True)
         self._pinned: Dict[str, torch.Tensor] = {}
         self._stream = torch.cuda.Stream(device=self.device) if self.device.type == "cuda" else None
+        # page-locking the host snapshot (112 GB at 8B on one rank) takes seconds: done once, on a
+        # side thread started now, so the first save() finds the buffers ready instead of stalling
+        self._prep = None
+        if self._stream is not None and self.flat:
+            shapes = {k: (tuple(v.shape), v.dtype) for k, v in _flat_state(trainer)[0].items()}
+            self._prep = threading.Thread(target=self._allocate_pinned, args=(shapes,), name="kfamd-ckpt-pin",
+                                          daemon=True)
+            self._prep.start()
         self._thread: Optional[threading.Thread] = None
         self._error: Optional[BaseException] = None
         self.last_published: Optional[int] = None
         self.last_seconds: Optional[float] = None
         self.snapshot_seconds: Optional[float] = None
+
+    def _allocate_pinned(self, shapes):
+        for k, (shape, dtype) in shapes.items():
+            self._pinned[k] = torch.empty(shape, dtype=dtype, pin_memory=True)
 
     # -- snapshot (caller's thread)
     def _host_copy(self, key: str, t: torch.Tensor) -> torch.Tensor:
@@ -395,6 +407,9 @@ class PeriodicCheckpointer:
     def save(self, step: int):
         """Snapshot the state after optimizer step ``step`` and write it in the background."""
         self.wait()                       # the previous write owns the pinned buffers
+        if self._prep is not None:
+            self._prep.join()
+            self._prep = None
         tr = self.trainer
         t0 = time.perf_counter()
         path = step_dir(self.root, step)

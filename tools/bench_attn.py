@@ -3,7 +3,9 @@ own fused attention (torch SDPA: the vendor AOTriton / CK flash path) at Llama-3
 causal GQA 32/8, d=128.  Both sides get the same bf16 inputs; times are per call (hip events
 via torch.cuda.synchronize around 20 calls after 3 warm-ups).
 
-  python tools/bench_attn.py [B:S ...]        (default 2:8192 1:32768)
+  python tools/bench_attn.py [--hip-only] [--iters N] [B:S ...]        (default 2:8192 1:32768)
+
+``--hip-only`` skips SDPA (A/B runs of two extension builds, tools/gpu_session.sh ``ext:``).
 """
 import math
 import os
@@ -20,7 +22,12 @@ from service_account_auth_improvements_amd.ops.attention import _split, attentio
 assert _ext.load(), "HIP extension not loaded"
 
 
-def bench(fn, it=20):
+HIP_ONLY = "--hip-only" in sys.argv
+ITERS = next((int(a.split("=", 1)[1]) for a in sys.argv if a.startswith("--iters=")), 20)
+
+
+def bench(fn, it=None):
+    it = it or ITERS
     for _ in range(3):
         fn()
     torch.cuda.synchronize()
@@ -32,7 +39,7 @@ def bench(fn, it=20):
 
 
 Hq, Hkv, D = 32, 8, 128
-shapes = [tuple(int(v) for v in a.split(":")) for a in sys.argv[1:]] or [(2, 8192), (1, 32768)]
+shapes = [tuple(int(v) for v in a.split(":")) for a in sys.argv[1:] if not a.startswith("--")] or [(2, 8192), (1, 32768)]
 for B, S in shapes:
     torch.manual_seed(0)
     qkv = torch.randn(B * S, (Hq + 2 * Hkv) * D, device="cuda", dtype=torch.bfloat16)
@@ -41,6 +48,11 @@ for B, S in shapes:
     o, lse = attention_fwd(qkv, B, S, Hq, Hkv, D)
     do = torch.randn_like(o)
     t_b = bench(lambda: attention_bwd(qkv, o, lse, do, B, S, Hq, Hkv, D))
+    tf = lambda t, prods: prods / 2 * fl / t / 1e12  # noqa: E731
+    if HIP_ONLY:
+        print(f"B={B} S={S}  hip  fwd {t_f * 1e3:7.3f} ms {tf(t_f, 2):5.0f} TF | bwd {t_b * 1e3:7.3f} ms "
+              f"{tf(t_b, 5):5.0f} TF | fwd+bwd {(t_f + t_b) * 1e3:7.3f} ms", flush=True)
+        continue
     # SDPA on [B, H, S, D] tensors of the same values
     q, k, v = (x.contiguous() for x in _split(qkv, B, S, Hq, Hkv, D))
     for x in (q, k, v):
