@@ -96,6 +96,24 @@ def main():
     rate = 7 * a.link_gbs
     results = []
     proxies = {}
+    # what C workgroups can move at all (unpaced, no training): below the modelled link rate the
+    # proxy itself becomes the exposed communication, as an RCCL run with too few channels would
+    unpaced = {}
+    for ch in sorted({int(x) for x in a.channels.split(",") if int(x) > 0}):
+        px = Proxy(lib, ch, 1e6, bucket_bytes)
+        n = (bucket_bytes // (16 * ch)) * 16 * ch
+        for _ in range(2):
+            px._launch(n * WORLD // (WORLD - 1))
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(px.stream)
+        for _ in range(5):
+            px._launch(n * WORLD // (WORLD - 1))
+        e1.record(px.stream)
+        torch.cuda.synchronize()
+        unpaced[ch] = round(5 * px.bytes_moved / 7 / (e0.elapsed_time(e1) / 1e3) / 1e9, 1)
+        del px
+        print(json.dumps({"channels": ch, "unpaced_copy_gbs": unpaced[ch], "modelled_link_gbs": rate}), flush=True)
     for ch in [int(x) for x in a.channels.split(",")]:
         if ch > 0 and ch not in proxies:
             proxies[ch] = Proxy(lib, ch, rate, bucket_bytes)
@@ -124,7 +142,8 @@ def main():
     for r in results:
         if r["channels"]:
             t8 = r["ms_per_step"] + tail_ms
-            summary["predicted"][str(r["channels"])] = {"slowdown_pct": round(100 * (r["ms_per_step"] / t1 - 1), 2),
+            summary["predicted"][str(r["channels"])] = {"unpaced_copy_gbs": unpaced.get(r["channels"]),
+                                                        "slowdown_pct": round(100 * (r["ms_per_step"] / t1 - 1), 2),
                                                         "n8_ms_per_step": round(t8, 1),
                                                         "n8_efficiency": round(t1 / t8, 4)}
     print(json.dumps({"summary": summary}), flush=True)

@@ -45,6 +45,7 @@ for step in "$@"; do
   case "$kind" in
     tests)
       log=$O/pytest.log
+      [ -f "$log" ] && log=$O/pytest_$n.log     # a second tests step in one session keeps the first log
       k=(); [ -n "$a1" ] && k=(-k "$a1")
       timeout -k 10 900 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu tests "${k[@]}" > "$log" 2>&1 \
         || fail "$step" $? "$log"

@@ -17,6 +17,8 @@
 namespace {
 constexpr int NT = 256;          // threads per workgroup (an RCCL channel runs 256-512)
 constexpr int PIECE = 65536;     // bytes per paced piece
+constexpr int U = 8;             // 16-B loads in flight per thread (32 KB per workgroup), as a channel
+                                 // kernel keeps many outstanding: ~15-20 GB/s per workgroup
 
 __global__ __launch_bounds__(NT) void proxy_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
                                                     long bytes_per_block, long ticks_per_piece) {
@@ -29,11 +31,17 @@ __global__ __launch_bounds__(NT) void proxy_kernel(const uint4* __restrict__ src
   long piece = 0;
   for (long base = 0; base < n16; base += p16, ++piece) {
     const long end = base + p16 < n16 ? base + p16 : n16;
-    for (long i = base + threadIdx.x; i < end; i += NT) {
-      uint4 v = s[i];
-      fifo[threadIdx.x] = v;
-      d[i] = fifo[threadIdx.x];
+    long i0 = base + threadIdx.x;
+    for (; i0 + (long)(U - 1) * NT < end; i0 += (long)NT * U) {
+      uint4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = s[i0 + (long)u * NT];
+#pragma unroll
+      for (int u = 0; u < U; ++u) d[i0 + (long)u * NT] = v[u];
     }
+    for (; i0 < end; i0 += NT) d[i0] = s[i0];
+    fifo[threadIdx.x] = s[base];    // the FIFO reservation stays live (read below, never taken)
+    if (ticks_per_piece < 0) d[base] = fifo[threadIdx.x ^ 1];
     // pace: piece k may finish no earlier than t0 + (k + 1) * ticks_per_piece
     const uint64_t due = t0 + (uint64_t)(piece + 1) * (uint64_t)ticks_per_piece;
     while (__builtin_amdgcn_s_memrealtime() < due) __builtin_amdgcn_s_sleep(8);
