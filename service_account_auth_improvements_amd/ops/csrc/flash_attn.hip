@@ -1071,7 +1071,12 @@ BwdFork* bwd_fork() {
   BwdFork& f = per_dev[dev];
   std::lock_guard<std::mutex> lk(f.mu);
   if (!f.side) {
-    if (hipStreamCreateWithFlags(&f.side, hipStreamNonBlocking) != hipSuccess ||
+    // the dK/dV chain (the longer kernel) on the device's highest-priority stream: its workgroups are
+    // dispatched ahead of dQ's, which fill the CUs around them (backward 7.370-7.376 vs 7.451-7.461
+    // ms at B4 S8192, alternating builds on one box: profiles/fa_structure_r6.md)
+    int lo_prio = 0, hi_prio = 0;
+    (void)hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio);
+    if (hipStreamCreateWithPriority(&f.side, hipStreamNonBlocking, hi_prio) != hipSuccess ||
         hipEventCreateWithFlags(&f.fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&f.pre, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&f.join, hipEventDisableTiming) != hipSuccess) {

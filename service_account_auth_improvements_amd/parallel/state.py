@@ -134,6 +134,11 @@ def init_distributed(tp: int = 1, pp: int = 1, backend: Optional[str] = None,
             kw = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
             if backend == "nccl":
                 kw["device_id"] = dev
+                # at least 32 RCCL channels: the one-GPU DP8 proxy (profiles/dp8_overlap_proxy.md)
+                # moves the step's ~28 GB at the modelled 7-link xGMI rate only from 32 channel
+                # workgroups up (8 / 16 fall short and the all-to-all is exposed, +4 %); 32 and 64 cost
+                # the step 0.7 / 1.1 %, inside the run spread, so no upper cap is set
+                os.environ.setdefault("NCCL_MIN_NCHANNELS", "32")
             dist.init_process_group(**kw)
         # rank = ((pp_rank * dp) + dp_rank) * tp + tp_rank
         st.tp_rank = rank % tp
