@@ -252,3 +252,19 @@ def test_zero1_state_is_resharded_when_the_data_parallel_size_changes(tmp_path):
         with open(tmp_path / f"R{w}" / "meta.json") as f:
             meta = json.load(f)
         assert meta["step"] == 2 and meta["parallel"]["dp"] == w
+
+
+def test_hip_preinit_is_skipped_for_cpu_jobs_and_when_disabled(monkeypatch):
+    """train_entry._hip_preinit: never for --device cpu or KFAMD_HIP_PREINIT=0 (and never where
+    there is no GPU device node); otherwise one daemon thread that loads torch's own HIP runtime."""
+    from service_account_auth_improvements_amd.runtime import train_entry as te
+    assert te._hip_preinit("cpu") is None
+    monkeypatch.setenv("KFAMD_HIP_PREINIT", "0")
+    assert te._hip_preinit("auto") is None
+    monkeypatch.setenv("KFAMD_HIP_PREINIT", "1")
+    t = te._hip_preinit("auto")
+    if not os.path.exists("/dev/kfd"):
+        assert t is None
+    else:
+        assert t.daemon and t.name == "kfamd-hip-preinit"
+        t.join(timeout=30)
