@@ -1,0 +1,130 @@
+"""Checkpoint-restart on the GPU, end to end (GPU counterpart of
+tests/test_checkpoint_restart_elastic.py).
+
+kfamd-launch (the PyTorchJob pod's agent, ``--max-restarts 2``) runs the worker
+(runtime/train_entry.py) on the Llama-3-8B architecture with ``--ckpt-dir --save-every``.  Once a
+checkpoint is published and the worker is two steps past it, the worker process is SIGKILLed.  The
+agent restarts it, the new worker resumes from ``latest`` and finishes the job.  A second,
+uninterrupted run of the same command is the reference.  One JSON line:
+
+  kill -> resumed worker's first step (recovery time) and its parts, the resumed step, and
+  whether every step's loss after the resume equals the uninterrupted run's bit for bit.
+
+  python tools/bench_restart_gpu.py [--layers 8] [--steps 16] [--save-every 5]
+"""
+import argparse
+import json
+import os
+import shutil
+import signal
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def _events(path):
+    out = []
+    try:
+        with open(path) as f:
+            for line in f:
+                try:
+                    out.append(json.loads(line))
+                except ValueError:
+                    pass
+    except OSError:
+        pass
+    return out
+
+
+def run(a, tag, kill: bool, tmp):
+    from service_account_auth_improvements_amd import native
+    ev = os.path.join(tmp, f"{tag}.events")
+    ck = os.path.join(a.ckpt_root, tag)
+    shutil.rmtree(ck, ignore_errors=True)
+    cmd = [native.binary("kfamd_launch"), "--nnodes", "1", "--nproc-per-node", "1", "--master-addr", "127.0.0.1",
+           "--master-port", str(a.port), "--max-restarts", "2", "--",
+           sys.executable, "-m", "service_account_auth_improvements_amd", "train", "--model", a.model,
+           "--seq-len", str(a.seq_len), "--micro-batch", str(a.micro_batch), "--zero1", "--device", a.device,
+           "--steps", str(a.steps), "--ckpt-dir", ck, "--save-every", str(a.save_every)]
+    if a.layers:
+        cmd[cmd.index("--seq-len"):cmd.index("--seq-len")] = ["--layers", str(a.layers)]
+    env = dict(os.environ, KFAMD_EVENTS_FILE=ev, PYTHONPATH=ROOT)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    log = open(os.path.join(tmp, f"{tag}.log"), "w")
+    p = subprocess.Popen(cmd, env=env, cwd=ROOT, stdout=log, stderr=subprocess.STDOUT)
+    killed = None
+    deadline = time.time() + a.timeout
+    try:
+        while p.poll() is None:
+            if time.time() > deadline:
+                raise TimeoutError(f"{tag}: no exit within {a.timeout} s")
+            if kill and killed is None:
+                recs = _events(ev)
+                pub = [e for e in recs if e["event"] == "checkpoint_published"]
+                st = [e for e in recs if e["event"] == "step"]
+                if pub and st and st[-1]["step"] >= pub[0]["step"] + 2:
+                    killed = {"pid": st[-1]["pid"], "at_step": st[-1]["step"], "latest": pub[-1]["step"],
+                              "t": time.time()}
+                    os.kill(killed["pid"], signal.SIGKILL)
+            time.sleep(0.05)
+    finally:
+        if p.poll() is None:
+            p.kill()
+        shutil.rmtree(ck, ignore_errors=True)
+    if p.returncode != 0:
+        raise RuntimeError(f"{tag}: launcher exit {p.returncode}; see {log.name}")
+    return _events(ev), killed
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--seq-len", type=int, default=8192)
+    ap.add_argument("--device", default="auto")
+    ap.add_argument("--layers", type=int, default=8, help="0 = the model's own depth")
+    ap.add_argument("--steps", type=int, default=16)
+    ap.add_argument("--save-every", type=int, default=5)
+    ap.add_argument("--micro-batch", type=int, default=4)
+    ap.add_argument("--ckpt-root", default="/dev/shm/kfamd_restart")
+    ap.add_argument("--port", type=int, default=29911)
+    ap.add_argument("--timeout", type=float, default=500)
+    a = ap.parse_args()
+    tmp = tempfile.mkdtemp(prefix="restart-gpu-")
+    ref, _ = run(a, "ref", False, tmp)
+    got, killed = run(a, "kill", True, tmp)
+    if killed is None:
+        raise RuntimeError("the run finished before the kill")
+
+    def losses(evs):
+        out = {}
+        for e in evs:
+            if e["event"] == "step":
+                out.setdefault(e["step"], []).append(e["loss"])
+        return out
+    lr, lg = losses(ref), losses(got)
+    res = [e for e in got if e["event"] == "resumed"]
+    second = [e for e in got if e["event"] == "process_start"][-1]
+    after = [e for e in got if e["ts"] >= second["ts"]]
+
+    def t_of(kind):
+        return next(e["ts"] for e in after if e["event"] == kind)
+    out = {"layers": a.layers, "micro_batch": a.micro_batch, "killed_at_step": killed["at_step"],
+           "resumed_from_step": res[-1]["step"] if res else None,
+           "recovery_s": round(t_of("first_step") - killed["t"], 2),
+           "restart_to_process_s": round(second["ts"] - killed["t"], 2),
+           "import_s": round(t_of("imported") - second["ts"], 2),
+           "init_and_load_s": round(t_of("resumed") - t_of("imported"), 2),
+           "resumed_to_first_step_s": round(t_of("first_step") - t_of("resumed"), 2),
+           "steps_rerun": sorted(s for s, v in lg.items() if len(v) > 1),
+           "losses_match_uninterrupted": all(all(v == lr[s][0] for v in lg[s]) for s in lr) and set(lg) == set(lr),
+           "publish_s": [e["seconds"] for e in got if e["event"] == "checkpoint_published"]}
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
