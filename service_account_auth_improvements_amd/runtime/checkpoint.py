@@ -379,7 +379,7 @@ class PeriodicCheckpointer:
         # page-locking the host snapshot (112 GB at 8B on one rank) takes seconds: done once, on a
         # side thread started now, so the first save() finds the buffers ready instead of stalling
         self._prep = None
-        if self._stream is not None and self.flat:
+        if self._stream is not None and self.flat and os.environ.get("KFAMD_CKPT_PREPIN", "1") != "0":
             shapes = {k: (tuple(v.shape), v.dtype) for k, v in _flat_state(trainer)[0].items()}
             self._prep = threading.Thread(target=self._allocate_pinned, args=(shapes,), name="kfamd-ckpt-pin",
                                           daemon=True)
