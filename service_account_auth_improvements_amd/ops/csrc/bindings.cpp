@@ -35,7 +35,8 @@ int kf_cross_entropy(void*, long, int, int, const long*, long, long, float*, flo
 int kf_flash_fwd(const void*, long, void*, long, float*, int, int, int, int, int, float, int,
                  hipStream_t);
 int kf_flash_bwd(const void*, long, const void*, long, const void*, long, const float*, float*,
-                 float*, float*, void*, long, int, int, int, int, int, float, int, hipStream_t);
+                 float*, float*, void*, long, int, int, int, int, int, float, int, int, hipStream_t);
+long kf_flash_bwd_acc_floats(int, int, int, int, int);
 int kf_decode_splits(int, int, int);
 int kf_decode_splits1(int, int, int);
 int kf_decode_attn_fused(const void*, long, const void*, const void*, const int*, const int*, void*, long, float*,
@@ -271,7 +272,7 @@ std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& qkv, int64_t B, i
 
 at::Tensor flash_bwd(const at::Tensor& qkv, const at::Tensor& o, const at::Tensor& lse,
                      const at::Tensor& dout, int64_t B, int64_t S, int64_t Hq, int64_t Hkv, int64_t D,
-                     double scale, bool causal) {
+                     double scale, bool causal, bool deterministic) {
   check_bf16_cuda(qkv, "qkv");
   check_bf16_cuda(o, "o");
   check_bf16_cuda(dout, "dout");
@@ -284,14 +285,16 @@ at::Tensor flash_bwd(const at::Tensor& qkv, const at::Tensor& o, const at::Tenso
   c10::hip::HIPGuardMasqueradingAsCUDA g(qkv.device());
   auto f32 = qkv.options().dtype(at::kFloat);
   auto delta = at::empty({B, Hq, S}, f32);
-  auto acc = at::empty({2 * B * S * Hkv * D}, f32);   // zeroed by kf_flash_bwd on its dK/dV stream
+  // zeroed by kf_flash_bwd on its dK/dV stream (atomic mode) or fully stored (deterministic slots)
+  const long nacc = kf_flash_bwd_acc_floats((int)B, (int)S, (int)Hkv, causal ? 1 : 0, deterministic ? 1 : 0);
+  auto acc = at::empty({2 * nacc}, f32);
   float* dk = acc.data_ptr<float>();
-  float* dv = dk + B * S * Hkv * D;
+  float* dv = dk + nacc;
   auto dqkv = at::empty({B * S, (Hq + 2 * Hkv) * D}, qkv.options());
   check_rc(kf_flash_bwd(qkv.data_ptr(), qkv.stride(0), o.data_ptr(), o.stride(0), dout.data_ptr(),
                         dout.stride(0), lse.data_ptr<float>(), delta.data_ptr<float>(), dk, dv,
                         dqkv.data_ptr(), dqkv.stride(0), (int)B, (int)S, (int)Hq, (int)Hkv, (int)D,
-                        (float)scale, causal ? 1 : 0, cur_stream()),
+                        (float)scale, causal ? 1 : 0, deterministic ? 1 : 0, cur_stream()),
            "flash_bwd");
   return dqkv;
 }

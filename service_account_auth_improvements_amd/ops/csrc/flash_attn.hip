@@ -785,7 +785,9 @@ __host__ __device__ inline int n_chunks(int kb, int S, bool causal) {
 }
 }  // namespace fb
 
-template <bool CAUSAL>
+// DET (deterministic mode) is a template parameter, not a run-time flag: the atomic
+// instantiation compiles to round 5's instruction stream, whose main loop is hand-scheduled
+template <bool CAUSAL, bool DET>
 __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kernel(
     const bf16_t* __restrict__ qkv, long ld, const bf16_t* __restrict__ dout, long lddo,
     const float* __restrict__ lse, const float* __restrict__ delta, float* __restrict__ dk_acc,
@@ -795,6 +797,7 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
   const int G = Hq / Hkv;
   const int lid = xcd_remap(blockIdx.x, B * Hkv * items_per_head);
   int item = lid % items_per_head;
+  const int slot = item;            // this work item's partial-sum slot (DET)
   const int bh = lid / items_per_head;
   const int hkv = bh % Hkv, b = bh / Hkv;
   const int nkb = S / BKVW;
@@ -995,10 +998,21 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
           }
       }
       __syncthreads();
-      float* dst = dst_base + (rowB + kv0 + 128 * pass) * (long)(Hkv * D) + (long)hkv * D;
-      for (int e = tid; e < 128 * 128; e += 64 * NWK) {
-        const int key = e >> 7, d = e & 127;
-        atomicAdd(dst + (long)key * Hkv * D + d, T[key * 128 + (d ^ ((key & 31) << 2))]);
+      // atomics: every work item of a key block adds into one [T, Hkv*D] accumulator (fp32 sum
+      // order varies run to run); deterministic mode: each item stores its partial into its own
+      // slot rows, and flash_bwd_post_kernel sums a key block's slots in item order
+      float* dst = DET ? dst_base + ((long)(b * items_per_head + slot) * BKVW + 128 * pass) * (long)(Hkv * D) + (long)hkv * D
+                       : dst_base + (rowB + kv0 + 128 * pass) * (long)(Hkv * D) + (long)hkv * D;
+      if constexpr (DET) {
+        for (int e = tid; e < 128 * 128; e += 64 * NWK) {
+          const int key = e >> 7, d = e & 127;
+          dst[(long)key * Hkv * D + d] = T[key * 128 + (d ^ ((key & 31) << 2))];
+        }
+      } else {
+        for (int e = tid; e < 128 * 128; e += 64 * NWK) {
+          const int key = e >> 7, d = e & 127;
+          atomicAdd(dst + (long)key * Hkv * D + d, T[key * 128 + (d ^ ((key & 31) << 2))]);
+        }
       }
       __syncthreads();
     }
@@ -1007,19 +1021,41 @@ __global__ __launch_bounds__(64 * fb::NWK, 8 / fb::NWK) void flash_bwd_dkdv_kern
   flush(dV, 1.f, dv_acc);
 }
 
-// fp32 dK/dV accumulators -> bf16 k/v columns of the fused dqkv [T, (Hq + 2Hkv) * 128]
+// fp32 dK/dV accumulators -> bf16 k/v columns of the fused dqkv [T, (Hq + 2Hkv) * 128].
+// Deterministic mode (ns > 0): the accumulators are per-work-item slots [B][ns][BKVW][Hkv * 128],
+// and each key's value is the sum of its key block's slots in item order.
 __global__ __launch_bounds__(256) void flash_bwd_post_kernel(const float* __restrict__ dk,
                                                              const float* __restrict__ dv,
                                                              bf16_t* __restrict__ dqkv, long ld, int T,
-                                                             int Hq, int Hkv) {
+                                                             int Hq, int Hkv, int S, int ns, int causal) {
   const int ck = Hkv * 16, per_row = 2 * ck;   // 8-element chunks
   const long total = (long)T * per_row;
+  const long row_f = (long)Hkv * 128;
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
     const int t = (int)(i / per_row), c = (int)(i - (long)t * per_row);
-    const float* src = c < ck ? dk + (long)t * Hkv * 128 + c * 8 : dv + (long)t * Hkv * 128 + (c - ck) * 8;
-    const f32x4 a = ldf4(src), bb = ldf4(src + 4);
-    const float f[8] = {a[0], a[1], a[2], a[3], bb[0], bb[1], bb[2], bb[3]};
-    st16(dqkv + (long)t * ld + Hq * 128 + c * 8, pack8(f));
+    const float* base = c < ck ? dk : dv;
+    const int col = (c < ck ? c : c - ck) * 8;
+    float f[8];
+    if (ns == 0) {
+      const float* src = base + (long)t * row_f + col;
+      const f32x4 a = ldf4(src), bb = ldf4(src + 4);
+      f[0] = a[0]; f[1] = a[1]; f[2] = a[2]; f[3] = a[3]; f[4] = bb[0]; f[5] = bb[1]; f[6] = bb[2]; f[7] = bb[3];
+    } else {
+      using namespace fb;
+      const int b = t / S, key = t - b * S, kb = key / BKVW, kl = key - kb * BKVW;
+      int slot0 = 0;
+      for (int k = 0; k < kb; ++k) slot0 += n_chunks(k, S, causal != 0);
+      const int nc = n_chunks(kb, S, causal != 0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = 0.f;
+      for (int cc = 0; cc < nc; ++cc) {
+        const float* src = base + ((long)(b * ns + slot0 + cc) * BKVW + kl) * row_f + col;
+        const f32x4 a = ldf4(src), bb = ldf4(src + 4);
+        f[0] += a[0]; f[1] += a[1]; f[2] += a[2]; f[3] += a[3];
+        f[4] += bb[0]; f[5] += bb[1]; f[6] += bb[2]; f[7] += bb[3];
+      }
+    }
+    st16(dqkv + (long)t * ld + Hq * 128 + (c < ck ? 0 : Hkv * 128) + col, pack8(f));
   }
 }
 
@@ -1090,14 +1126,30 @@ BwdFork* bwd_fork() {
 
 // waves per dQ workgroup (DqCfg)
 constexpr int DQ_NW = 8;
-// dk_acc/dv_acc: fp32 [B*S, Hkv*128] scratch (zeroed here); delta: fp32 [B, Hq, S] scratch.
+// dK/dV work items per (batch, kv head): one per key block and query chunk
+static int dkdv_items(int S, int causal) {
+  int items = 0;
+  for (int kb = 0; kb < S / fb::BKVW; ++kb) items += fb::n_chunks(kb, S, causal);
+  return items;
+}
+// floats of ONE of the two dK / dV scratch buffers kf_flash_bwd needs: [B*S, Hkv*128] for the
+// atomic accumulation, [B][items][BKVW][Hkv*128] partial slots in deterministic mode
+long kf_flash_bwd_acc_floats(int B, int S, int Hkv, int causal, int deterministic) {
+  if (deterministic) return (long)B * dkdv_items(S, causal) * fb::BKVW * Hkv * D;
+  return (long)B * S * Hkv * D;
+}
+
+// dk_acc/dv_acc: fp32 scratch of kf_flash_bwd_acc_floats each (zeroed here in the atomic mode);
+// delta: fp32 [B, Hq, S] scratch.  deterministic = 1: bitwise run-to-run reproducible dK/dV
+// (per-item partial slots summed in a fixed order by the post kernel instead of fp32 atomics).
 int kf_flash_bwd(const void* qkv, long ld, const void* o, long ldo, const void* dout, long lddo,
                  const float* lse, float* delta, float* dk_acc, float* dv_acc, void* dqkv,
                  long lddqkv, int B, int S, int Hq, int Hkv, int D_, float scale, int causal,
-                 hipStream_t st) {
+                 int deterministic, hipStream_t st) {
   using namespace fb;
   if (D_ != D || S % BKVW != 0 || S % BQ != 0 || Hq % Hkv != 0) return 1;
   const int T = B * S;
+  const int det = deterministic ? 1 : 0;
   const size_t acc_bytes = (size_t)T * Hkv * D * sizeof(float);
   BwdFork* fk = bwd_fork_enabled() ? bwd_fork() : nullptr;
   std::unique_lock<std::mutex> lk;
@@ -1111,35 +1163,41 @@ int kf_flash_bwd(const void* qkv, long ld, const void* o, long ldo, const void* 
     if (skv != st && hipEventRecord(fk->join, skv) == hipSuccess) (void)hipStreamWaitEvent(st, fk->join, 0);
     return rc;
   };
-  if (hipMemsetAsync(dk_acc, 0, acc_bytes, skv) != hipSuccess ||
-      hipMemsetAsync(dv_acc, 0, acc_bytes, skv) != hipSuccess)
+  // deterministic mode: every slot row is stored by its work item, nothing to zero
+  if (!det && (hipMemsetAsync(dk_acc, 0, acc_bytes, skv) != hipSuccess ||
+               hipMemsetAsync(dv_acc, 0, acc_bytes, skv) != hipSuccess))
     return fail(2);
   flash_bwd_pre_kernel<<<(T * Hq + 15) / 16, 256, 0, st>>>((const bf16_t*)o, ldo, (const bf16_t*)dout,
                                                            lddo, delta, B, S, Hq);
   if (skv != st &&
       (hipEventRecord(fk->pre, st) != hipSuccess || hipStreamWaitEvent(skv, fk->pre, 0) != hipSuccess))
     return fail(2);
-  int items = 0;
-  for (int kb = 0; kb < S / BKVW; ++kb) items += n_chunks(kb, S, causal);
+  const int items = dkdv_items(S, causal);
   const int g_kv = B * Hkv * items, g_q = B * Hq * ((S + DqCfg<DQ_NW>::RW - 1) / DqCfg<DQ_NW>::RW);
   const float sl2 = scale * LOG2E;
+  const bf16_t* q_ = (const bf16_t*)qkv;
+  const bf16_t* do_ = (const bf16_t*)dout;
+  auto dkdv = [&](auto kern) {
+    kern<<<g_kv, 64 * NWK, 0, skv>>>(q_, ld, do_, lddo, lse, delta, dk_acc, dv_acc, B, S, Hq, Hkv, scale, items);
+  };
   if (causal) {
-    flash_bwd_dkdv_kernel<true><<<g_kv, 64 * NWK, 0, skv>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo, lse,
-                                                         delta, dk_acc, dv_acc, B, S, Hq, Hkv, scale, items);
-    flash_bwd_dq_kernel<true, DQ_NW><<<g_q, 64 * DQ_NW, 0, st>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo, lse,
-                                                   delta, (bf16_t*)dqkv, lddqkv, B, S, Hq, Hkv, sl2, scale);
+    if (det) dkdv(flash_bwd_dkdv_kernel<true, true>);
+    else dkdv(flash_bwd_dkdv_kernel<true, false>);
+    flash_bwd_dq_kernel<true, DQ_NW><<<g_q, 64 * DQ_NW, 0, st>>>(q_, ld, do_, lddo, lse, delta, (bf16_t*)dqkv, lddqkv, B,
+                                                                 S, Hq, Hkv, sl2, scale);
   } else {
-    flash_bwd_dkdv_kernel<false><<<g_kv, 64 * NWK, 0, skv>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo, lse,
-                                                          delta, dk_acc, dv_acc, B, S, Hq, Hkv, scale, items);
-    flash_bwd_dq_kernel<false, DQ_NW><<<g_q, 64 * DQ_NW, 0, st>>>((const bf16_t*)qkv, ld, (const bf16_t*)dout, lddo, lse,
-                                                    delta, (bf16_t*)dqkv, lddqkv, B, S, Hq, Hkv, sl2, scale);
+    if (det) dkdv(flash_bwd_dkdv_kernel<false, true>);
+    else dkdv(flash_bwd_dkdv_kernel<false, false>);
+    flash_bwd_dq_kernel<false, DQ_NW><<<g_q, 64 * DQ_NW, 0, st>>>(q_, ld, do_, lddo, lse, delta, (bf16_t*)dqkv, lddqkv, B,
+                                                                  S, Hq, Hkv, sl2, scale);
   }
   if (skv != st &&
       (hipEventRecord(fk->join, skv) != hipSuccess || hipStreamWaitEvent(st, fk->join, 0) != hipSuccess))
     return 2;
   const long chunks = (long)T * Hkv * 32;
   const int pg = (int)std::min<long>((chunks + 255) / 256, 16384);
-  flash_bwd_post_kernel<<<pg, 256, 0, st>>>(dk_acc, dv_acc, (bf16_t*)dqkv, lddqkv, T, Hq, Hkv);
+  flash_bwd_post_kernel<<<pg, 256, 0, st>>>(dk_acc, dv_acc, (bf16_t*)dqkv, lddqkv, T, Hq, Hkv, S,
+                                            det ? items : 0, causal);
   return 0;
 }
 }

@@ -74,12 +74,32 @@ def _fsync_dir(path: str):
         os.close(fd)
 
 
+class HostPieces:
+    """A tensor's host copy as consecutive byte pieces (page-locked snapshot buffers): its shape
+    and dtype, and the uint8 CPU tensors holding its bytes in order."""
+    __slots__ = ("shape", "dtype", "pieces")
+
+    def __init__(self, shape, dtype, pieces):
+        self.shape, self.dtype, self.pieces = tuple(shape), dtype, pieces
+
+    @property
+    def nbytes(self) -> int:
+        return sum(p.numel() for p in self.pieces)
+
+
 def write_safetensors(path: str, tensors: Dict[str, torch.Tensor], metadata: Optional[dict] = None):
-    """Stream CPU tensors into a safetensors file: header, then each tensor's bytes written
-    straight from its memory (no bytes copy of a 30 GB master shard), fsync, atomic rename."""
+    """Stream CPU tensors (or :class:`HostPieces`) into a safetensors file: header, then each
+    tensor's bytes written straight from its memory (no bytes copy of a 30 GB master shard),
+    fsync, atomic rename."""
     header, off, order = {}, 0, []
     for k in sorted(tensors):
         t = tensors[k]
+        if isinstance(t, HostPieces):
+            n = t.nbytes
+            header[k] = {"dtype": _ST_DTYPE[t.dtype], "shape": list(t.shape), "data_offsets": [off, off + n]}
+            order.append(k)
+            off += n
+            continue
         if t.device.type != "cpu":
             raise ValueError(f"{k}: write_safetensors takes host tensors")
         n = t.numel() * t.element_size()
@@ -95,7 +115,12 @@ def write_safetensors(path: str, tensors: Dict[str, torch.Tensor], metadata: Opt
         f.write(struct.pack("<Q", len(hb)))
         f.write(hb)
         for k in order:
-            t = tensors[k].contiguous()
+            t = tensors[k]
+            if isinstance(t, HostPieces):
+                for piece in t.pieces:
+                    f.write(memoryview(piece.numpy()))
+                continue
+            t = t.contiguous()
             if t.numel():
                 f.write(memoryview(t.reshape(-1).view(torch.uint8).numpy()))
         f.flush()
@@ -348,6 +373,42 @@ def step_dir(root: str, step: int) -> str:
     return os.path.join(root, f"step-{step:08d}")
 
 
+PIN_PIECE = 256 << 20          # bytes per page-locked snapshot piece
+
+
+class PinnedPieces:
+    """Page-locked host memory for checkpoint snapshots, from the HIP runtime torch itself loaded,
+    called through ctypes (which releases the GIL for the whole call) in pieces of at most
+    ``PIN_PIECE`` bytes (which keeps the runtime's own locks short).  ``torch.empty(...,
+    pin_memory=True)`` of whole multi-GB tensors on a side thread held both for seconds: the
+    training loop's first step waited 4.2 s behind it (profiles/ckpt_cost_r6.md).  Freed by
+    :meth:`free` (the checkpointer's ``close``)."""
+
+    def __init__(self):
+        import ctypes
+        self._ct = ctypes
+        lib = os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so")
+        self._hip = ctypes.CDLL(lib) if os.path.exists(lib) else ctypes.CDLL("libamdhip64.so")
+        self._ptrs: List[int] = []
+
+    def alloc(self, nbytes: int) -> torch.Tensor:
+        ct = self._ct
+        p = ct.c_void_p()
+        rc = self._hip.hipHostMalloc(ct.byref(p), ct.c_size_t(nbytes), ct.c_uint(0))
+        if rc != 0 or not p.value:
+            raise MemoryError(f"hipHostMalloc({nbytes}) failed: {rc}")
+        self._ptrs.append(p.value)
+        return torch.frombuffer((ct.c_ubyte * nbytes).from_address(p.value), dtype=torch.uint8)
+
+    def pieces(self, nbytes: int) -> List[torch.Tensor]:
+        return [self.alloc(min(PIN_PIECE, nbytes - a)) for a in range(0, nbytes, PIN_PIECE)]
+
+    def free(self):
+        for p in self._ptrs:
+            self._hip.hipHostFree(self._ct.c_void_p(p))
+        self._ptrs = []
+
+
 class PeriodicCheckpointer:
     """Asynchronous periodic checkpoints with an atomically published ``latest`` (module doc).
 
@@ -374,10 +435,12 @@ class PeriodicCheckpointer:
             dist.broadcast_object_list(tok, src=0)
         self.token = tok[0]
         os.makedirs(root, exist_ok=True)
-        self._pinned: Dict[str, torch.Tensor] = {}
+        self._pinned: Dict[str, HostPieces] = {}
         self._stream = torch.cuda.Stream(device=self.device) if self.device.type == "cuda" else None
+        self._pin = PinnedPieces() if self._stream is not None else None
         # page-locking the host snapshot (112 GB at 8B on one rank) takes seconds: done once, on a
-        # side thread started now, so the first save() finds the buffers ready instead of stalling
+        # side thread started now (GIL-free, in pieces: PinnedPieces), so the first save() finds
+        # the buffers ready instead of stalling
         self._prep = None
         if self._stream is not None and self.flat and os.environ.get("KFAMD_CKPT_PREPIN", "1") != "0":
             shapes = {k: (tuple(v.shape), v.dtype) for k, v in _flat_state(trainer)[0].items()}
@@ -390,18 +453,28 @@ class PeriodicCheckpointer:
         self.last_seconds: Optional[float] = None
         self.snapshot_seconds: Optional[float] = None
 
+    def _host_buffer(self, shape, dtype) -> HostPieces:
+        n = 1
+        for d in shape:
+            n *= int(d)
+        return HostPieces(shape, dtype, self._pin.pieces(n * torch.empty((), dtype=dtype).element_size()))
+
     def _allocate_pinned(self, shapes):
         for k, (shape, dtype) in shapes.items():
-            self._pinned[k] = torch.empty(shape, dtype=dtype, pin_memory=True)
+            self._pinned[k] = self._host_buffer(shape, dtype)
 
     # -- snapshot (caller's thread)
-    def _host_copy(self, key: str, t: torch.Tensor) -> torch.Tensor:
+    def _host_copy(self, key: str, t: torch.Tensor):
         if self._stream is None:
             return t.detach().contiguous().clone()
         buf = self._pinned.get(key)
-        if buf is None or buf.shape != t.shape or buf.dtype != t.dtype:
-            buf = self._pinned[key] = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
-        buf.copy_(t.detach(), non_blocking=True)
+        if buf is None or buf.shape != tuple(t.shape) or buf.dtype != t.dtype:
+            buf = self._pinned[key] = self._host_buffer(tuple(t.shape), t.dtype)
+        src = t.detach().reshape(-1).view(torch.uint8)
+        a = 0
+        for piece in buf.pieces:
+            piece.copy_(src[a:a + piece.numel()], non_blocking=True)
+            a += piece.numel()
         return buf
 
     def save(self, step: int):
@@ -516,3 +589,11 @@ class PeriodicCheckpointer:
 
     def close(self):
         self.wait()
+        if self._prep is not None:
+            self._prep.join()
+            self._prep = None
+        if self._pin is not None:
+            if self._stream is not None:
+                self._stream.synchronize()
+            self._pinned = {}
+            self._pin.free()

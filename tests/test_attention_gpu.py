@@ -54,7 +54,7 @@ def test_flash_bwd(B, S, Hq, Hkv, causal):
     o, lse = torch.ops.kfamd.flash_fwd(qkv, B, S, Hq, Hkv, 128, sc, causal)
     g = torch.Generator(device="cpu").manual_seed(11)
     do = torch.randn(o.shape, generator=g).to(DEV, torch.bfloat16)
-    dqkv = torch.ops.kfamd.flash_bwd(qkv, o, lse, do, B, S, Hq, Hkv, 128, sc, causal)
+    dqkv = torch.ops.kfamd.flash_bwd(qkv, o, lse, do, B, S, Hq, Hkv, 128, sc, causal, False)
     x = qkv.float().detach().requires_grad_(True)
     q, k, v = _split(x, B, S, Hq, Hkv, 128)
     o_ref, _ = reference.attention(q, k, v, causal)
@@ -67,6 +67,27 @@ def test_flash_bwd(B, S, Hq, Hkv, causal):
         assert rel < 3e-2, (name, rel)
 
 
+@pytest.mark.parametrize("causal", [True, False])
+def test_flash_bwd_deterministic_mode_is_bitwise_and_matches_the_atomic_mode(causal):
+    """KFAMD_DETERMINISTIC / flash_bwd(..., deterministic=True): at S = 4096 every key block's
+    dK/dV gets 2-3 query chunks (QCH 1536), whose fp32 atomic sums vary in their last bits run to
+    run.  The deterministic mode stores each chunk's partial in its own slot and the post pass sums
+    them in item order: repeated calls are bitwise equal, and equal to the atomic mode within fp32
+    rounding (bf16 output)."""
+    B, S, Hq, Hkv = 1, 4096, 8, 2
+    sc = 1 / math.sqrt(128)
+    qkv = _qkv(B, S, Hq, Hkv, seed=33)
+    o, lse = torch.ops.kfamd.flash_fwd(qkv, B, S, Hq, Hkv, 128, sc, causal)
+    do = torch.randn(o.shape, generator=torch.Generator(device="cpu").manual_seed(9)).to(DEV, torch.bfloat16)
+    det = [torch.ops.kfamd.flash_bwd(qkv, o, lse, do, B, S, Hq, Hkv, 128, sc, causal, True) for _ in range(4)]
+    for x in det[1:]:
+        assert torch.equal(x, det[0])
+    ato = torch.ops.kfamd.flash_bwd(qkv, o, lse, do, B, S, Hq, Hkv, 128, sc, causal, False)
+    assert torch.equal(det[0][:, :Hq * 128], ato[:, :Hq * 128])             # dQ: the same kernel
+    err = ((det[0].float() - ato.float()).abs().max() / ato.float().abs().max()).item()
+    assert err < 1e-2, err
+
+
 def test_flash_bwd_stream_fork_ordering():
     """The backward forks its dK/dV chain (accumulator memset -> dK/dV) onto a side stream and
     joins before the fp32->bf16 post-pass.  Back-to-back calls on a NON-default stream, with the
@@ -77,12 +98,12 @@ def test_flash_bwd_stream_fork_ordering():
     qkv = _qkv(B, S, Hq, Hkv, seed=21)
     o, lse = torch.ops.kfamd.flash_fwd(qkv, B, S, Hq, Hkv, 128, sc, True)
     do = torch.randn(o.shape, generator=torch.Generator(device="cpu").manual_seed(5)).to(DEV, torch.bfloat16)
-    base = torch.ops.kfamd.flash_bwd(qkv, o, lse, do, B, S, Hq, Hkv, 128, sc, True)
+    base = torch.ops.kfamd.flash_bwd(qkv, o, lse, do, B, S, Hq, Hkv, 128, sc, True, False)
     torch.cuda.synchronize()
     s = torch.cuda.Stream(device=DEV)
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
-        outs = [torch.ops.kfamd.flash_bwd(qkv, o, lse, do, B, S, Hq, Hkv, 128, sc, True) for _ in range(4)]
+        outs = [torch.ops.kfamd.flash_bwd(qkv, o, lse, do, B, S, Hq, Hkv, 128, sc, True, False) for _ in range(4)]
         outs = [x.float().clone() for x in outs]
     torch.cuda.synchronize()
     ref = base.float()
@@ -105,7 +126,7 @@ def test_flash_fwd_bwd_at_bench_shape(B, b, g):
     qkv = _qkv(B, S, Hq, Hkv, seed=99)
     o, lse = torch.ops.kfamd.flash_fwd(qkv, B, S, Hq, Hkv, D, sc, True)
     do = torch.randn(o.shape, generator=torch.Generator(device="cpu").manual_seed(13)).to(DEV, torch.bfloat16)
-    dqkv = torch.ops.kfamd.flash_bwd(qkv, o, lse, do, B, S, Hq, Hkv, D, sc, True)
+    dqkv = torch.ops.kfamd.flash_bwd(qkv, o, lse, do, B, S, Hq, Hkv, D, sc, True, False)
     torch.cuda.synchronize()
     rows = slice(b * S, (b + 1) * S)
     heads = range(g * G, (g + 1) * G)
@@ -144,7 +165,7 @@ def test_flash_long_context_32k():
     qkv = _qkv(B, S, Hq, Hkv, seed=5)
     o, lse = torch.ops.kfamd.flash_fwd(qkv, B, S, Hq, Hkv, D, sc, True)
     do = torch.randn(o.shape, generator=torch.Generator(device="cpu").manual_seed(21)).to(DEV, torch.bfloat16)
-    dqkv = torch.ops.kfamd.flash_bwd(qkv, o, lse, do, B, S, Hq, Hkv, D, sc, True)
+    dqkv = torch.ops.kfamd.flash_bwd(qkv, o, lse, do, B, S, Hq, Hkv, D, sc, True, False)
     torch.cuda.synchronize()
     h, g = 5, 5 // G
     k = qkv[:, (Hq + g) * D:(Hq + g + 1) * D].float()

@@ -154,6 +154,21 @@ def test_streaming_safetensors_writer_round_trips_through_the_safe_loader(tmp_pa
     assert not os.path.exists(p + ".tmp")
 
 
+def test_streaming_writer_takes_a_tensor_as_page_locked_pieces(tmp_path):
+    """A snapshot held as byte pieces (checkpoint.HostPieces: the GPU path's page-locked buffers)
+    is written as the one tensor it came from."""
+    from safetensors.torch import load_file
+
+    from service_account_auth_improvements_amd.runtime.checkpoint import HostPieces, write_safetensors
+    x = torch.randn(1000, 3).to(torch.bfloat16)
+    raw = x.reshape(-1).view(torch.uint8)
+    pieces = [raw[a:a + 777].clone() for a in range(0, raw.numel(), 777)]
+    p = str(tmp_path / "p.safetensors")
+    write_safetensors(p, {"x": HostPieces(x.shape, x.dtype, pieces), "y": torch.arange(3)})
+    back = load_file(p)
+    assert torch.equal(back["x"], x) and torch.equal(back["y"], torch.arange(3))
+
+
 # ------------------------------------------------------------------ periodic checkpoint-restart
 
 def _events(path):

@@ -9,5 +9,5 @@ qkv=torch.randn(B*S,(Hq+2*Hkv)*D,device="cuda",dtype=torch.bfloat16)
 o,lse=torch.ops.kfamd.flash_fwd(qkv,B,S,Hq,Hkv,D,1/math.sqrt(D),True)
 do=torch.randn_like(o)
 for _ in range(3):
-    torch.ops.kfamd.flash_bwd(qkv,o,lse,do,B,S,Hq,Hkv,D,1/math.sqrt(D),True)
+    torch.ops.kfamd.flash_bwd(qkv,o,lse,do,B,S,Hq,Hkv,D,1/math.sqrt(D),True,False)
 torch.cuda.synchronize()
