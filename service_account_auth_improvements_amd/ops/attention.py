@@ -38,10 +38,13 @@ def attention_fwd(qkv, B, S, Hq, Hkv, D, causal=True):
 
 
 def deterministic_default() -> bool:
-    """``KFAMD_DETERMINISTIC=1``: bitwise run-to-run reproducible attention backward (dK/dV partial
-    sums in a fixed order instead of fp32 atomics; +~0.1 ms per Llama-3-8B layer at S 8192 for the
-    larger post pass), e.g. for bit-identical checkpoint-restart at long sequences."""
-    return os.environ.get("KFAMD_DETERMINISTIC", "0") == "1"
+    """The attention backward is bitwise run-to-run reproducible by default: each dK/dV work item
+    stores its partial sums in its own slot and the post pass adds a key block's slots in a fixed
+    order, instead of fp32 atomics whose order varies once a key block has several query chunks
+    (S > 1536).  Same box, B4 S8192: backward 7.130 vs 7.065-7.098 ms, ~1-2 ms per training step
+    (profiles/restart_gpu_r6.md); it is what makes a restarted GPU job's losses equal an
+    uninterrupted run's bit for bit.  ``KFAMD_DETERMINISTIC=0`` selects the atomic form."""
+    return os.environ.get("KFAMD_DETERMINISTIC", "1") != "0"
 
 
 def attention_bwd(qkv, o, lse, do, B, S, Hq, Hkv, D, causal=True, deterministic=None):
