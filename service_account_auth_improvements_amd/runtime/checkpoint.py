@@ -267,19 +267,114 @@ def save_checkpoint(path: str, trainer, extra: Optional[dict] = None, data=None)
 def _opt_sources(path: str, st) -> List[Tuple[str, str, int, int, str]]:
     """Every optimizer range stored for this (tp, pp) shard by ANY dp rank of the saving world:
     (file, group, lo, hi, key prefix)."""
-    from safetensors import safe_open
     out = []
     pre = f"tp{st.tp_rank}-pp{st.pp_rank}-dp"
     for fn in sorted(os.listdir(path)):
         if not (fn.startswith(pre) and fn.endswith(".safetensors")):
             continue
         f = os.path.join(path, fn)
-        with safe_open(f, framework="pt", device="cpu") as h:
-            for k in h.keys():
+        fi = _FileIndex(f)
+        try:
+            for k in fi.keys():
                 m = _OPT_KEY.match(k)
                 if m and m.group(4) == "master":
                     out.append((f, m.group(1), int(m.group(2)), int(m.group(3)), k[:-len("/master")]))
+        finally:
+            fi.close()
     return out
+
+
+class _FileIndex:
+    """Byte spans of the tensors in a safetensors file (its JSON header, parsed directly) and a
+    read-only descriptor for positional reads.  Nothing in the file is executed or unpickled."""
+
+    def __init__(self, path: str):
+        with open(path, "rb") as f:
+            (n,) = struct.unpack("<Q", f.read(8))
+            hdr = json.loads(f.read(n))
+        self.path, self.base = path, 8 + n
+        self.meta = {k: v for k, v in hdr.items() if k != "__metadata__"}
+        self.fd = os.open(path, os.O_RDONLY)
+
+    def keys(self):
+        return self.meta.keys()
+
+    def span(self, key: str):
+        m = self.meta[key]
+        a, b = m["data_offsets"]
+        return m["dtype"], tuple(m["shape"]), self.base + a, b - a
+
+    def close(self):
+        os.close(self.fd)
+
+
+class _Loader:
+    """Checkpoint reader for resume: byte ranges of the files are read with positional reads on
+    8 threads (the syscalls release the GIL) into two page-locked 128 MB staging buffers, each
+    copied to the GPU on a side stream while the next one is read, so disk/page-cache reads and
+    host-to-device copies overlap.  CPU destinations are read into directly."""
+
+    CHUNK = 128 << 20
+
+    def __init__(self, device):
+        from concurrent.futures import ThreadPoolExecutor
+        self.cuda = device.type == "cuda"
+        self.pool = ThreadPoolExecutor(8, thread_name_prefix="kfamd-ckpt-read")
+        self.k = 0
+        if self.cuda:
+            self.pin = PinnedPieces()
+            self.bufs = [self.pin.alloc(self.CHUNK) for _ in range(2)]
+            self.events = [None, None]
+            self.stream = torch.cuda.Stream(device=device)
+            self.stream.wait_stream(torch.cuda.current_stream(device))   # e.g. zero-fills queued before
+
+    @staticmethod
+    def _pread_part(fd: int, off: int, mv):
+        got = 0
+        while got < len(mv):
+            r = os.preadv(fd, [mv[got:]], off + got)
+            if r <= 0:
+                raise IOError(f"short read at byte {off + got}")
+            got += r
+
+    def _pread(self, fd: int, off: int, mv):
+        n = len(mv)
+        step = max(4 << 20, -(-n // 8))
+        for fut in [self.pool.submit(self._pread_part, fd, off + a, mv[a:a + step]) for a in range(0, n, step)]:
+            fut.result()
+
+    def load(self, fi: _FileIndex, key: str, elem_lo: int, dst: torch.Tensor):
+        """Fill contiguous ``dst`` with elements [elem_lo, elem_lo + dst.numel()) of ``key``."""
+        dtype, _, start, nbytes = fi.span(key)
+        if _ST_DTYPE[dst.dtype] != dtype:
+            raise TypeError(f"{fi.path}:{key} is {dtype}, the destination {dst.dtype}")
+        bdst = dst.reshape(-1).view(torch.uint8)
+        off = start + elem_lo * dst.element_size()
+        if off + bdst.numel() > start + nbytes:
+            raise ValueError(f"{fi.path}:{key}: range past the tensor")
+        if not self.cuda:
+            self._pread(fi.fd, off, memoryview(bdst.numpy()))
+            return
+        for a in range(0, bdst.numel(), self.CHUNK):
+            i = self.k % 2
+            self.k += 1
+            if self.events[i] is not None:
+                self.events[i].synchronize()          # the copy out of this buffer has finished
+            m = min(self.CHUNK, bdst.numel() - a)
+            buf = self.bufs[i][:m]
+            self._pread(fi.fd, off + a, memoryview(buf.numpy()))
+            with torch.cuda.stream(self.stream):
+                bdst[a:a + m].copy_(buf, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+            self.events[i] = ev
+
+    def close(self):
+        if self.cuda:
+            self.stream.synchronize()
+            self.bufs = []
+            self.pin.free()
+        self.pool.shutdown()
 
 
 def load_checkpoint(path: str, trainer, data=None) -> dict:
@@ -287,8 +382,8 @@ def load_checkpoint(path: str, trainer, data=None) -> dict:
     this rank are filled by flat-range overlap with whatever ranges the saving world stored, so
     a checkpoint written at one data-parallel size (or with / without ZeRO-1) resumes at another:
     ZeRO-1 state is re-sharded, elements past the saved (padded) length are zero.  A different
-    TP or PP layout cannot be re-sharded this way and is refused."""
-    from safetensors import safe_open
+    TP or PP layout cannot be re-sharded this way and is refused.  Reads go through
+    :class:`_Loader` (parallel positional reads overlapped with host-to-device copies)."""
     if not hasattr(trainer, "model") or not hasattr(trainer.model, "groups"):
         return load_module_checkpoint(path, trainer, data)
     st = trainer.st
@@ -300,35 +395,42 @@ def load_checkpoint(path: str, trainer, data=None) -> dict:
                          "TP/PP re-sharding is not supported -- resume with the saving layout")
     dev = trainer.model.groups[0].params.device
     pfile = os.path.join(path, f"tp{st.tp_rank}-pp{st.pp_rank}-dp0.safetensors")
-    with safe_open(pfile, framework="pt", device="cpu") as h:
-        for g in trainer.model.groups:
-            src = h.get_slice(f"param/{g.name}")
-            n = min(src.get_shape()[0], g.numel)
-            g.params[:n].copy_(src[:n].to(dev))
-            if n < g.numel:
-                g.params[n:].zero_()
     sources = _opt_sources(path, st)
-    handles = {}
+    # zero what the checkpoint does not cover (padding past the saved length) before the loader's
+    # stream starts writing the rest
+    pidx = _FileIndex(pfile)
+    plen = {}
+    for g in trainer.model.groups:
+        n = min(pidx.span(f"param/{g.name}")[1][0], g.numel)
+        plen[g.name] = n
+        if n < g.numel:
+            g.params[n:].zero_()
+    for sh in trainer.opt.shards:
+        for buf in (sh.master, sh.m, sh.v):
+            buf.zero_()
+    files = {pfile: pidx}
+    ld = _Loader(dev)
     try:
+        for g in trainer.model.groups:
+            ld.load(pidx, f"param/{g.name}", 0, g.params[:plen[g.name]])
         for sh in trainer.opt.shards:
             filled = 0
-            for buf in (sh.master, sh.m, sh.v):
-                buf.zero_()
             for f, gname, lo, hi, pre in sources:
                 if gname != sh.group.name or hi <= sh.lo or lo >= sh.hi:
                     continue
                 a, b = max(lo, sh.lo), min(hi, sh.hi)
-                h = handles.get(f) or handles.setdefault(f, safe_open(f, framework="pt", device="cpu"))
+                fi = files.get(f) or files.setdefault(f, _FileIndex(f))
                 for suf, buf in (("master", sh.master), ("m", sh.m), ("v", sh.v)):
-                    buf[a - sh.lo:b - sh.lo].copy_(h.get_slice(f"{pre}/{suf}")[a - lo:b - lo].to(dev))
+                    ld.load(fi, f"{pre}/{suf}", a - lo, buf[a - sh.lo:b - sh.lo])
                 filled += b - a
             saved_len = max((hi for _, gname, _, hi, _ in sources if gname == sh.group.name), default=0)
             need = min(sh.hi, saved_len) - min(sh.lo, saved_len)
             if filled < need:
                 raise KeyError(f"optimizer range {sh.group.name}[{sh.lo}, {sh.hi}) is not covered by {path}")
     finally:
-        for h in handles.values():
-            h.__exit__(None, None, None)
+        ld.close()
+        for fi in files.values():
+            fi.close()
     trainer.opt.step_count = int(meta["step"])
     if hasattr(trainer, "step_idx"):
         trainer.step_idx = int(meta["step"])
