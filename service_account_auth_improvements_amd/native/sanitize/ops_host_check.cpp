@@ -230,17 +230,19 @@ void check_gpu() {
     auto oref = attn_ref(q, k, v, scale);
     expect_close("flash_fwd o", o, oref.permute({0, 2, 1, 3}).reshape({B * S, Hq * D}), 2e-2, 2e-2);
     auto dout = at::randn({B * S, Hq * D}, bf);
-    auto dqkv = call("kfamd::flash_bwd", {qkv, o, lse, dout, B, S, Hq, Hkv, D, scale, true})[0].toTensor();
+    auto dqkv = call("kfamd::flash_bwd", {qkv, o, lse, dout, B, S, Hq, Hkv, D, scale, true, true})[0].toTensor();
+    auto dqkv_atomic = call("kfamd::flash_bwd", {qkv, o, lse, dout, B, S, Hq, Hkv, D, scale, true, false})[0].toTensor();
     oref.backward(dout.to(at::kFloat).reshape({B, S, Hq, D}).permute({0, 2, 1, 3}));
     auto back = [&](const at::Tensor& gr, int64_t H) { return gr.permute({0, 2, 1, 3}).reshape({B * S, H * D}); };
     expect_close("flash_bwd dq", dqkv.narrow(1, 0, Hq * D), back(q.grad(), Hq), 5e-2, 5e-2);
     expect_close("flash_bwd dk", dqkv.narrow(1, Hq * D, Hkv * D), back(k.grad(), Hkv), 5e-2, 5e-2);
     expect_close("flash_bwd dv", dqkv.narrow(1, (Hq + Hkv) * D, Hkv * D), back(v.grad(), Hkv), 5e-2, 5e-2);
+    expect_close("flash_bwd atomic vs deterministic", dqkv_atomic, dqkv, 2e-2, 2e-2);
     expect_reject("flash_fwd head dim 64", "kfamd::flash_fwd", {qkv, B, S, Hq, Hkv, (int64_t)64, scale, true});
     expect_reject("flash_fwd S % 128", "kfamd::flash_fwd",
                   {at::randn({B * 200, (Hq + 2 * Hkv) * D}, bf), B, (int64_t)200, Hq, Hkv, D, scale, true});
     expect_reject("flash_bwd lse size", "kfamd::flash_bwd",
-                  {qkv, o, lse.narrow(2, 0, 128).contiguous(), dout, B, S, Hq, Hkv, D, scale, true});
+                  {qkv, o, lse.narrow(2, 0, 128).contiguous(), dout, B, S, Hq, Hkv, D, scale, true, true});
   }
   // embedding fwd / bwd (sorted scatter-add), one vocab shard starting at 100
   {
