@@ -254,7 +254,55 @@ def _full_opt_state(path):
     return out
 
 
-def test_zero1_state_is_resharded_when_the_data_parallel_size_changes(tmp_path):
+def test_periodic_saves_spread_the_optimizer_over_part_files_and_ignore_stale_ones(tmp_path, monkeypatch):
+    """With small parts (KFAMD_CKPT_PART_MIN) a rank's optimizer state is cut into several part
+    files written concurrently; the done marker lists them, and a part file of a killed earlier
+    world left in the same step directory is never read on resume."""
+    from service_account_auth_improvements_amd.runtime import checkpoint as ckm
+    monkeypatch.setenv("KFAMD_CKPT_PART_MIN", "4096")
+    base = ["--model", "tiny", "--device", "cpu", "--seq-len", "32", "--micro-batch", "2"]
+    full = _run_entry(tmp_path, "full", base + ["--steps", "6"])
+    ck = str(tmp_path / "ck")
+    _run_entry(tmp_path, "p1", base + ["--steps", "4", "--ckpt-dir", ck, "--save-every", "3"])
+    d = ckm.latest_checkpoint(ck)
+    parts = sorted(f for f in os.listdir(d) if f.startswith("tp0-pp0-dp0"))
+    assert len(parts) == ckm._writers() and "tp0-pp0-dp0.safetensors" in parts, parts
+    with open(os.path.join(d, "rank0.done")) as f:
+        assert sorted(json.load(f)["files"]) == parts
+    # the main file keeps the parameters whole; every optimizer range is in exactly one part
+    fi = ckm._FileIndex(os.path.join(d, "tp0-pp0-dp0.safetensors"))
+    assert all(k.startswith("param/") for k in fi.keys())
+    fi.close()
+    srcs = ckm._opt_sources(d, type("St", (), {"tp_rank": 0, "pp_rank": 0})())
+    assert len({s[0] for s in srcs}) == len(parts) - 1
+    # a stale part of another world: the same ranges, garbage values
+    stale = {}
+    for f, g, lo, hi, pre in srcs:
+        for suf in ("master", "m", "v"):
+            stale[f"{pre}/{suf}"] = torch.full((hi - lo,), 1e9)
+    ckm.write_safetensors(os.path.join(d, "tp0-pp0-dp0.part99.safetensors"), stale)
+    p2 = _run_entry(tmp_path, "p2", base + ["--steps", "6", "--ckpt-dir", ck, "--save-every", "3"])
+    steps = lambda ev: [(e["step"], e["loss"]) for e in ev if e["event"] == "step"]   # noqa: E731
+    assert steps(p2) == steps(full)[3:]
+
+
+def test_opt_parts_cut_the_ranges_into_equal_runs():
+    from service_account_auth_improvements_amd.runtime.checkpoint import _opt_parts
+
+    class Sh:
+        def __init__(self, lo, hi):
+            self.lo, self.hi = lo, hi
+    shards = [Sh(0, 10), Sh(100, 100), Sh(40, 71)]
+    out = _opt_parts(shards, 4, 1)
+    assert [(a, b, j) for _, a, b, j in out] == [(0, 10, 1), (100, 100, 1), (40, 41, 1), (41, 52, 2), (52, 63, 3),
+                                                 (63, 71, 4)]
+    assert [(a, b, j) for _, a, b, j in _opt_parts(shards, 1, 0)] == [(0, 10, 0), (100, 100, 0), (40, 71, 0)]
+
+
+@pytest.mark.parametrize("part_min", [None, "2048"])
+def test_zero1_state_is_resharded_when_the_data_parallel_size_changes(tmp_path, monkeypatch, part_min):
+    if part_min:
+        monkeypatch.setenv("KFAMD_CKPT_PART_MIN", part_min)
     assert run_ranks(_reshard_body, world=2, args=(str(tmp_path), "save")) == [0, 0]
     for w in (1, 3):
         assert run_ranks(_reshard_body, world=w, args=(str(tmp_path), "load")) == [0] * w
