@@ -34,6 +34,18 @@ def rmsnorm_fwd(a, w, eps, residual=None):
     return y, h, rstd
 
 
+def rmsnorm_fwd_parts(a, part, w, eps):
+    """rmsnorm_fwd(a, residual=bf16(part.sum(0))) for ``part`` the fp32 K-split partials
+    [S, rows, H] of :func:`bgemm_parts`: the batched-decode GEMM's reduce launch folded into the
+    norm (ops/csrc/rmsnorm.hip).  Returns (y, h, rstd); h is bitwise the unfused path's."""
+    if a.is_cuda:
+        return _k().rmsnorm_fwd_parts(a, part, w, eps)
+    d = part[0].clone()
+    for t in range(1, part.shape[0]):
+        d += part[t]
+    return reference.rmsnorm_fwd(a, d.to(a.dtype), w, eps)
+
+
 def rmsnorm_bwd(dy, h, rstd, w, dw_out, accumulate=False, dres=None):
     """Returns dh (+ dres); writes (or accumulates) dw into ``dw_out``."""
     if dy.is_cuda:
@@ -110,6 +122,15 @@ def bgemm(x, w, swiglu: bool = False, splits: int = 0):
         F_ = y.shape[1] // 2
         y = torch.nn.functional.silu(y[:, :F_]) * y[:, F_:]
     return y.to(x.dtype)
+
+
+def bgemm_parts(x, w):
+    """:func:`bgemm` with the K-split reduce left to the consumer: the fp32 partials [S, M, N]
+    when the automatic split is S > 1 (sum them with :func:`rmsnorm_fwd_parts`), else the bf16
+    [M, N] product."""
+    if x.is_cuda:
+        return _k().bgemm_parts(x, w)
+    return bgemm(x, w)
 
 
 def skinny_gemm_norm_ok(x, K: int) -> bool:

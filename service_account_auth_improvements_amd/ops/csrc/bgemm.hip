@@ -358,7 +358,9 @@ extern "C" int kf_bgemm_splits(int M, int N, int K) {
 
 // Y[M, N] = X[M, K] . W^T with W [N, K] (SwiGLU: W = [gate; up] with up rows at +up_off, Y
 // [M, up_off] = silu(X gate^T) * (X up^T)).  part: fp32 workspace of S * M * NP floats (NP = N,
-// or 2 * up_off for SwiGLU) when S > 1.  Returns 1 (nothing launched) outside the kernel's range.
+// or 2 * up_off for SwiGLU) when S > 1.  y = nullptr with S > 1 (not SwiGLU): only the partials
+// are written and the reduce launch is left to the consumer (kf_rmsnorm_fwd_parts sums them in
+// its prologue).  Returns 1 (nothing launched) outside the kernel's range.
 extern "C" int kf_bgemm(const void* x, long ldx, int M, const void* w, int N, int K, void* y, long ldy, int swiglu,
                         int up_off, int S, float* part, hipStream_t st) {
   if (M < 1 || M > 256 || K % BG_KQ || ldx % 8 || ldy % 4 || S < 1 || (K / BG_KQ) % S) return 1;
@@ -366,6 +368,7 @@ extern "C" int kf_bgemm(const void* x, long ldx, int M, const void* w, int N, in
   const int wt = kf_bgemm_wt(M, N, K);
   if (swiglu ? (up_off % (32 * wt) || N != 2 * up_off) : N % (BG_BN * wt)) return 1;
   if (S > 1 && !part) return 1;
+  if (!y && (S == 1 || swiglu)) return 1;
   const int NB = swiglu ? up_off / (32 * wt) : N / (BG_BN * wt), NP = swiglu ? 2 * up_off : N;
   const int kslice = K / S, grid = NB * S;
   auto X = (const bf16_t*)x;
@@ -391,7 +394,7 @@ extern "C" int kf_bgemm(const void* x, long ldx, int M, const void* w, int N, in
   }
 #undef BG_CASE
   KF_CHECK_LAUNCH();
-  if (S > 1) {
+  if (S > 1 && y) {
     const long threads = (long)M * (swiglu ? up_off : N) / 4;
     const int blocks = (int)((threads + 255) / 256);
     if (swiglu) hipLaunchKernelGGL(bgemm_reduce_kernel<true>, dim3(blocks), dim3(256), 0, st, part, S, M, NP, Y, ldy);

@@ -17,6 +17,8 @@
 #include <tuple>
 
 extern "C" {
+int kf_rmsnorm_fwd_parts(const void*, const float*, int, void*, void*, float*, const void*, int, int, float,
+                         hipStream_t);
 int kf_rmsnorm_fwd(const void*, const void*, void*, void*, float*, const void*, int, int, float,
                    hipStream_t);
 int kf_rmsnorm_bwd(const void*, const void*, const float*, const void*, const void*, void*, float*,
@@ -116,6 +118,27 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> rmsnorm_fwd(const at::Tensor& a,
   check_rc(kf_rmsnorm_fwd(a.data_ptr(), bp, hp, y.data_ptr(), rstd.data_ptr<float>(), w.data_ptr(),
                           (int)rows, (int)H, (float)eps, cur_stream()),
            "rmsnorm_fwd");
+  return {y, h, rstd};
+}
+
+// h = a + bf16(sum_s part[s]); y = rmsnorm(h) * w with part the fp32 K-split partials [S, rows, H]
+// of the batched-decode GEMM (bgemm_parts): the reduce launch folded into the norm
+std::tuple<at::Tensor, at::Tensor, at::Tensor> rmsnorm_fwd_parts(const at::Tensor& a, const at::Tensor& part,
+                                                                 const at::Tensor& w, double eps) {
+  check_bf16_cuda(a, "a");
+  check_bf16_cuda(w, "w");
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous() && part.dim() == 3,
+              "rmsnorm_fwd_parts: fp32 [S, rows, H] partials");
+  TORCH_CHECK(a.is_contiguous() && w.is_contiguous() && a.dim() == 2, "rmsnorm_fwd_parts: contiguous [rows, H] input");
+  const int64_t rows = a.size(0), H = a.size(1);
+  TORCH_CHECK(part.size(1) == rows && part.size(2) == H && w.numel() == H, "rmsnorm_fwd_parts: shape mismatch");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(a.device());
+  auto y = at::empty_like(a);
+  auto h = at::empty_like(a);
+  auto rstd = at::empty({rows}, a.options().dtype(at::kFloat));
+  check_rc(kf_rmsnorm_fwd_parts(a.data_ptr(), part.data_ptr<float>(), (int)part.size(0), h.data_ptr(), y.data_ptr(),
+                                rstd.data_ptr<float>(), w.data_ptr(), (int)rows, (int)H, (float)eps, cur_stream()),
+           "rmsnorm_fwd_parts");
   return {y, h, rstd};
 }
 
@@ -530,6 +553,25 @@ at::Tensor bgemm(const at::Tensor& x, const at::Tensor& w, bool swiglu, int64_t 
   return y;
 }
 
+// bgemm whose K-split partials are left for the consumer: fp32 [S, M, N] when the automatic split
+// is S > 1 (no reduce launch; rmsnorm_fwd_parts sums them), else the bf16 [M, N] product
+at::Tensor bgemm_parts(const at::Tensor& x, const at::Tensor& w) {
+  check_bf16_cuda(x, "x");
+  check_bf16_cuda(w, "w");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && w.dim() == 2 && w.is_contiguous(), "bgemm_parts: 2-D operands");
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K, "bgemm_parts: K mismatch");
+  TORCH_CHECK(M >= 1 && M <= 256 && K % 256 == 0 && N % 64 == 0, "bgemm_parts: needs 1 <= M <= 256, K % 256 == 0, N % 64 == 0");
+  const int S = kf_bgemm_splits((int)M, (int)N, (int)K);
+  if (S == 1) return bgemm(x, w, false, 1);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  auto part = at::empty({(int64_t)S, M, N}, x.options().dtype(at::kFloat));
+  check_rc(kf_bgemm(x.data_ptr(), x.stride(0), (int)M, w.data_ptr(), (int)N, (int)K, nullptr, N, 0, (int)N, S,
+                    part.data_ptr<float>(), cur_stream()),
+           "bgemm_parts");
+  return part;
+}
+
 // Decode GEMM with the residual-add + RMSNorm fused in as a prologue:
 //   h = x (+ res);  y = (rmsnorm(h) * nw) . w^T  [SwiGLU epilogue when swiglu].
 // Returns (y, h); h aliases x when res is None.  Needs M <= 8 and M * K <= 32768.
@@ -748,6 +790,8 @@ void grad_accum_(at::Tensor main_, at::Tensor g, int64_t mode) {
 
 TORCH_LIBRARY(kfamd, m) {
   m.def("rmsnorm_fwd", &rmsnorm_fwd);
+  m.def("rmsnorm_fwd_parts", &rmsnorm_fwd_parts);
+  m.def("bgemm_parts", &bgemm_parts);
   m.def("rmsnorm_bwd", &rmsnorm_bwd);
   m.def("rope_", &rope_);
   m.def("swiglu_fwd", &swiglu_fwd);

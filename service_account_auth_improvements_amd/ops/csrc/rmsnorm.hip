@@ -183,6 +183,79 @@ __global__ __launch_bounds__(1024) void colsum_to_bf16_kernel(const float* __res
   }
 }
 
+// Decode: h = a + bf16(sum_s part[s]); y = rmsnorm(h) * w, where part [S, rows, H] holds the fp32
+// K-split partial sums of the batched-decode GEMM that produced the residual branch
+// (ops/csrc/bgemm.hip with its reduce launch skipped).  The partials are summed in slice order
+// and rounded to bf16 exactly as bgemm_reduce_kernel rounds them, so h is bitwise the unfused
+// path's h.  One 256-thread block per row: a decode step has only 33-256 rows, so the row's
+// CPT x S partial loads are spread over four waves and all issued before the first use.
+template <int CPT, int S>
+__global__ __launch_bounds__(256) void rmsnorm_fwd_parts_kernel(
+    const bf16_t* __restrict__ a, const float* __restrict__ part, bf16_t* __restrict__ h_out,
+    bf16_t* __restrict__ y, float* __restrict__ rstd, const bf16_t* __restrict__ w, int rows, int H, float eps) {
+  __shared__ float red[4];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int row = blockIdx.x;
+  if (row >= rows) return;
+  const int nv = H >> 3;
+  const size_t base = (size_t)row * H, pstride = (size_t)rows * H;
+  u32x4 av[CPT], wq[CPT];
+  f32x4 pv[CPT][S][2];
+#pragma unroll
+  for (int i = 0; i < CPT; ++i) {
+    const int v = min(i * 256 + tid, nv - 1);
+    av[i] = ld16(a + base + v * 8);
+    wq[i] = ld16(w + v * 8);
+#pragma unroll
+    for (int t = 0; t < S; ++t) {
+      pv[i][t][0] = ldf4(part + t * pstride + base + v * 8);
+      pv[i][t][1] = ldf4(part + t * pstride + base + v * 8 + 4);
+    }
+  }
+  u32x4 hq[CPT];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < CPT; ++i) {
+    const int v = i * 256 + tid;
+    f32x4 d0 = f32x4{0.f, 0.f, 0.f, 0.f}, d1 = d0;
+#pragma unroll
+    for (int t = 0; t < S; ++t) {
+      d0 += pv[i][t][0];
+      d1 += pv[i][t][1];
+    }
+    float x[8], dr[8];
+    unpack8(u32x4{pack2(d0[0], d0[1]), pack2(d0[2], d0[3]), pack2(d1[0], d1[1]), pack2(d1[2], d1[3])}, dr);
+    unpack8(av[i], x);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] += dr[j];
+    hq[i] = pack8(x);
+    if (v < nv) st16(h_out + base + v * 8, hq[i]);
+    unpack8(hq[i], x);
+    float sq = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sq += x[j] * x[j];
+    ss += v < nv ? sq : 0.f;
+  }
+  ss = wave_sum(ss);
+  if (lane == 0) red[wv] = ss;
+  __syncthreads();
+  ss = red[0] + red[1] + red[2] + red[3];
+  const float r = rsqrtf(ss / (float)H + eps);
+  if (tid == 0) rstd[row] = r;
+#pragma unroll
+  for (int i = 0; i < CPT; ++i) {
+    const int v = i * 256 + tid;
+    if (v < nv) {
+      float x[8], wf[8], o[8];
+      unpack8(hq[i], x);
+      unpack8(wq[i], wf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = x[j] * r * wf[j];
+      st16(y + base + v * 8, pack8(o));
+    }
+  }
+}
+
 #define DISPATCH_VPT(nv, ...)                 \
   do {                                        \
     int _v = ((nv) + 63) / 64;                \
@@ -223,6 +296,23 @@ int kf_rmsnorm_bwd(const void* dy, const void* h, const float* rstd, const void*
                                                  (const bf16_t*)dres, (bf16_t*)dh, dw_part, rows, H);
   }
   colsum_to_bf16_kernel<<<cdiv(H, 64), 1024, 0, s>>>(dw_part, nblocks, H, (bf16_t*)dw_out, accumulate);
+  return 0;
+}
+
+// part: fp32 [S, rows, H] (S = 2, 4 or 8; H a multiple of 8, at most 4096 -- two chunks per thread)
+int kf_rmsnorm_fwd_parts(const void* a, const float* part, int S, void* h_out, void* y, float* rstd, const void* w,
+                         int rows, int H, float eps, hipStream_t s) {
+  if (H % 8 != 0 || H > 4096 || rows < 1) return 1;
+  const int cpt = (H / 8 + 255) / 256;
+#define RN_PARTS(C, SV)                                                                                       \
+  rmsnorm_fwd_parts_kernel<C, SV><<<rows, 256, 0, s>>>((const bf16_t*)a, part, (bf16_t*)h_out, (bf16_t*)y, rstd, \
+                                                       (const bf16_t*)w, rows, H, eps)
+  if (cpt == 1) {
+    if (S == 2) RN_PARTS(1, 2); else if (S == 4) RN_PARTS(1, 4); else if (S == 8) RN_PARTS(1, 8); else return 1;
+  } else {
+    if (S == 2) RN_PARTS(2, 2); else if (S == 4) RN_PARTS(2, 4); else if (S == 8) RN_PARTS(2, 8); else return 1;
+  }
+#undef RN_PARTS
   return 0;
 }
 

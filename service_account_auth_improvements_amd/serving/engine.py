@@ -54,6 +54,10 @@ GEMV_MAX_ROWS = 4             # ... but not than the VALU GEMV (ops/csrc/gemv.hi
 BGEMM = os.environ.get("KFAMD_BGEMM", "1") != "0"
 BGEMM_MAX_N = 4096
 BGEMM_MIN_ROWS, BGEMM_MAX_ROWS = 33, 128   # at 32 rows its reduce launch costs more than it saves
+# the K-split partials of the wo / wd batched-decode GEMMs go straight into the RMSNorm that
+# consumes the residual branch (ops.rmsnorm_fwd_parts), without the separate reduce launch;
+# KFAMD_DECODE_FUSE_SPLITS=0: reduce launch + plain RMSNorm (A/Bs)
+FUSE_SPLITS = os.environ.get("KFAMD_DECODE_FUSE_SPLITS", "1") != "0"
 # prompts admitted in one scheduler iteration are prefilled together up to this many tokens
 PREFILL_MAX_TOKENS = int(os.environ.get("KFAMD_PREFILL_MAX_TOKENS", "16384"))
 PREFILL_PAD_RATIO = 1.25      # ... in length groups padded to at most 1.25x
@@ -81,6 +85,25 @@ def _load_tuned_decode_gemms(dev, cfg, tp: int) -> bool:
     tn.tuning_enable(False)           # never tune inside a serving process
     tn.read_file(path)
     return True
+
+
+class _SplitSum:
+    """A decode projection's output left as the batched-decode GEMM's fp32 K-split partials
+    [S, M, N]; the RMSNorm that adds it to the residual stream sums them (:meth:`Engine._norm`)."""
+    __slots__ = ("part",)
+
+    def __init__(self, part):
+        self.part = part
+
+    def dense(self):
+        d = self.part[0].clone()
+        for t in range(1, self.part.shape[0]):
+            d += self.part[t]
+        return d.to(torch.bfloat16)
+
+
+def _dense(d):
+    return d.dense() if isinstance(d, _SplitSum) else d
 
 
 class Engine:
@@ -220,21 +243,35 @@ class Engine:
             return ops.bgemm(x, w)
         return torch.mm(x, w.t())
 
+    def _mm_res(self, x, w):
+        """A projection whose output only feeds the next residual add + RMSNorm: with the
+        batched-decode GEMM at a K split, its fp32 partials (:class:`_SplitSum`), no reduce launch."""
+        if FUSE_SPLITS and x.is_cuda and self._use_bgemm(x, w):
+            y = ops.bgemm_parts(x, w)
+            return _SplitSum(y) if y.dim() == 3 else y
+        return self._tp_ar(self._mm(x, w))
+
+    def _norm(self, x, w, d):
+        """Residual add + RMSNorm; ``d`` may be a projection's unreduced partials."""
+        if isinstance(d, _SplitSum):
+            return ops.rmsnorm_fwd_parts(x, d.part, w, self.cfg.norm_eps)
+        return ops.rmsnorm_fwd(x, w, self.cfg.norm_eps, residual=d)
+
     def _decode_mlp(self, i, h1, da):
         m, cfg = self.m, self.cfg
         wgu = m.P(f"l{i}.wgu")
         if ops.skinny_gemm_norm_ok(h1, wgu.shape[1]):
             # residual add + RMSNorm + gate/up GEMM + SwiGLU: one kernel
-            s, h2 = ops.skinny_gemm_norm(h1, da, m.P(f"l{i}.norm2"), cfg.norm_eps, wgu, swiglu=True)
-            return h2, self._tp_ar(self._mm(s, m.P(f"l{i}.wd")))
-        mm, h2, _ = ops.rmsnorm_fwd(h1, m.P(f"l{i}.norm2"), cfg.norm_eps, residual=da)
+            s, h2 = ops.skinny_gemm_norm(h1, _dense(da), m.P(f"l{i}.norm2"), cfg.norm_eps, wgu, swiglu=True)
+            return h2, self._mm_res(s, m.P(f"l{i}.wd"))
+        mm, h2, _ = self._norm(h1, m.P(f"l{i}.norm2"), da)
         if mm.is_cuda and (mm.shape[0] <= GEMV_MAX_ROWS or (mm.shape[0] <= SKINNY_MAX_ROWS and wgu.shape[1] % 256 == 0)):
             s = ops.skinny_gemm(mm, wgu, swiglu=True)          # gate/up GEMM + SwiGLU in one kernel
         elif mm.is_cuda and self._use_bgemm(mm, wgu):
             s = ops.bgemm(mm, wgu, swiglu=True)
         else:
             s = ops.swiglu_fwd(torch.mm(mm, wgu.t()))
-        return h2, self._tp_ar(self._mm(s, m.P(f"l{i}.wd")))
+        return h2, self._mm_res(s, m.P(f"l{i}.wd"))
 
     def _decode_body(self, tokens, slots, pos, lengths):
         m, cfg = self.m, self.cfg
@@ -244,19 +281,19 @@ class Engine:
             wqkv = m.P(f"l{i}.wqkv")
             if ops.gemv_norm_rope_ok(r, wqkv.shape[1], cfg.head_dim):
                 # residual add + RMSNorm + qkv GEMV + RoPE + KV-cache append: one kernel
-                qkv, h1 = ops.gemv_norm_rope(r, d, m.P(f"l{i}.norm1"), cfg.norm_eps, wqkv, m.hq, m.cos, m.sin,
-                                             slots, pos, self.kc[li], self.vc[li])
+                qkv, h1 = ops.gemv_norm_rope(r, _dense(d), m.P(f"l{i}.norm1"), cfg.norm_eps, wqkv, m.hq, m.cos,
+                                             m.sin, slots, pos, self.kc[li], self.vc[li])
             else:
                 if ops.skinny_gemm_norm_ok(r, wqkv.shape[1]):
-                    qkv, h1 = ops.skinny_gemm_norm(r, d, m.P(f"l{i}.norm1"), cfg.norm_eps, wqkv)
+                    qkv, h1 = ops.skinny_gemm_norm(r, _dense(d), m.P(f"l{i}.norm1"), cfg.norm_eps, wqkv)
                 else:
-                    a, h1, _ = ops.rmsnorm_fwd(r, m.P(f"l{i}.norm1"), cfg.norm_eps, residual=d)
+                    a, h1, _ = self._norm(r, m.P(f"l{i}.norm1"), d)
                     qkv = self._mm(a, wqkv)
                 rope_append_(qkv, m.hq, m.cos, m.sin, slots, pos, self.kc[li], self.vc[li])
             o = decode_attention(qkv, self.kc[li], self.vc[li], slots, lengths, m.hq)
-            da = self._tp_ar(self._mm(o, m.P(f"l{i}.wo")))
+            da = self._mm_res(o, m.P(f"l{i}.wo"))
             r, d = self._decode_mlp(i, h1, da)
-        y, _, _ = ops.rmsnorm_fwd(r, m.P("final_norm"), cfg.norm_eps, residual=d)
+        y, _, _ = self._norm(r, m.P("final_norm"), d)
         return self._logits_full(y)
 
     def _graph_for(self, Bb: int):

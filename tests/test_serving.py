@@ -257,3 +257,19 @@ def test_tp_predictor_leader_drives_followers():
         exp.append(ref.decode([t], [0], [37 + j])[0])
     assert (logits - torch.stack([x.float() for x in exp])).abs().max().item() < 5e-2
     assert all(len(o) == 4 for o in outs)
+
+
+def test_split_partials_norm_reference_equals_reduce_then_norm():
+    """CPU reference of ops.rmsnorm_fwd_parts (the decode engine's reduce-in-norm path): the
+    partials summed in slice order and rounded to bf16, then the plain residual RMSNorm."""
+    from service_account_auth_improvements_amd import ops
+    from service_account_auth_improvements_amd.serving.engine import _SplitSum, _dense
+    g = torch.Generator().manual_seed(3)
+    a = torch.randn(5, 64, generator=g).bfloat16()
+    part = torch.randn(4, 5, 64, generator=g)
+    w = (1 + 0.1 * torch.randn(64, generator=g)).bfloat16()
+    y, h, r = ops.rmsnorm_fwd_parts(a, part, w, 1e-5)
+    d = _dense(_SplitSum(part))
+    y2, h2, r2 = ops.rmsnorm_fwd(a, w, 1e-5, residual=d)
+    assert torch.equal(h, h2) and torch.equal(y, y2) and torch.equal(r, r2)
+    assert _dense(None) is None and _dense(d) is d

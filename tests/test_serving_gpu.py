@@ -419,3 +419,57 @@ def test_small_batch_decode_graph_replays_the_eager_step():
             le = ee.decode(toks, slots, pos).clone()
             assert torch.nn.functional.cosine_similarity(lg.float().flatten(), le.float().flatten(), dim=0) > 0.999
             toks = le.float().argmax(-1).tolist()
+
+
+@pytest.mark.parametrize("M,K", [(64, 4096), (128, 4096), (128, 14336)])
+def test_rmsnorm_fwd_parts_matches_the_reduce_and_norm(M, K):
+    """The decode projection's K-split partials summed inside the next RMSNorm
+    (ops.rmsnorm_fwd_parts) against the bgemm reduce launch + plain RMSNorm: h bitwise, y and
+    rstd to the last rounding, and y against an fp32 reference of the whole op."""
+    from service_account_auth_improvements_amd import ops
+    g = torch.Generator(device="cpu").manual_seed(M + K)
+    N = 4096
+    x = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) * 0.02).to(DEV, torch.bfloat16)
+    h1 = torch.randn(M, N, generator=g).to(DEV, torch.bfloat16)
+    nw = (1 + 0.1 * torch.randn(N, generator=g)).to(DEV, torch.bfloat16)
+    part = ops.bgemm_parts(x, w)
+    assert part.dim() == 3 and part.shape[1:] == (M, N) and part.shape[0] > 1
+    y0, h0, r0 = ops.rmsnorm_fwd(h1, nw, 1e-5, residual=ops.bgemm(x, w))
+    y1, h1f, r1 = ops.rmsnorm_fwd_parts(h1, part, nw, 1e-5)
+    torch.cuda.synchronize()
+    assert torch.equal(h1f, h0)
+    assert torch.allclose(r1, r0, rtol=1e-6, atol=0)
+    assert (y1.float() - y0.float()).abs().max().item() <= 0.02 * y0.float().abs().max().item()
+    hf = h1.float() + torch.mm(x.float(), w.float().t())
+    ref = hf * torch.rsqrt(hf.pow(2).mean(-1, keepdim=True) + 1e-5) * nw.float()
+    assert ((y1.float() - ref).abs().max() / ref.abs().max()).item() < 2e-2
+
+
+def test_large_batch_decode_with_fused_splits_matches_the_reduce_launches(monkeypatch):
+    """Batch 64 decode (Llama-3-8B shapes, 2 layers): with the wo / wd partials summed in the
+    following RMSNorms the logits equal the reduce-launch step's to rounding, and the fused path
+    is the one that ran."""
+    from service_account_auth_improvements_amd import ops
+    from service_account_auth_improvements_amd.serving import engine as eng
+    e = eng.build_engine("llama3-8b", device=DEV, n_slots=64, max_len=256, n_layers=2, use_graphs=False)
+    g = torch.Generator().manual_seed(5)
+    B = 64
+    for b in range(B):
+        e.prefill(b, torch.randint(0, e.cfg.vocab_size, (16 + b,), generator=g).tolist())
+    toks = [int(t) for t in torch.randint(0, e.cfg.vocab_size, (B,), generator=g)]
+    slots, pos = list(range(B)), [16 + b for b in range(B)]
+    kc0, vc0 = e.kc.clone(), e.vc.clone()
+    calls = []
+    real = ops.bgemm_parts
+    monkeypatch.setattr(ops, "bgemm_parts", lambda x, w: calls.append(x.shape[0]) or real(x, w))
+    monkeypatch.setattr(eng, "FUSE_SPLITS", True)
+    fused = e.decode(toks, slots, pos).float()
+    assert calls and all(m == B for m in calls), calls
+    e.kc.copy_(kc0)
+    e.vc.copy_(vc0)
+    monkeypatch.setattr(eng, "FUSE_SPLITS", False)
+    plain = e.decode(toks, slots, pos).float()
+    cos = torch.nn.functional.cosine_similarity(fused.flatten(), plain.flatten(), dim=0)
+    assert cos > 0.9999, float(cos)
+    assert (fused - plain).abs().max().item() <= 0.02 * plain.abs().max().item()
