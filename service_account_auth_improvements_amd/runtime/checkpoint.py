@@ -637,19 +637,32 @@ class PeriodicCheckpointer:
         self._stream = torch.cuda.Stream(device=self.device) if self.device.type == "cuda" else None
         self._pin = PinnedPieces() if self._stream is not None else None
         # page-locking the host snapshot (112 GB at 8B on one rank) takes seconds: done once, on a
-        # side thread started now (GIL-free, in pieces: PinnedPieces), so the first save() finds
-        # the buffers ready instead of stalling
+        # side thread (GIL-free, in pieces: PinnedPieces), so the first save() finds the buffers
+        # ready instead of stalling.  The thread starts at start_prep(), which the worker calls
+        # once its first step has completed (KFAMD_CKPT_PREPIN=init: at construction; =0: never,
+        # the first save allocates)
         self._prep = None
-        if self._stream is not None and self.flat and os.environ.get("KFAMD_CKPT_PREPIN", "1") != "0":
-            shapes = {k: (tuple(v.shape), v.dtype) for k, v in _flat_state(trainer)[0].items()}
-            self._prep = threading.Thread(target=self._allocate_pinned, args=(shapes,), name="kfamd-ckpt-pin",
-                                          daemon=True)
-            self._prep.start()
+        self._prep_shapes = None
+        mode = os.environ.get("KFAMD_CKPT_PREPIN", "1")
+        if self._stream is not None and self.flat and mode != "0":
+            self._prep_shapes = {k: (tuple(v.shape), v.dtype) for k, v in _flat_state(trainer)[0].items()}
+            if mode == "init":
+                self.start_prep()
         self._thread: Optional[threading.Thread] = None
         self._error: Optional[BaseException] = None
         self.last_published: Optional[int] = None
         self.last_seconds: Optional[float] = None
         self.snapshot_seconds: Optional[float] = None
+
+    def start_prep(self):
+        """Start page-locking the snapshot buffers on a side thread (once).  Pinning tens of GB
+        while the first step was being launched delayed that step by ~1 s (profiles/
+        restart_gpu_r6.md), so the worker starts it after its first step."""
+        if self._prep is None and self._prep_shapes is not None:
+            shapes, self._prep_shapes = self._prep_shapes, None
+            self._prep = threading.Thread(target=self._allocate_pinned, args=(shapes,), name="kfamd-ckpt-pin",
+                                          daemon=True)
+            self._prep.start()
 
     def _host_buffer(self, shape, dtype) -> HostPieces:
         n = 1

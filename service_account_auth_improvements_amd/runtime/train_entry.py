@@ -297,6 +297,8 @@ def _loop(a, tr, data, st, t_start, tokens_per_step):
             if cuda:
                 _device_sync()           # once: the first_step timestamp is a completed step
             _event("first_step", loss=float(rec.loss) if rec.loss is not None else None)
+            if ckpt is not None:
+                ckpt.start_prep()        # page-lock the snapshot buffers now, off the first step
         if pending is not None:
             emit(pending)                # step N-1, while step N runs on the device
             prev = pending
