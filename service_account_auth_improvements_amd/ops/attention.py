@@ -127,6 +127,20 @@ def rope_append_(qkv, Hq, cos_t, sin_t, slots, pos, k_cache, v_cache):
     kv_append_(qkv, Hq, slots, pos, k_cache, v_cache)
 
 
+def rope_append_parts(part, Hq, cos_t, sin_t, slots, pos, k_cache, v_cache):
+    """:func:`rope_append_` on the qkv projection's fp32 K-split partials [S, B, N]
+    (``ops.bgemm_parts``): the partials are summed and rounded to bf16 in the same launch.
+    Returns the rotated qkv rows [B, N]."""
+    if part.is_cuda:
+        return _ext.ops().rope_append_parts(part, Hq, cos_t, sin_t, slots, pos, k_cache, v_cache)
+    d = part[0].clone()
+    for t in range(1, part.shape[0]):
+        d += part[t]
+    qkv = d.to(k_cache.dtype)
+    rope_append_(qkv, Hq, cos_t, sin_t, slots, pos, k_cache, v_cache)
+    return qkv
+
+
 def kv_fill_(qkv, S, Hq, slot, k_cache, v_cache):
     """Prefill: rows [0, S) of one sequence's fused qkv -> positions [0, S) of `slot`."""
     if qkv.is_cuda:

@@ -45,6 +45,8 @@ int kf_decode_attn_fused(const void*, long, const void*, const void*, const int*
                          float*, int*, int, int, int, int, int, int, float, hipStream_t);
 int kf_decode_attn(const void*, long, const void*, const void*, const int*, const int*, void*, long,
                    float*, float*, int, int, int, int, int, int, float, hipStream_t);
+int kf_rope_append_parts(const float*, int, void*, int, int, int, int, const float*, const float*, const int*,
+                         const int*, void*, void*, int, hipStream_t);
 int kf_rope_append(void*, long, int, int, int, int, const float*, const float*, const int*, const int*, void*,
                    void*, int, hipStream_t);
 int kf_kv_append(const void*, long, int, int, int, int, const int*, const int*, void*, void*, int,
@@ -443,6 +445,29 @@ void rope_append_(at::Tensor& qkv, int64_t Hq, const at::Tensor& cos_t, const at
            "rope_append");
 }
 
+// rope_append_ on the qkv projection's fp32 K-split partials [S, B, (Hq + 2 Hkv) * D] (bgemm_parts):
+// the reduce launch folded in.  Returns the rotated bf16 qkv rows.
+at::Tensor rope_append_parts(const at::Tensor& part, int64_t Hq, const at::Tensor& cos_t, const at::Tensor& sin_t,
+                             const at::Tensor& slots, const at::Tensor& pos, at::Tensor& kc, at::Tensor& vc) {
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous() && part.dim() == 3,
+              "rope_append_parts: fp32 [S, B, N] partials");
+  const int64_t B = part.size(1), Hkv = kc.size(1), D = kc.size(3);
+  check_cache(kc, vc, Hkv, D);
+  TORCH_CHECK(part.size(2) == (Hq + 2 * Hkv) * D, "rope_append_parts: row width");
+  TORCH_CHECK(cos_t.scalar_type() == at::kFloat && sin_t.scalar_type() == at::kFloat && cos_t.is_contiguous() &&
+                  sin_t.is_contiguous() && cos_t.size(-1) == D / 2 && cos_t.size(0) >= kc.size(2),
+              "rope_append_parts: cos/sin tables must be fp32 [>=Lmax, D/2]");
+  check_rows_i32(slots, B, "slots");
+  check_rows_i32(pos, B, "pos");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(part.device());
+  auto qkv = at::empty({B, part.size(2)}, kc.options());
+  check_rc(kf_rope_append_parts(part.data_ptr<float>(), (int)part.size(0), qkv.data_ptr(), (int)B, (int)Hq, (int)Hkv,
+                                (int)D, cos_t.data_ptr<float>(), sin_t.data_ptr<float>(), slots.data_ptr<int>(),
+                                pos.data_ptr<int>(), kc.data_ptr(), vc.data_ptr(), (int)kc.size(2), cur_stream()),
+           "rope_append_parts");
+  return qkv;
+}
+
 // Decode qkv projection, fused: h = x (+ res); qkv = (rmsnorm(h) * nw) . w^T; RoPE at pos[b] on
 // the q/k heads; rotated k and v appended to the cache at (slots[b], pos[b]).  Returns (qkv, h);
 // == skinny_gemm_norm + rope_append_ bit for bit.  1 <= B <= 4 rows, head dim 128.
@@ -792,6 +817,7 @@ TORCH_LIBRARY(kfamd, m) {
   m.def("rmsnorm_fwd", &rmsnorm_fwd);
   m.def("rmsnorm_fwd_parts", &rmsnorm_fwd_parts);
   m.def("bgemm_parts", &bgemm_parts);
+  m.def("rope_append_parts", &rope_append_parts);
   m.def("rmsnorm_bwd", &rmsnorm_bwd);
   m.def("rope_", &rope_);
   m.def("swiglu_fwd", &swiglu_fwd);

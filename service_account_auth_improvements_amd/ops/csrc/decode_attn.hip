@@ -644,6 +644,87 @@ __global__ void rope_append_kernel(bf16_t* __restrict__ qkv, long ld, int Hq, in
   }
 }
 
+// rope_append_kernel fed by the fp32 K-split partials [S, B, (Hq + 2 Hkv) * D] of the qkv
+// batched-decode GEMM (its reduce launch skipped): each thread sums its 8 + 8 elements in slice
+// order, rounds them to bf16 exactly as bgemm_reduce_kernel does, writes the qkv row (rotated q
+// and k, v as is) and appends k / v to the cache -- the same values as reduce + rope_append.
+template <int S>
+__global__ void rope_append_parts_kernel(const float* __restrict__ part, bf16_t* __restrict__ qkv, int Hq, int Hkv,
+                                         const float* __restrict__ cos_t, const float* __restrict__ sin_t,
+                                         const int* __restrict__ slots, const int* __restrict__ pos,
+                                         bf16_t* __restrict__ kc, bf16_t* __restrict__ vc, int Lmax, int B) {
+  constexpr int HALF = D / 2, CPH = HALF / 8;
+  const int it = blockIdx.x * blockDim.x + threadIdx.x;
+  const int per_row = (Hq + 2 * Hkv) * CPH, N = (Hq + 2 * Hkv) * D;
+  if (it >= B * per_row) return;
+  const int b = it / per_row, rem = it % per_row, h = rem / CPH, c = rem % CPH;
+  const long off = (long)b * N + (long)h * D + c * 8;
+  const long pstride = (long)B * N;
+  f32x4 v[S][4];
+#pragma unroll
+  for (int t = 0; t < S; ++t) {
+    v[t][0] = ldf4(part + t * pstride + off);
+    v[t][1] = ldf4(part + t * pstride + off + 4);
+    v[t][2] = ldf4(part + t * pstride + off + HALF);
+    v[t][3] = ldf4(part + t * pstride + off + HALF + 4);
+  }
+  f32x4 sl0 = f32x4{0.f, 0.f, 0.f, 0.f}, sl1 = sl0, sh0 = sl0, sh1 = sl0;
+#pragma unroll
+  for (int t = 0; t < S; ++t) {
+    sl0 += v[t][0];
+    sl1 += v[t][1];
+    sh0 += v[t][2];
+    sh1 += v[t][3];
+  }
+  u32x4 lo = u32x4{pack2(sl0[0], sl0[1]), pack2(sl0[2], sl0[3]), pack2(sl1[0], sl1[1]), pack2(sl1[2], sl1[3])};
+  u32x4 hi = u32x4{pack2(sh0[0], sh0[1]), pack2(sh0[2], sh0[3]), pack2(sh1[0], sh1[1]), pack2(sh1[2], sh1[3])};
+  const int p = pos[b];
+  const bool is_v = h >= Hq + Hkv;
+  if (!is_v) {
+    float a[8], bb[8], o1[8], o2[8];
+    unpack8(lo, a);
+    unpack8(hi, bb);
+    const float* pc = cos_t + (long)p * HALF + c * 8;
+    const float* ps = sin_t + (long)p * HALF + c * 8;
+    const f32x4 c0 = ldf4(pc), c1 = ldf4(pc + 4), s0 = ldf4(ps), s1 = ldf4(ps + 4);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float cc = j < 4 ? c0[j] : c1[j - 4], ss = j < 4 ? s0[j] : s1[j - 4];
+      o1[j] = a[j] * cc - bb[j] * ss;
+      o2[j] = bb[j] * cc + a[j] * ss;
+    }
+    lo = pack8(o1);
+    hi = pack8(o2);
+  }
+  bf16_t* px = qkv + off;
+  st16(px, lo);
+  st16(px + HALF, hi);
+  if (h >= Hq) {
+    const int kh = is_v ? h - Hq - Hkv : h - Hq;
+    bf16_t* dst = (is_v ? vc : kc) + (((long)slots[b] * Hkv + kh) * Lmax + p) * D + c * 8;
+    st16(dst, lo);
+    st16(dst + HALF, hi);
+  }
+}
+
+extern "C" int kf_rope_append_parts(const float* part, int S, void* qkv, int B, int Hq, int Hkv, int Dh,
+                                    const float* cos_t, const float* sin_t, const int* slots, const int* pos, void* kc,
+                                    void* vc, int Lmax, hipStream_t st) {
+  if (Dh != D || B < 1) return 1;
+  const int threads = B * (Hq + 2 * Hkv) * (D / 16);
+  const dim3 grid(cdiv(threads, 256));
+#define RA_PARTS(SV)                                                                                            \
+  hipLaunchKernelGGL(rope_append_parts_kernel<SV>, grid, dim3(256), 0, st, part, (bf16_t*)qkv, Hq, Hkv, cos_t, sin_t, \
+                     slots, pos, (bf16_t*)kc, (bf16_t*)vc, Lmax, B)
+  if (S == 2) RA_PARTS(2);
+  else if (S == 4) RA_PARTS(4);
+  else if (S == 8) RA_PARTS(8);
+  else return 1;
+#undef RA_PARTS
+  KF_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int kf_rope_append(void* qkv, long ld, int B, int Hq, int Hkv, int Dh, const float* cos_t,
                               const float* sin_t, const int* slots, const int* pos, void* kc, void* vc, int Lmax,
                               hipStream_t st) {

@@ -39,7 +39,7 @@ import torch.distributed as dist
 
 from .. import ops
 from ..models.llama import Llama, LlamaConfig
-from ..ops.attention import attention_fwd, decode_attention, kv_fill_, rope_append_
+from ..ops.attention import attention_fwd, decode_attention, kv_fill_, rope_append_, rope_append_parts
 from ..parallel.state import ParallelState, tp_all_reduce
 
 BUCKETS = (1, 2, 4, 8, 16, 32, 64, 128, 256)
@@ -251,6 +251,16 @@ class Engine:
             return _SplitSum(y) if y.dim() == 3 else y
         return self._tp_ar(self._mm(x, w))
 
+    def _qkv_parts(self, a, w):
+        """The qkv projection at 33-128 rows: the batched-decode GEMM's fp32 partials for
+        rope_append_parts (its K split's reduce folded into that launch), else the bf16 product.
+        Unfused, hipBLASLt ties the batched-decode GEMM here (profiles/serve_bgemm.md)."""
+        rows = a.shape[0]
+        if (FUSE_SPLITS and a.is_cuda and BGEMM and self.m.tp == 1 and BGEMM_MIN_ROWS <= rows <= BGEMM_MAX_ROWS
+                and ops.bgemm_ok(a, w)):
+            return ops.bgemm_parts(a, w)
+        return self._mm(a, w)
+
     def _norm(self, x, w, d):
         """Residual add + RMSNorm; ``d`` may be a projection's unreduced partials."""
         if isinstance(d, _SplitSum):
@@ -288,8 +298,11 @@ class Engine:
                     qkv, h1 = ops.skinny_gemm_norm(r, _dense(d), m.P(f"l{i}.norm1"), cfg.norm_eps, wqkv)
                 else:
                     a, h1, _ = self._norm(r, m.P(f"l{i}.norm1"), d)
-                    qkv = self._mm(a, wqkv)
-                rope_append_(qkv, m.hq, m.cos, m.sin, slots, pos, self.kc[li], self.vc[li])
+                    qkv = self._qkv_parts(a, wqkv)
+                if qkv.dim() == 3:      # K-split partials: summed inside the RoPE / append launch
+                    qkv = rope_append_parts(qkv, m.hq, m.cos, m.sin, slots, pos, self.kc[li], self.vc[li])
+                else:
+                    rope_append_(qkv, m.hq, m.cos, m.sin, slots, pos, self.kc[li], self.vc[li])
             o = decode_attention(qkv, self.kc[li], self.vc[li], slots, lengths, m.hq)
             da = self._mm_res(o, m.P(f"l{i}.wo"))
             r, d = self._decode_mlp(i, h1, da)

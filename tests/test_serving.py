@@ -273,3 +273,22 @@ def test_split_partials_norm_reference_equals_reduce_then_norm():
     y2, h2, r2 = ops.rmsnorm_fwd(a, w, 1e-5, residual=d)
     assert torch.equal(h, h2) and torch.equal(y, y2) and torch.equal(r, r2)
     assert _dense(None) is None and _dense(d) is d
+
+
+def test_rope_append_parts_reference_equals_reduce_then_rope_append():
+    """CPU reference of rope_append_parts (the decode engine's qkv reduce-in-RoPE path)."""
+    from service_account_auth_improvements_amd.ops import reference
+    from service_account_auth_improvements_amd.ops.attention import rope_append_, rope_append_parts
+    g = torch.Generator().manual_seed(4)
+    Hq, Hkv, L = 4, 2, 16
+    part = torch.randn(2, 3, (Hq + 2 * Hkv) * 128, generator=g)
+    cos, sin = reference.rope_tables(L, 128)
+    slots = torch.tensor([2, 0, 1], dtype=torch.int32)
+    pos = torch.tensor([0, 5, 15], dtype=torch.int32)
+    kc = torch.zeros(3, Hkv, L, 128, dtype=torch.bfloat16)
+    vc = torch.zeros_like(kc)
+    kc2, vc2 = kc.clone(), vc.clone()
+    got = rope_append_parts(part, Hq, cos, sin, slots, pos, kc, vc)
+    ref = (part[0] + part[1]).to(torch.bfloat16)
+    rope_append_(ref, Hq, cos, sin, slots, pos, kc2, vc2)
+    assert torch.equal(got, ref) and torch.equal(kc, kc2) and torch.equal(vc, vc2)

@@ -473,3 +473,29 @@ def test_large_batch_decode_with_fused_splits_matches_the_reduce_launches(monkey
     cos = torch.nn.functional.cosine_similarity(fused.flatten(), plain.flatten(), dim=0)
     assert cos > 0.9999, float(cos)
     assert (fused - plain).abs().max().item() <= 0.02 * plain.abs().max().item()
+
+
+@pytest.mark.parametrize("M", [64, 128])
+def test_rope_append_parts_matches_reduce_then_rope_append(M):
+    """The qkv projection's K-split partials summed inside the RoPE / KV-append launch: qkv rows
+    and both caches bitwise equal to bgemm's reduce launch followed by rope_append_."""
+    from service_account_auth_improvements_amd import ops
+    from service_account_auth_improvements_amd.ops.attention import rope_append_, rope_append_parts
+    from service_account_auth_improvements_amd.ops import reference
+    g = torch.Generator(device="cpu").manual_seed(M)
+    Hq, Hkv, D, K, L = 32, 8, 128, 4096, 64
+    x = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+    w = (torch.randn((Hq + 2 * Hkv) * D, K, generator=g) * 0.02).to(DEV, torch.bfloat16)
+    cos, sin = (t.to(DEV) for t in reference.rope_tables(L, D))
+    slots = torch.randperm(M, generator=g).to(DEV, torch.int32)
+    pos = torch.randint(0, L, (M,), generator=g).to(DEV, torch.int32)
+    kc = torch.zeros(M, Hkv, L, D, device=DEV, dtype=torch.bfloat16)
+    vc = torch.zeros_like(kc)
+    kc2, vc2 = kc.clone(), vc.clone()
+    part = ops.bgemm_parts(x, w)
+    assert part.dim() == 3
+    got = rope_append_parts(part, Hq, cos, sin, slots, pos, kc, vc)
+    ref = ops.bgemm(x, w)
+    rope_append_(ref, Hq, cos, sin, slots, pos, kc2, vc2)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref) and torch.equal(kc, kc2) and torch.equal(vc, vc2)
