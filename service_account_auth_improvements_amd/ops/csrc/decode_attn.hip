@@ -602,6 +602,12 @@ extern "C" int kf_decode_attn(const void* q, long q_ld, const void* kc, const vo
   return 0;
 }
 
+// The rotation of one RoPE pair with the rounding pinned down (explicit fma, the other product
+// rounded on its own): hipcc contracts `a * c - b * s` differently from kernel to kernel, and the
+// decode kernels that rotate (rope_append, rope_append_parts, gemv_norm_rope) must agree bit for bit
+__device__ __forceinline__ float rope_lo(float a, float b, float c, float s) { return __builtin_fmaf(a, c, -(b * s)); }
+__device__ __forceinline__ float rope_hi(float b, float a, float c, float s) { return __builtin_fmaf(b, c, a * s); }
+
 // Decode step prologue fused into one launch: RoPE (half-split, fp32 tables) in place on the
 // q and k heads of each fused qkv row at position pos[b], and the rotated k plus v appended
 // to the cache at pos[b] of slot slots[b].  One thread per 8 rotation pairs.
@@ -628,8 +634,8 @@ __global__ void rope_append_kernel(bf16_t* __restrict__ qkv, long ld, int Hq, in
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float cc = j < 4 ? c0[j] : c1[j - 4], ss = j < 4 ? s0[j] : s1[j - 4];
-      o1[j] = a[j] * cc - bb[j] * ss;
-      o2[j] = bb[j] * cc + a[j] * ss;
+      o1[j] = rope_lo(a[j], bb[j], cc, ss);
+      o2[j] = rope_hi(bb[j], a[j], cc, ss);
     }
     lo = pack8(o1);
     hi = pack8(o2);
@@ -690,8 +696,8 @@ __global__ void rope_append_parts_kernel(const float* __restrict__ part, bf16_t*
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float cc = j < 4 ? c0[j] : c1[j - 4], ss = j < 4 ? s0[j] : s1[j - 4];
-      o1[j] = a[j] * cc - bb[j] * ss;
-      o2[j] = bb[j] * cc + a[j] * ss;
+      o1[j] = rope_lo(a[j], bb[j], cc, ss);
+      o2[j] = rope_hi(bb[j], a[j], cc, ss);
     }
     lo = pack8(o1);
     hi = pack8(o2);

@@ -301,7 +301,7 @@ __global__ __launch_bounds__(64 * WV) void gemv_kernel(const bf16_t* __restrict_
         float v = bf2f(f2bf(g));
         if (head < ra.hq + ra.hkv) {
           const float o = bf2f(f2bf(u)), c = ep_cos, sn = ep_sin;
-          v = d < 64 ? v * c - o * sn : v * c + o * sn;
+          v = d < 64 ? __builtin_fmaf(v, c, -(o * sn)) : __builtin_fmaf(v, c, o * sn);   // == rope_lo / rope_hi
         }
         const bf16_t vb = f2bf(v);
         y[(long)m * ldy + row] = vb;
