@@ -61,6 +61,7 @@ FUSE_SPLITS = os.environ.get("KFAMD_DECODE_FUSE_SPLITS", "1") != "0"
 # ... and the qkv projection on the batched-decode GEMM with its partials summed inside the RoPE /
 # KV-append launch (KFAMD_DECODE_FUSE_QKV=0: hipBLASLt + rope_append_)
 FUSE_QKV = os.environ.get("KFAMD_DECODE_FUSE_QKV", "1") != "0"
+QKV_PARTS_MIN_ROWS = 65       # at 64 rows hipBLASLt's qkv GEMM is faster than this pair (+1 %, s18)
 # prompts admitted in one scheduler iteration are prefilled together up to this many tokens
 PREFILL_MAX_TOKENS = int(os.environ.get("KFAMD_PREFILL_MAX_TOKENS", "16384"))
 PREFILL_PAD_RATIO = 1.25      # ... in length groups padded to at most 1.25x
@@ -255,12 +256,12 @@ class Engine:
         return self._tp_ar(self._mm(x, w))
 
     def _qkv_parts(self, a, w):
-        """The qkv projection at 33-128 rows: the batched-decode GEMM's fp32 partials for
+        """The qkv projection at 65-128 rows: the batched-decode GEMM's fp32 partials for
         rope_append_parts (its K split's reduce folded into that launch), else the bf16 product.
         Unfused, hipBLASLt ties the batched-decode GEMM here (profiles/serve_bgemm.md)."""
         rows = a.shape[0]
-        if (FUSE_SPLITS and FUSE_QKV and a.is_cuda and BGEMM and self.m.tp == 1 and BGEMM_MIN_ROWS <= rows <= BGEMM_MAX_ROWS
-                and ops.bgemm_ok(a, w)):
+        if (FUSE_SPLITS and FUSE_QKV and a.is_cuda and BGEMM and self.m.tp == 1
+                and QKV_PARTS_MIN_ROWS <= rows <= BGEMM_MAX_ROWS and ops.bgemm_ok(a, w)):
             return ops.bgemm_parts(a, w)
         return self._mm(a, w)
 
