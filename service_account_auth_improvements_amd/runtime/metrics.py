@@ -14,7 +14,7 @@ serves
   hip_memory_peak_allocated_bytes                                gauges (the HIP caching allocator)
   train_collective_{calls,bytes,seconds}_total{op}               counters (parallel/ddp.CollectiveStats)
   train_collective_bus_bandwidth_bytes_per_second{op}           gauge: cumulative bytes x bus factor / seconds
-  train_checkpoint_last_step / train_checkpoint_save_seconds    gauges (runtime/ckpt_async.py)
+  train_checkpoint_last_step / train_checkpoint_save_seconds    gauges (runtime/checkpoint.PeriodicCheckpointer)
 
 Every value is fed by the worker loop ONE STEP LATE from data that is already on the host
 (the previous step's end event, its pinned loss copy): nothing here synchronises the device.
@@ -56,6 +56,7 @@ class TrainMetrics:
                              registry=r)
         self._seen = {}              # op -> [calls, bytes, seconds, timed bytes] already exported
         self._server = None
+        self.port = None
         if port is not None and port >= 0:
             from prometheus_client import start_http_server
             res = start_http_server(port, addr=addr, registry=r)
