@@ -214,7 +214,7 @@ def main():
                          "rows, reduce-scatter + all-gather in place of the TP all-reduces")
     ap.add_argument("--recompute", action="store_true",
                     help="per-layer activation recomputation (memory plans that need it, e.g. 70B at long S)")
-    ap.add_argument("--head-chunk", type=int, default=4096,
+    ap.add_argument("--head-chunk", type=int, default=int(os.environ.get("KFAMD_HEAD_CHUNK", "4096")),
                     help="LM head + cross-entropy row chunk in tokens (0 = materialise all logits)")
     ap.add_argument("--force-collectives", action="store_true",
                     help="REHEARSAL: run the DP collectives (ZeRO-1 / fp32 reduction) on a one-rank RCCL "
