@@ -56,6 +56,25 @@ def test_async_optimizer_is_bit_identical():
     assert torch.equal(out[0][1], out[1][1]) and torch.equal(out[0][2], out[1][2])
 
 
+def test_training_is_bitwise_reproducible_run_to_run_at_long_sequence():
+    """Two runs of the same training job (Llama-3-8B widths, 2 layers, S 4096: several query
+    chunks per dK/dV key block) produce bit-identical losses and parameters -- what bitwise
+    checkpoint-restart rests on (the attention backward's deterministic slots are the default;
+    profiles/restart_gpu_r6.md)."""
+    out = []
+    for _ in range(2):
+        st = ParallelState(device=torch.device("cuda", 0))
+        tr = Trainer(TrainConfig(model="llama3-8b", seq_len=4096, micro_batch=1, n_layers=2, lr=1e-4), st)
+        data = SyntheticData(tr.mcfg.vocab_size, 1, 4096, "cuda:0", seed=9)
+        losses = [float(tr.train_step([data.next()])) for _ in range(3)]
+        tr.sync_params()
+        out.append((losses, tr.model.mats.params.clone(), tr.model.norms.params.clone()))
+        del tr
+        torch.cuda.empty_cache()
+    assert out[0][0] == out[1][0], (out[0][0], out[1][0])
+    assert torch.equal(out[0][1], out[1][1]) and torch.equal(out[0][2], out[1][2])
+
+
 def test_activation_recompute_bit_identical_gpu():
     """Per-layer recomputation on the GPU kernels: same loss, gradients and parameters."""
     out = []
