@@ -99,8 +99,11 @@ def _hip_preinit(device_arg: str):
     counts devices, selects this rank's (LOCAL_RANK modulo the count, as
     parallel/state.local_device_index) and creates its context with ``hipFree(NULL)``.
     ``KFAMD_HIP_PREINIT=0`` or ``--device cpu`` turns it off; any failure leaves the work to
-    torch's own lazy init."""
-    if device_arg == "cpu" or os.environ.get("KFAMD_HIP_PREINIT", "1") == "0":
+    torch's own lazy init.  ``KFAMD_HIP_PREINIT=after-c`` starts the device work only once the
+    import has loaded ``torch._C`` (its native libraries, the HIP runtime among them), so the
+    runtime init overlaps the Python part of the import but not its dynamic loading."""
+    mode = os.environ.get("KFAMD_HIP_PREINIT", "1")
+    if device_arg == "cpu" or mode == "0":
         return None
     import ctypes
     import importlib.util
@@ -114,6 +117,12 @@ def _hip_preinit(device_arg: str):
 
     def run():
         try:
+            if mode == "after-c":
+                import sys
+                import time as _t
+                deadline = _t.monotonic() + 30.0
+                while "torch._C" not in sys.modules and _t.monotonic() < deadline:
+                    _t.sleep(0.005)
             h = ctypes.CDLL(lib, mode=ctypes.RTLD_GLOBAL)
             n = ctypes.c_int(0)
             if h.hipGetDeviceCount(ctypes.byref(n)) != 0 or n.value < 1:
