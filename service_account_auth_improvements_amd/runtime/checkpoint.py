@@ -648,6 +648,14 @@ class PeriodicCheckpointer:
             self._prep_shapes = {k: (tuple(v.shape), v.dtype) for k, v in _flat_state(trainer)[0].items()}
             if mode == "init":
                 self.start_prep()
+        # device staging: when the card has room for a second copy of the state beside the step's
+        # peak, the snapshot is a device-to-device copy (~3 TB/s) that the next optimizer update
+        # waits for, and the device-to-host copy (~56 GB/s) runs from that copy while the
+        # following steps proceed.  Decided at the first save (the peak is known by then);
+        # KFAMD_CKPT_DEVICE_STAGE=0 turns it off.
+        self._stage: Optional[Dict[str, torch.Tensor]] = None
+        self._stage_decided = self._stream is None or os.environ.get("KFAMD_CKPT_DEVICE_STAGE", "1") == "0"
+        self.staged = False
         self._thread: Optional[threading.Thread] = None
         self._error: Optional[BaseException] = None
         self.last_published: Optional[int] = None
@@ -675,6 +683,17 @@ class PeriodicCheckpointer:
             self._pinned[k] = self._host_buffer(shape, dtype)
 
     # -- snapshot (caller's thread)
+    STAGE_MARGIN = 8 << 30          # HBM left free beside the step's peak and the staging copy
+
+    def _decide_stage(self, tensors: Dict[str, torch.Tensor]):
+        self._stage_decided = True
+        need = sum(t.numel() * t.element_size() for t in tensors.values())
+        total = torch.cuda.get_device_properties(self.device).total_memory
+        peak = torch.cuda.max_memory_allocated(self.device)
+        if peak + need + self.STAGE_MARGIN <= total:
+            self._stage = {k: torch.empty_like(v) for k, v in tensors.items()}
+            self.staged = True
+
     def _host_copy(self, key: str, t: torch.Tensor):
         if self._stream is None:
             return t.detach().contiguous().clone()
@@ -712,18 +731,29 @@ class PeriodicCheckpointer:
         host = {}
         ev = None
         if self._stream is not None:
+            if not self._stage_decided:
+                self._decide_stage(tensors)
             self._stream.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(self._stream):
-                for k, v in tensors.items():
+                src = tensors
+                if self._stage is not None:
+                    for k, v in tensors.items():
+                        self._stage[k].copy_(v, non_blocking=True)
+                    src = self._stage
+                ev_state = torch.cuda.Event()
+                ev_state.record(self._stream)      # the state has been read (into the staging copy)
+                for k, v in src.items():
                     host[k] = self._host_copy(k, v)
             ev = torch.cuda.Event()
-            ev.record(self._stream)
-            # the next optimizer update rewrites master / m / v / params: it waits for the copy
+            ev.record(self._stream)                # ... and is on the host
+            # the next optimizer update rewrites master / m / v / params: it waits for the state
+            # to have been read -- the device copy when staged, else the host copy
+            gate = ev_state if self._stage is not None else ev
             waits = getattr(tr, "pre_opt_waits", None)
             if waits is not None:
-                waits.append(ev)
+                waits.append(gate)
             else:
-                ev.synchronize()
+                gate.synchronize()
         else:
             host = {k: self._host_copy(k, v) for k, v in tensors.items()}
         self.snapshot_seconds = time.perf_counter() - t0
@@ -809,4 +839,5 @@ class PeriodicCheckpointer:
             if self._stream is not None:
                 self._stream.synchronize()
             self._pinned = {}
+            self._stage = None
             self._pin.free()

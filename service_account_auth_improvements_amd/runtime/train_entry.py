@@ -315,7 +315,7 @@ def _loop(a, tr, data, st, t_start, tokens_per_step):
         _heartbeat()
         if ckpt is not None and (step + 1) % a.save_every == 0 and step + 1 < end:
             ckpt.save(step + 1)
-            _event("checkpoint_queued", step=step + 1)
+            _event("checkpoint_queued", step=step + 1, device_staged=ckpt.staged)
     if pending is not None:
         emit(pending)
     if ckpt is not None:
